@@ -1,0 +1,160 @@
+/*
+ * ofdis.h -- C-ABI of the MI355X-native DIS optical-flow / stereo-depth hot path.
+ *
+ * This is the drop-in boundary for lordnn/OF_DIS.  Every entry point below names the
+ * reference interface it replaces (paths relative to the reference tree).  Plain C types
+ * only: no torch, no HIP types in any signature (device pointers and streams are void*).
+ *
+ * Library: of_dis_amd/libofdis.so (built by of_dis_amd/csrc/Makefile, hipcc --offload-arch=gfx950).
+ */
+#ifndef OFDIS_H
+#define OFDIS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFDIS_ABI_VERSION 1
+
+/* Status codes.  The reference has no error channel (it exit(1)s on OOM, FDF1.0.1/image.cpp:26-27,
+ * and never validates parameters); every entry point here returns one of these instead. */
+typedef enum ofdis_status {
+  OFDIS_OK = 0,
+  OFDIS_ERR_INVALID_ARGUMENT = 1, /* bad pointer / size / parameter combination          */
+  OFDIS_ERR_UNSUPPORTED = 2,      /* valid in the reference but not implemented here       */
+  OFDIS_ERR_OUT_OF_MEMORY = 3,    /* device or host allocation failed                      */
+  OFDIS_ERR_DEVICE = 4,           /* a HIP runtime call failed                             */
+  OFDIS_ERR_NO_DEVICE = 5,        /* no gfx950 device visible                              */
+  OFDIS_ERR_IO = 6                /* file could not be opened / read / written             */
+} ofdis_status;
+
+/* SELECTMODE of the reference build (CMakeLists.txt:36-61): 1 = optical flow, 2 = stereo depth. */
+enum { OFDIS_MODE_OF = 1, OFDIS_MODE_DE = 2 };
+
+/*
+ * Parameters of one run.  Mirrors OFC::optparam's explicitly-set fields (oflow.h:45-66) plus
+ * the two compile-time switches SELECTMODE / SELECTCHANNEL, which are runtime fields here.
+ * Values are taken exactly as the reference constructor receives them (oflow.cpp:80-104):
+ * dp_thresh is NOT squared by the caller, steps/outlier threshold/novals are derived.
+ */
+typedef struct ofdis_params {
+  int mode;         /* OFDIS_MODE_OF (nop = 2) or OFDIS_MODE_DE (nop = 1)                 */
+  int noc;          /* channels: 1 = intensity, 3 = BGR interleaved (SELECTCHANNEL 1 / 3)  */
+  int sc_f;         /* coarsest scale                                                     */
+  int sc_l;         /* finest scale                                                       */
+  int max_iter;     /* patch iterations                                                   */
+  int min_iter;
+  float dp_thresh;  /* early-stop on |delta_p| ratio (squared internally, oflow.cpp:87)    */
+  float dr_thresh;  /* early-stop on residual ratio                                        */
+  float res_thresh; /* early-stop on mean absolute residual                                */
+  int p_samp_s;     /* patch edge length (even)                                            */
+  float patove;     /* patch overlap in [0,1)                                              */
+  int usefbcon;     /* forward-backward merging (patchgrid.cpp:277-375)                    */
+  int costfct;      /* 0 L2, 1 L1, 2 pseudo-Huber (10 = NCC is unimplemented upstream)     */
+  int patnorm;      /* mean-normalise patches                                              */
+  int usetvref;     /* variational refinement                                              */
+  float tv_alpha, tv_gamma, tv_delta;
+  int tv_innerit;   /* TV outer iterations per level = tv_innerit * (level + 1)            */
+  int tv_solverit;  /* SOR sweeps per TV iteration                                         */
+  float tv_sor;     /* SOR relaxation omega                                                */
+  int verbosity;    /* 0 silent, 1 total time, 2 per-scale TIME lines (oflow.cpp:297,336)  */
+} ofdis_params;
+
+/* ------------------------------------------------------------------ parameters */
+
+int ofdis_abi_version(void);
+const char *ofdis_status_string(int status);
+
+/* AutoFirstScaleSelect (run_dense.cpp:181-184). */
+int ofdis_auto_first_scale(int imgwidth, int fratio, int patchsize);
+
+/* Operating points 1-4 with automatic coarsest scale (run_dense.cpp:226-268). */
+int ofdis_params_oppoint(ofdis_params *p, int oppoint, int width_org, int mode, int noc);
+
+/* The 20 explicit positional parameters of run_dense.cpp:270-295, as strings (argv[4..23]). */
+int ofdis_params_from_strings(ofdis_params *p, int count, const char *const *values, int mode, int noc);
+
+/* Validation the reference never does: p even and >= 2, p*p*noc divisible by 4 (patch.cpp:230),
+ * 0 <= sc_l <= sc_f, width/height divisible by 2^sc_f, costfct in {0,1,2}, noc in {1,3}. */
+int ofdis_params_validate(const ofdis_params *p, int width, int height, int imgpadding);
+
+/* ------------------------------------------------------------------ library boundary */
+
+/*
+ * OFC::OFClass::OFClass (oflow.h:99-126, oflow.cpp:31-338) with host pointers.
+ * im_ao[s] .. im_bo_dy[s] for s in [sc_l, sc_f]: padded (w_s + 2*imgpadding) x (h_s + 2*imgpadding)
+ * x noc float arrays (images replicate-padded, gradients zero-padded); entries below sc_l may be NULL.
+ * outflow: (width >> sc_l) * (height >> sc_l) * nop floats, interleaved.  initflow: NULL or
+ * (width >> (sc_f+1)) * (height >> (sc_f+1)) * nop floats.  Runs on the default device; blocking.
+ */
+int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx, const float *const *im_ao_dy,
+                        const float *const *im_bo, const float *const *im_bo_dx, const float *const *im_bo_dy,
+                        int imgpadding, float *outflow, const float *initflow, int width, int height,
+                        const ofdis_params *p);
+
+/* ------------------------------------------------------------------ batched device path */
+
+typedef struct ofdis_context ofdis_context;
+
+/* One context per GPU (and per host thread using it).  No hidden globals. */
+int ofdis_context_create(int device, ofdis_context **out);
+void ofdis_context_destroy(ofdis_context *ctx);
+
+/*
+ * Whole run_dense.cpp main() hot path for a batch of n independent frame pairs, all on device:
+ * divisibility padding (run_dense.cpp:299-312) -> pyramid + Sobel gradients (:131-179) ->
+ * OFClass (:392-401) -> x 2^sc_l + INTER_LINEAR upsample + crop (:407-415).
+ * img_a/img_b: device u8 [n][height][width][noc] (BGR order when noc = 3).
+ * flow_out: device float [n][height][width][nop] (nop = 2 OF, 1 DE).
+ * stream: hipStream_t (NULL = the context's own stream).  Asynchronous w.r.t. the host.
+ */
+int ofdis_run_batch_u8(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
+                       int height, const ofdis_params *p, float *flow_out, void *stream);
+
+/* Same with host buffers (CLI path; synchronous). */
+int ofdis_run_batch_u8_host(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
+                            int height, const ofdis_params *p, float *flow_out);
+
+/* Device pyramid only (run_dense.cpp:131-179 + :299-312): writes, for each level s in [sc_l, sc_f],
+ * padded image/dx/dy of frame 0 to host arrays (same layout as ofdis_oflow_compute's inputs). */
+int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int height, const ofdis_params *p,
+                          int imgpadding, float *const *img_pyr, float *const *dx_pyr, float *const *dy_pyr);
+
+/* Per-stage capture for parity tests: when set, the next run copies frame 0's flow at scale s after
+ * patch aggregation (dis_flow[s]) and after variational refinement (tv_flow[s]), each
+ * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL). */
+int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, float *const *tv_flow, int nscales);
+
+/* HIP-event timing of individual kernels on the launch stream (used by bench.py for the roofline). */
+int ofdis_context_enable_kernel_timing(ofdis_context *ctx, int enable);
+/* Accumulated device time (ms) and launch count for kernel `name` since timing was enabled. */
+int ofdis_context_kernel_time(ofdis_context *ctx, const char *name, double *total_ms, long *launches);
+/* Comma-separated list of kernel names known to the timer. */
+const char *ofdis_kernel_names(void);
+
+/* Per-frame algorithmic byte counts of the §8(d) byte model for this workload. */
+int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const char *kernel, double *bytes_per_frame);
+
+/* ------------------------------------------------------------------ files and inputs */
+
+/* SaveFlowFile (run_dense.cpp:17-58): "PIEH", int32 w, int32 h, w*h*nc float32 row-major. */
+int ofdis_write_flo(const char *path, const float *flow, int width, int height, int nc);
+/* SavePFMFile (run_dense.cpp:61-82): "Pf\n%d %d\n%f\n" with -1.0, rows bottom-up, values negated. */
+int ofdis_write_pfm(const char *path, const float *depth, int width, int height);
+/* ReadFlowFile (run_dense.cpp:85-129). w/h out; flow may be NULL to query the size. */
+int ofdis_read_flo(const char *path, float *flow, int *width, int *height, int nc);
+/* Binary PGM (P5, noc = 1) / PPM (P6, noc = 3, returned in BGR order like cv::imread). */
+int ofdis_read_pnm(const char *path, uint8_t *pixels, int *width, int *height, int *noc, size_t capacity);
+
+/* Deterministic synthetic frame pair: band-limited texture + noise, frame b is frame
+ * a moved along a known smooth flow (OF) or a horizontal disparity (DE).  Host buffers [h][w][noc]. */
+int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, int mode);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OFDIS_H */

@@ -1,0 +1,1209 @@
+/*
+ * ofdis_oracle.c -- TEST INFRASTRUCTURE ONLY (see ofdis_oracle.h).
+ *
+ * A clean-room, pixel-wise CPU restatement of the reference hot path.  Each function cites the
+ * reference file:line it restates.  Floating-point expressions keep the reference's evaluation
+ * order exactly (no FMA: build with -ffp-contract=off), so that the HIP kernels, which keep the
+ * same order, can be checked bit-for-bit against this file.
+ */
+#include "ofdis_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ helpers */
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+/* std::max(a,b) / std::min(a,b) semantics: (a<b)?b:a and (b<a)?b:a */
+static inline float stdmaxf(float a, float b) { return (a < b) ? b : a; }
+static inline float stdminf(float a, float b) { return (b < a) ? b : a; }
+/* _mm_min_ps / _mm_max_ps semantics: second operand when unordered or equal */
+static inline float ssemin(float a, float b) { return (a < b) ? a : b; }
+static inline float ssemax(float a, float b) { return (a > b) ? a : b; }
+
+/* Eigen::DenseBase::sum() for a dynamic float vector with SSE packets (redux_impl,
+ * LinearVectorizedTraversal, NoUnrolling; aligned start 0): two 4-lane packet accumulators over
+ * packet pairs, res0+res1, odd trailing packet, predux = (l0+l2)+(l1+l3), scalar tail. */
+float ofo_eigen_sum(const float *x, int n) {
+  const int aligned = (n / 4) * 4, aligned2 = (n / 8) * 8;
+  if (aligned == 0) {
+    float r = x[0];
+    for (int i = 1; i < n; ++i) r = r + x[i];
+    return r;
+  }
+  float r0[4], r1[4];
+  for (int l = 0; l < 4; ++l) r0[l] = x[l];
+  if (aligned > 4) {
+    for (int l = 0; l < 4; ++l) r1[l] = x[4 + l];
+    for (int i = 8; i < aligned2; i += 8)
+      for (int l = 0; l < 4; ++l) {
+        r0[l] = r0[l] + x[i + l];
+        r1[l] = r1[l] + x[i + 4 + l];
+      }
+    for (int l = 0; l < 4; ++l) r0[l] = r0[l] + r1[l];
+    if (aligned > aligned2)
+      for (int l = 0; l < 4; ++l) r0[l] = r0[l] + x[aligned2 + l];
+  }
+  float res = (r0[0] + r0[2]) + (r0[1] + r0[3]);
+  for (int i = aligned; i < n; ++i) res = res + x[i];
+  return res;
+}
+
+/* ------------------------------------------------------------------ parameters */
+
+/* run_dense.cpp:181-184 */
+int ofo_auto_first_scale(int imgwidth, int fratio, int patchsize) {
+  float r = log2f((2.0f * (float)imgwidth) / ((float)fratio * (float)patchsize));
+  int v = (int)floorf(r);
+  return v > 0 ? v : 0;
+}
+
+/* run_dense.cpp:226-268 */
+int ofo_params_oppoint(ofdis_params *p, int oppoint, int width_org, int mode, int noc) {
+  memset(p, 0, sizeof(*p));
+  p->mode = mode;
+  p->noc = noc;
+  p->dp_thresh = 0.05f;
+  p->dr_thresh = 0.95f;
+  p->res_thresh = 0.0f;
+  p->usefbcon = 0;
+  p->patnorm = 1;
+  p->costfct = 0;
+  p->tv_alpha = 10.0f;
+  p->tv_gamma = 10.0f;
+  p->tv_delta = 5.0f;
+  p->tv_innerit = 1;
+  p->tv_solverit = 3;
+  p->tv_sor = 1.6f;
+  p->verbosity = 2;
+  const int fratio = 5;
+  switch (oppoint) {
+    case 1:
+      p->p_samp_s = 8; p->patove = 0.3f;
+      p->sc_f = ofo_auto_first_scale(width_org, fratio, p->p_samp_s);
+      p->sc_l = p->sc_f - 2 > 0 ? p->sc_f - 2 : 0;
+      p->max_iter = p->min_iter = 16; p->usetvref = 0;
+      break;
+    case 3:
+      p->p_samp_s = 12; p->patove = 0.75f;
+      p->sc_f = ofo_auto_first_scale(width_org, fratio, p->p_samp_s);
+      p->sc_l = p->sc_f - 4 > 0 ? p->sc_f - 4 : 0;
+      p->max_iter = p->min_iter = 16; p->usetvref = 1;
+      break;
+    case 4:
+      p->p_samp_s = 12; p->patove = 0.75f;
+      p->sc_f = ofo_auto_first_scale(width_org, fratio, p->p_samp_s);
+      p->sc_l = p->sc_f - 5 > 0 ? p->sc_f - 5 : 0;
+      p->max_iter = p->min_iter = 128; p->usetvref = 1;
+      break;
+    case 2:
+    default:
+      p->p_samp_s = 8; p->patove = 0.4f;
+      p->sc_f = ofo_auto_first_scale(width_org, fratio, p->p_samp_s);
+      p->sc_l = p->sc_f - 2 > 0 ? p->sc_f - 2 : 0;
+      p->max_iter = p->min_iter = 12; p->usetvref = 1;
+      break;
+  }
+  return 0;
+}
+
+/* run_dense.cpp:299-312 */
+void ofo_divisibility_pad(int width, int height, int sc_f, int *padw, int *padh) {
+  int scfct = 1 << sc_f;
+  int d = width % scfct;
+  *padw = d > 0 ? scfct - d : 0;
+  d = height % scfct;
+  *padh = d > 0 ? scfct - d : 0;
+}
+
+/* ------------------------------------------------------------------ pyramid (run_dense.cpp:131-179) */
+
+/* Sobel ksize 3, scale 1/8, BORDER_REFLECT_101, on an unpadded w x h x noc level.  OpenCV splits it
+ * as derivative [-1 0 1] along the axis and smoothing [1 2 1]/8 across it.  Level values are
+ * multiples of 4^-level below 256, so every intermediate is exact and the summation order
+ * is immaterial up to level 6. */
+static inline int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  if (i < 0) return -i;
+  if (i >= n) return 2 * n - 2 - i;
+  return i;
+}
+
+static void sobel_level(const float *L, int w, int h, int noc, float *dx, float *dy) {
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      int xm = reflect101(x - 1, w), xp = reflect101(x + 1, w);
+      int ym = reflect101(y - 1, h), yp = reflect101(y + 1, h);
+      for (int c = 0; c < noc; ++c) {
+#define PX(xx, yy) L[((yy) * w + (xx)) * noc + c]
+        float tm = PX(xp, ym) - PX(xm, ym);
+        float t0 = PX(xp, y) - PX(xm, y);
+        float tp = PX(xp, yp) - PX(xm, yp);
+        dx[(y * w + x) * noc + c] = (tm + tp) * 0.125f + t0 * 0.25f;
+        float sm = (PX(xm, ym) + PX(xp, ym)) * 0.125f + PX(x, ym) * 0.25f;
+        float sp = (PX(xm, yp) + PX(xp, yp)) * 0.125f + PX(x, yp) * 0.25f;
+        dy[(y * w + x) * noc + c] = sp - sm;
+#undef PX
+      }
+    }
+}
+
+static void pad_level(const float *L, int w, int h, int noc, int pad, int replicate, float *out) {
+  int W = w + 2 * pad, H = h + 2 * pad;
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      int sx = x - pad, sy = y - pad;
+      int inside = sx >= 0 && sx < w && sy >= 0 && sy < h;
+      for (int c = 0; c < noc; ++c) {
+        float v;
+        if (inside)
+          v = L[(sy * w + sx) * noc + c];
+        else if (replicate)
+          v = L[(clampi(sy, 0, h - 1) * w + clampi(sx, 0, w - 1)) * noc + c];
+        else
+          v = 0.0f;
+        out[(y * W + x) * noc + c] = v;
+      }
+    }
+}
+
+int ofo_build_pyramid(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
+                      float **img_pyr, float **dx_pyr, float **dy_pyr) {
+  int w = width, h = height;
+  float *cur = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
+  if (!cur) return OFDIS_ERR_OUT_OF_MEMORY;
+  for (size_t i = 0; i < (size_t)w * h * noc; ++i) cur[i] = (float)img[i]; /* convertTo CV_32F (:327) */
+  for (int s = 0; s <= sc_f; ++s) {
+    if (s > 0) { /* cv::resize(.5, INTER_LINEAR) -> OpenCV area-fast 2x: mean of the 2x2 block */
+      int nw = w / 2, nh = h / 2;
+      float *nx = (float *)malloc(sizeof(float) * (size_t)nw * nh * noc);
+      if (!nx) { free(cur); return OFDIS_ERR_OUT_OF_MEMORY; }
+      for (int y = 0; y < nh; ++y)
+        for (int x = 0; x < nw; ++x)
+          for (int c = 0; c < noc; ++c) {
+            float a = cur[((2 * y) * w + 2 * x) * noc + c], b = cur[((2 * y) * w + 2 * x + 1) * noc + c];
+            float d = cur[((2 * y + 1) * w + 2 * x) * noc + c], e = cur[((2 * y + 1) * w + 2 * x + 1) * noc + c];
+            nx[(y * nw + x) * noc + c] = ((a + b) + (d + e)) * 0.25f;
+          }
+      free(cur);
+      cur = nx; w = nw; h = nh;
+    }
+    if (s >= sc_l) {
+      float *dx = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
+      float *dy = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
+      if (!dx || !dy) { free(dx); free(dy); free(cur); return OFDIS_ERR_OUT_OF_MEMORY; }
+      sobel_level(cur, w, h, noc, dx, dy);
+      pad_level(cur, w, h, noc, imgpadding, 1, img_pyr[s]); /* BORDER_REPLICATE (:167) */
+      pad_level(dx, w, h, noc, imgpadding, 0, dx_pyr[s]);   /* BORDER_CONSTANT 0 (:172-173) */
+      pad_level(dy, w, h, noc, imgpadding, 0, dy_pyr[s]);
+      free(dx); free(dy);
+    }
+  }
+  free(cur);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ DIS patch (patch.cpp) */
+
+typedef struct {
+  int w, h, pad, tmp_w;    /* camparam (oflow.h:30-43) */
+  float tmp_lb, tmp_ubw, tmp_ubh;
+  int curr_lv;
+  int camlr;
+} cam_t;
+
+typedef struct {
+  int nop, p, novals, noc, costfct, patnorm, max_iter, min_iter, steps;
+  float dp_thresh_sq, dr_thresh, res_thresh, outlierthresh;
+} opt_t;
+
+/* Eigen LLT<2x2>.solve (unblocked llt_inplace + unrolled triangular solves). */
+static void llt2_solve(float H00, float H01, float H11, float b0, float b1, float *x0, float *x1) {
+  float L00 = H00, L10 = H01, L11 = H11;
+  if (!(H00 <= 0.0f)) {
+    L00 = sqrtf(H00);
+    L10 = H01 / L00;
+    float t = H11 - L10 * L10;
+    if (!(t <= 0.0f)) L11 = sqrtf(t);
+  }
+  float y0 = b0 / L00;
+  float y1 = (b1 - L10 * y0) / L11;
+  float z1 = y1 / L11;
+  float z0 = (y0 - L10 * z1) / L00;
+  *x0 = z0;
+  *x1 = z1;
+}
+
+static float llt1_solve(float H, float b) {
+  float L = H;
+  if (!(H <= 0.0f)) L = sqrtf(H);
+  float y = b / L;
+  return y / L;
+}
+
+/* getPatchStaticBil (patch.cpp:345-413) + mean normalisation. */
+static void patch_sample_bil(const cam_t *c, const opt_t *o, const float *img, const float mid[2], float *out) {
+  int pos0 = (int)ceilf(mid[0] + 0.00001f);
+  int pos1 = (int)ceilf(mid[1] + 0.00001f);
+  int pos2 = (int)floorf(mid[0]);
+  int pos3 = (int)floorf(mid[1]);
+  float rx = mid[0] - (float)pos2, ry = mid[1] - (float)pos3;
+  float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+  pos0 += c->pad;
+  pos1 += c->pad;
+  const int p = o->p, noc = o->noc;
+  int k = 0;
+  for (int iy = 0; iy < p; ++iy) {
+    int row = pos1 - p / 2 + iy;
+    for (int ix = 0; ix < p; ++ix) {
+      int col = pos0 - p / 2 + ix;
+      for (int ch = 0; ch < noc; ++ch, ++k) {
+        float A = img[((size_t)row * c->tmp_w + col) * noc + ch];
+        float B = img[((size_t)row * c->tmp_w + col - 1) * noc + ch];
+        float C = img[((size_t)(row - 1) * c->tmp_w + col) * noc + ch];
+        float D = img[((size_t)(row - 1) * c->tmp_w + col - 1) * noc + ch];
+        out[k] = w0 * A + w1 * B + w2 * C + w3 * D;
+      }
+    }
+  }
+  if (o->patnorm > 0) {
+    float mean = ofo_eigen_sum(out, o->novals) / (float)o->novals;
+    for (int i = 0; i < o->novals; ++i) out[i] = out[i] - mean;
+  }
+}
+
+/* LossComputeErrorImage (patch.cpp:221-273): in = normalised sample, tmp = template. */
+static void patch_loss(const opt_t *o, float *pdiff, float *pweight, const float *tmp) {
+  const float bsq = 5.0f * 5.0f, b2sq = bsq * 2.0f;
+  for (int i = 0; i < o->novals; ++i) {
+    float d = pdiff[i] - tmp[i];
+    if (o->costfct == 0) {
+      pdiff[i] = d;
+      pweight[i] = fabsf(d);
+    } else if (o->costfct == 1) {
+      float pw = sqrtf(fabsf(d));
+      pweight[i] = pw;
+      pdiff[i] = copysignf(pw, d);
+    } else {
+      float pw = sqrtf((sqrtf(1.0f + (d * d) / bsq) - 1.0f) * b2sq);
+      pweight[i] = pw;
+      pdiff[i] = copysignf(pw, d);
+    }
+  }
+}
+
+typedef struct {
+  float pt_ref[2];
+  float p_in[2], p_iter[2], delta_p[2], pt_iter[2], pt_st[2];
+  float sq, sq_init, mares, mares_old;
+  int cnt, converged;
+  float H00, H01, H11;
+  float *tmp, *dxx, *dyy, *pdiff, *pweight;
+} patch_t;
+
+/* OptimizeComputeErrImg (patch.cpp:275-295) */
+static void patch_err(const cam_t *c, const opt_t *o, const float *im_b, patch_t *P) {
+  patch_sample_bil(c, o, im_b, P->pt_iter, P->pdiff);
+  patch_loss(o, P->pdiff, P->pweight, P->tmp);
+  if (o->nop == 2)
+    P->sq = P->delta_p[0] * P->delta_p[0] + P->delta_p[1] * P->delta_p[1];
+  else
+    P->sq = P->delta_p[0] * P->delta_p[0];
+  if (P->cnt == 1) P->sq_init = P->sq;
+  P->mares_old = P->mares;
+  /* lpNorm<1> = cwiseAbs().sum() */
+  float *ab = (float *)malloc(sizeof(float) * o->novals);
+  for (int i = 0; i < o->novals; ++i) ab[i] = fabsf(P->pweight[i]);
+  P->mares = ofo_eigen_sum(ab, o->novals) / (float)o->novals;
+  free(ab);
+  int keep = (P->cnt < o->max_iter) & (P->mares > o->res_thresh) &
+             ((P->cnt < o->min_iter) | (P->sq / P->sq_init >= o->dp_thresh_sq)) &
+             ((P->cnt < o->min_iter) | (P->mares / P->mares_old <= o->dr_thresh));
+  if (!keep) P->converged = 1;
+}
+
+static inline void paramtopt(const opt_t *o, patch_t *P) {
+  if (o->nop == 2) {
+    P->pt_iter[0] = P->pt_ref[0] + P->p_iter[0];
+    P->pt_iter[1] = P->pt_ref[1] + P->p_iter[1];
+  } else {
+    P->pt_iter[0] = P->pt_ref[0] + P->p_iter[0];
+  }
+}
+
+static inline int out_of_bounds(const cam_t *c, const float pt[2]) {
+  return pt[0] < c->tmp_lb || pt[1] < c->tmp_lb || pt[0] > c->tmp_ubw || pt[1] > c->tmp_ubh;
+}
+
+/* InitializePatch + SetTargetImage + OptimizeIter(p_init, true)
+ * (patch.cpp:55-67,69-86,88-115,117-154,156-210). */
+static void patch_run(const cam_t *c, const opt_t *o, const float *im_a, const float *im_a_dx,
+                      const float *im_a_dy, const float *im_b, const float p_init[2], patch_t *P) {
+  const int p = o->p, noc = o->noc, nv = o->novals;
+  /* ResetPatch */
+  P->pt_st[0] = P->pt_iter[0] = P->pt_ref[0];
+  P->pt_st[1] = P->pt_iter[1] = P->pt_ref[1];
+  P->p_in[0] = P->p_in[1] = P->p_iter[0] = P->p_iter[1] = P->delta_p[0] = P->delta_p[1] = 0.0f;
+  P->sq = P->sq_init = (float)1e-10;
+  P->mares = P->mares_old = (float)1e20;
+  P->cnt = 0;
+  P->converged = 0;
+  /* getPatchStaticNNGrad (patch.cpp:297-343) */
+  int px = (int)roundf(P->pt_ref[0]) + c->pad, py = (int)roundf(P->pt_ref[1]) + c->pad;
+  int k = 0;
+  for (int j = -p / 2; j <= p / 2 - 1; ++j)
+    for (int i = -p / 2; i <= p / 2 - 1; ++i) {
+      size_t idx = ((size_t)(py + j) * c->tmp_w + (px + i)) * noc;
+      for (int ch = 0; ch < noc; ++ch, ++k) {
+        P->tmp[k] = im_a[idx + ch];
+        P->dxx[k] = im_a_dx[idx + ch];
+        P->dyy[k] = im_a_dy[idx + ch];
+      }
+    }
+  if (o->patnorm > 0) {
+    float mean = ofo_eigen_sum(P->tmp, nv) / (float)nv;
+    for (int i = 0; i < nv; ++i) P->tmp[i] = P->tmp[i] - mean;
+  }
+  /* ComputeHessian (patch.cpp:69-86) */
+  float *prod = (float *)malloc(sizeof(float) * nv);
+  for (int i = 0; i < nv; ++i) prod[i] = P->dxx[i] * P->dxx[i];
+  P->H00 = ofo_eigen_sum(prod, nv);
+  if (o->nop == 2) {
+    for (int i = 0; i < nv; ++i) prod[i] = P->dxx[i] * P->dyy[i];
+    P->H01 = ofo_eigen_sum(prod, nv);
+    for (int i = 0; i < nv; ++i) prod[i] = P->dyy[i] * P->dyy[i];
+    P->H11 = ofo_eigen_sum(prod, nv);
+    if (P->H00 * P->H11 - P->H01 * P->H01 == 0.0f) {
+      P->H00 = (float)((double)P->H00 + 1e-10);
+      P->H11 = (float)((double)P->H11 + 1e-10);
+    }
+  } else {
+    if (P->H00 == 0.0f) P->H00 = (float)((double)P->H00 + 1e-10);
+  }
+  /* OptimizeStart */
+  P->p_in[0] = P->p_iter[0] = p_init[0];
+  if (o->nop == 2) P->p_in[1] = P->p_iter[1] = p_init[1];
+  paramtopt(o, P);
+  P->pt_st[0] = P->pt_iter[0];
+  P->pt_st[1] = P->pt_iter[1];
+  if (out_of_bounds(c, P->pt_iter)) {
+    P->converged = 1;
+    memcpy(P->pdiff, P->tmp, sizeof(float) * nv);
+    /* pweight is never written upstream (uninitialised heap, patch.cpp:133-139): defined as 0 here */
+    memset(P->pweight, 0, sizeof(float) * nv);
+  } else {
+    P->cnt = 0;
+    P->sq = P->sq_init = (float)1e-10;
+    P->mares = 1e5f;
+    P->mares_old = (float)1e20;
+    P->converged = 0;
+    patch_err(c, o, im_b, P);
+  }
+  /* OptimizeIter loop */
+  while (!P->converged) {
+    P->cnt++;
+    for (int i = 0; i < nv; ++i) prod[i] = P->dxx[i] * P->pdiff[i];
+    float b0 = ofo_eigen_sum(prod, nv);
+    if (o->nop == 2) {
+      for (int i = 0; i < nv; ++i) prod[i] = P->dyy[i] * P->pdiff[i];
+      float b1 = ofo_eigen_sum(prod, nv);
+      llt2_solve(P->H00, P->H01, P->H11, b0, b1, &P->delta_p[0], &P->delta_p[1]);
+      P->p_iter[0] = P->p_iter[0] - P->delta_p[0];
+      P->p_iter[1] = P->p_iter[1] - P->delta_p[1];
+    } else {
+      P->delta_p[0] = llt1_solve(P->H00, b0);
+      P->p_iter[0] = P->p_iter[0] - P->delta_p[0];
+      if (c->camlr == 0)
+        P->p_iter[0] = stdminf(P->p_iter[0], 0.0f);
+      else
+        P->p_iter[0] = stdmaxf(P->p_iter[0], 0.0f);
+    }
+    paramtopt(o, P);
+    float ex = P->pt_st[0] - P->pt_iter[0], ey = P->pt_st[1] - P->pt_iter[1];
+    if (sqrtf(ex * ex + ey * ey) > o->outlierthresh || out_of_bounds(c, P->pt_iter)) {
+      P->p_iter[0] = P->p_in[0];
+      if (o->nop == 2) P->p_iter[1] = P->p_in[1];
+      paramtopt(o, P);
+      P->converged = 1;
+    }
+    patch_err(c, o, im_b, P);
+  }
+  free(prod);
+}
+
+/* ------------------------------------------------------------------ grid (patchgrid.cpp) */
+
+typedef struct {
+  int nopw, noph, nopatches, offw, offh, steps;
+} grid_t;
+
+/* PatGridClass ctor geometry (patchgrid.cpp:42-75). */
+static void grid_geometry(const cam_t *c, const opt_t *o, grid_t *g) {
+  g->steps = o->steps;
+  g->nopw = (int)ceilf((float)c->w / (float)o->steps);
+  g->noph = (int)ceilf((float)c->h / (float)o->steps);
+  g->offw = (c->w - (g->nopw - 1) * o->steps) / 2;
+  g->offh = (c->h - (g->noph - 1) * o->steps) / 2;
+  g->nopatches = g->nopw * g->noph;
+}
+
+/* AggregateFlowDense, forward grid only (patchgrid.cpp:213-275, 377-397).
+ * params[ip*nop + k], pweight[ip*novals + i]. */
+static void aggregate(const cam_t *c, const opt_t *o, const grid_t *g, const patch_t *pats, float *flowout) {
+  const int w = c->w, h = c->h, nop = o->nop, p = o->p;
+  float *we = (float *)calloc((size_t)w * h, sizeof(float));
+  memset(flowout, 0, sizeof(float) * (size_t)w * h * nop);
+  for (int ip = 0; ip < g->nopatches; ++ip) {
+    const patch_t *P = &pats[ip];
+    const float *pw = P->pweight;
+    for (int y = -p / 2; y <= p / 2 - 1; ++y)
+      for (int x = -p / 2; x <= p / 2 - 1; ++x, ++pw) {
+        int yt = (int)((float)y + P->pt_ref[1]);
+        int xt = (int)((float)x + P->pt_ref[0]);
+        if (xt >= 0 && yt >= 0 && xt < w && yt < h) {
+          int i = yt * w + xt;
+          float absw;
+          if (o->noc == 1) {
+            absw = 1.0f / stdmaxf(2.0f, *pw);
+          } else {
+            absw = stdmaxf(2.0f, *pw); ++pw;
+            absw = absw + stdmaxf(2.0f, *pw); ++pw;
+            absw = absw + stdmaxf(2.0f, *pw);
+            absw = 1.0f / absw;
+          }
+          we[i] = we[i] + absw;
+          for (int k = 0; k < nop; ++k) flowout[nop * i + k] = flowout[nop * i + k] + P->p_iter[k] * absw;
+        }
+      }
+  }
+  for (int i = 0; i < w * h; ++i)
+    if (we[i] > 0)
+      for (int k = 0; k < nop; ++k) flowout[nop * i + k] = flowout[nop * i + k] / we[i];
+  free(we);
+}
+
+/* ------------------------------------------------------------------ FDF1.0.1 restatements */
+
+/* 5-tap / 3-tap separable convolutions, replicate border (image.cpp:419-624): evaluation order
+ * c0*s0 + ((c1*s1 + c2*s2) + (c3*s3 + c4*s4)) and c0*s0 + (c1*s1 + c2*s2). */
+static const float K5[5] = {1.0f / 12.0f, -8.0f / 12.0f, -0.0f, 8.0f / 12.0f, -1.0f / 12.0f};
+static const float K3[3] = {-0.5f, -0.0f, 0.5f};
+
+static void conv5_h(float *dst, const float *src, int w, int h) {
+  for (int y = 0; y < h; ++y) {
+    const float *s = src + (size_t)y * w;
+    for (int x = 0; x < w; ++x) {
+      float s0 = s[clampi(x - 2, 0, w - 1)], s1 = s[clampi(x - 1, 0, w - 1)], s2 = s[x];
+      float s3 = s[clampi(x + 1, 0, w - 1)], s4 = s[clampi(x + 2, 0, w - 1)];
+      dst[(size_t)y * w + x] = K5[0] * s0 + ((K5[1] * s1 + K5[2] * s2) + (K5[3] * s3 + K5[4] * s4));
+    }
+  }
+}
+static void conv5_v(float *dst, const float *src, int w, int h) {
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      float s0 = src[(size_t)clampi(y - 2, 0, h - 1) * w + x], s1 = src[(size_t)clampi(y - 1, 0, h - 1) * w + x];
+      float s2 = src[(size_t)y * w + x];
+      float s3 = src[(size_t)clampi(y + 1, 0, h - 1) * w + x], s4 = src[(size_t)clampi(y + 2, 0, h - 1) * w + x];
+      dst[(size_t)y * w + x] = K5[0] * s0 + ((K5[1] * s1 + K5[2] * s2) + (K5[3] * s3 + K5[4] * s4));
+    }
+}
+static void conv3_h(float *dst, const float *src, int w, int h) {
+  for (int y = 0; y < h; ++y) {
+    const float *s = src + (size_t)y * w;
+    for (int x = 0; x < w; ++x) {
+      float s0 = s[clampi(x - 1, 0, w - 1)], s1 = s[x], s2 = s[clampi(x + 1, 0, w - 1)];
+      dst[(size_t)y * w + x] = K3[0] * s0 + (K3[1] * s1 + K3[2] * s2);
+    }
+  }
+}
+static void conv3_v(float *dst, const float *src, int w, int h) {
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      float s0 = src[(size_t)clampi(y - 1, 0, h - 1) * w + x], s1 = src[(size_t)y * w + x];
+      float s2 = src[(size_t)clampi(y + 1, 0, h - 1) * w + x];
+      dst[(size_t)y * w + x] = K3[0] * s0 + (K3[1] * s1 + K3[2] * s2);
+    }
+}
+
+/* image_warp (opticalflow_aux.c:31-75) */
+void ofo_image_warp(float *dst, float *mask, const float *src, const float *wx, const float *wy, int w, int h,
+                    int noc) {
+  const size_t plane = (size_t)w * h;
+  for (int j = 0; j < h; ++j)
+    for (int i = 0; i < w; ++i) {
+      size_t o = (size_t)j * w + i;
+      float xx = (float)i + wx[o], yy = (float)j + wy[o];
+      int x = (int)floorf(xx), y = (int)floorf(yy);
+      float dx = xx - (float)x, dy = yy - (float)y;
+      mask[o] = (xx >= 0 && xx <= (float)(w - 1) && yy >= 0 && yy <= (float)(h - 1)) ? 1.0f : 0.0f;
+      int x1 = clampi(x, 0, w - 1), x2 = clampi(x + 1, 0, w - 1);
+      int y1 = clampi(y, 0, h - 1), y2 = clampi(y + 1, 0, h - 1);
+      for (int c = 0; c < noc; ++c) {
+        const float *s = src + c * plane;
+        dst[c * plane + o] = s[(size_t)y1 * w + x1] * (1.0f - dx) * (1.0f - dy) + s[(size_t)y1 * w + x2] * dx * (1.0f - dy) +
+                             s[(size_t)y2 * w + x1] * (1.0f - dx) * dy + s[(size_t)y2 * w + x2] * dx * dy;
+      }
+    }
+}
+
+/* get_derivatives (opticalflow_aux.c:77-132) */
+void ofo_get_derivatives(const float *im1, const float *im2, int w, int h, int noc, float *dx, float *dy,
+                         float *dt, float *dxx, float *dxy, float *dyy, float *dxt, float *dyt) {
+  const size_t plane = (size_t)w * h;
+  float *t = (float *)malloc(sizeof(float) * plane);
+  for (int c = 0; c < noc; ++c) {
+    size_t o = c * plane;
+    for (size_t i = 0; i < plane; ++i) {
+      t[i] = 0.5f * (im2[o + i] + im1[o + i]);
+      dt[o + i] = im2[o + i] - im1[o + i];
+    }
+    conv5_h(dx + o, t, w, h);
+    conv5_v(dy + o, t, w, h);
+    conv5_h(dxx + o, dx + o, w, h);
+    conv5_v(dxy + o, dx + o, w, h);
+    conv5_v(dyy + o, dy + o, w, h);
+    conv5_h(dxt + o, dt + o, w, h);
+    conv5_v(dyt + o, dt + o, w, h);
+  }
+  free(t);
+}
+
+/* compute_smoothness (opticalflow_aux.c:138-187) */
+void ofo_compute_smoothness(float *dst_h, float *dst_v, const float *uu, const float *vv, int w, int h,
+                            float quarter_alpha) {
+  const size_t n = (size_t)w * h;
+  float *ux = (float *)malloc(sizeof(float) * n), *vx = (float *)malloc(sizeof(float) * n);
+  float *uy = (float *)malloc(sizeof(float) * n), *vy = (float *)malloc(sizeof(float) * n);
+  float *s = (float *)malloc(sizeof(float) * n);
+  conv3_h(ux, uu, w, h);
+  conv3_h(vx, vv, w, h);
+  conv3_v(uy, uu, w, h);
+  conv3_v(vy, vv, w, h);
+  const float eps = 0.001f * 0.001f;
+  for (size_t i = 0; i < n; ++i)
+    s[i] = quarter_alpha / sqrtf(eps + ((ux[i] * ux[i] + uy[i] * uy[i]) + (vx[i] * vx[i] + vy[i] * vy[i])));
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      size_t i = (size_t)y * w + x;
+      dst_h[i] = (x < w - 1) ? s[i] + s[i + 1] : 0.0f;
+      dst_v[i] = (y < h - 1) ? s[i] + s[i + w] : 0.0f;
+    }
+  free(ux); free(vx); free(uy); free(vy); free(s);
+}
+
+/* sub_laplacian (opticalflow_aux.c:194-223): b = ((((b - th[x-1]) + th[x]) - tv[y-1]) + tv[y]) */
+void ofo_sub_laplacian(float *dst, const float *src, const float *wh, const float *wv, int w, int h) {
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w - 1; ++x) {
+      size_t i = (size_t)y * w + x;
+      float t = wh[i] * (src[i + 1] - src[i]);
+      dst[i] = dst[i] + t;
+      dst[i + 1] = dst[i + 1] - t;
+    }
+  for (int y = 0; y < h - 1; ++y)
+    for (int x = 0; x < w; ++x) {
+      size_t i = (size_t)y * w + x;
+      float t = wv[i] * (src[i + w] - src[i]);
+      dst[i] = dst[i] + t;
+      dst[i + w] = dst[i + w] - t;
+    }
+}
+
+#define DNORM (0.1f * 0.1f)
+#define EPS_COLOR (0.001f * 0.001f)
+#define EPS_GRAD (0.001f * 0.001f)
+
+/* compute_data (opticalflow_aux.c:408-594).  The RGB branch keeps the upstream slips exactly:
+ * channel 1's colour term uses Iy of channel 2, and the gradient robust sum keeps only channel 3. */
+void ofo_compute_data(float *a11, float *a12, float *a22, float *b1, float *b2, const float *mask,
+                      const float *du, const float *dv, const float *Ix, const float *Iy, const float *Iz,
+                      const float *Ixx, const float *Ixy, const float *Iyy, const float *Ixz, const float *Iyz,
+                      int w, int h, int noc, float hdo3, float hgo3) {
+  const size_t n = (size_t)w * h;
+  for (size_t i = 0; i < n; ++i) {
+    float A11 = 0.0f, A12 = 0.0f, A22 = 0.0f, B1 = 0.0f, B2 = 0.0f;
+    const float u = du[i], v = dv[i], m = mask[i];
+    float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
+    if (noc == 1) {
+      if (hdo3 != 0.0f) {
+        tmpx = Ix[i]; tmpy = Iy[i];
+        tmp2 = (Iz[i] + tmpx * u) + tmpy * v;
+        n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+        tmp = (tmp2 * tmp2) / n1;
+        tmp = (m * hdo3) / sqrtf(EPS_COLOR + 3.0f * tmp);
+        tmp3 = tmp / n1;
+        tmp2 = tmp3 * tmpx;
+        tmp3 = tmp3 * tmpy;
+        A11 = A11 + tmp2 * tmpx;
+        A12 = A12 + tmp2 * tmpy;
+        A22 = A22 + tmp3 * tmpy;
+        B1 = B1 - tmp2 * Iz[i];
+        B2 = B2 - tmp3 * Iz[i];
+      }
+      tmpx = Ixx[i]; tmpy = Iyy[i]; tmpxy = Ixy[i];
+      tmp2 = (Ixz[i] + tmpx * u) + tmpxy * v;
+      tmp3 = (Iyz[i] + tmpxy * u) + tmpy * v;
+      tmpxy = tmpxy * tmpxy;
+      n1 = (tmpxy + DNORM) + tmpx * tmpx;
+      n2 = (tmpxy + DNORM) + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n1 + (tmp3 * tmp3) / n2;
+      tmp = (m * hgo3) / sqrtf(EPS_GRAD + 3.0f * tmp);
+      tmp2 = tmp / n2; tmp3 = tmp / n1;
+      tmpxy = Ixy[i];
+      A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+      B1 = (B1 - (tmp3 * tmpx) * Ixz[i]) - (tmp2 * tmpxy) * Iyz[i];
+      B2 = (B2 - (tmp2 * tmpy) * Iyz[i]) - (tmp3 * tmpxy) * Ixz[i];
+      tmpxy = tmpxy * tmpxy;
+      A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+      A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+      A11 = A11 * 3.0f; A12 = A12 * 3.0f; A22 = A22 * 3.0f; B1 = B1 * 3.0f; B2 = B2 * 3.0f;
+    } else {
+      const size_t o2 = n, o3 = 2 * n;
+      float n3, n4, n5, n6;
+      if (hdo3 != 0.0f) {
+        tmpx = Ix[i]; tmpy = Iy[i];
+        tmp2 = (Iz[i] + tmpx * u) + tmpy * v;
+        n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+        tmp = (tmp2 * tmp2) / n1;
+        tmpx = Ix[o2 + i]; tmpy = Iy[o2 + i];
+        tmp2 = (Iz[o2 + i] + tmpx * u) + tmpy * v;
+        n2 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+        tmp = tmp + (tmp2 * tmp2) / n2;
+        tmpx = Ix[o3 + i]; tmpy = Iy[o3 + i];
+        tmp2 = (Iz[o3 + i] + tmpx * u) + tmpy * v;
+        n3 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+        tmp = tmp + (tmp2 * tmp2) / n3;
+        tmp = (m * hdo3) / sqrtf(EPS_COLOR + tmp);
+        tmp3 = tmp / n3;
+        tmp2 = tmp3 * tmpx;
+        tmp3 = tmp3 * tmpy;
+        A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+        B1 = B1 - tmp2 * Iz[o3 + i]; B2 = B2 - tmp3 * Iz[o3 + i];
+        tmpx = Ix[o2 + i]; tmpy = Iy[o2 + i];
+        tmp3 = tmp / n2;
+        tmp2 = tmp3 * tmpx;
+        tmp3 = tmp3 * tmpy;
+        A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+        B1 = B1 - tmp2 * Iz[o2 + i]; B2 = B2 - tmp3 * Iz[o2 + i];
+        tmpx = Ix[i]; tmpy = Iy[o2 + i]; /* upstream slip: channel 2's Iy */
+        tmp3 = tmp / n1;
+        tmp2 = tmp3 * tmpx;
+        tmp3 = tmp3 * tmpy;
+        A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+        B1 = B1 - tmp2 * Iz[i]; B2 = B2 - tmp3 * Iz[i];
+      }
+      /* gradient: the robust sum is overwritten per channel (only channel 3 survives) */
+      tmpx = Ixx[i]; tmpy = Iyy[i]; tmpxy = Ixy[i];
+      tmp2 = (Ixz[i] + tmpx * u) + tmpxy * v;
+      tmp3 = (Iyz[i] + tmpxy * u) + tmpy * v;
+      tmpxy = tmpxy * tmpxy;
+      n1 = (tmpxy + DNORM) + tmpx * tmpx;
+      n2 = (tmpxy + DNORM) + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n1 + (tmp3 * tmp3) / n2;
+      tmpx = Ixx[o2 + i]; tmpy = Iyy[o2 + i]; tmpxy = Ixy[o2 + i];
+      tmp2 = (Ixz[o2 + i] + tmpx * u) + tmpxy * v;
+      tmp3 = (Iyz[o2 + i] + tmpxy * u) + tmpy * v;
+      tmpxy = tmpxy * tmpxy;
+      n3 = (tmpxy + DNORM) + tmpx * tmpx;
+      n4 = (tmpxy + DNORM) + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n3 + (tmp3 * tmp3) / n4;
+      tmpx = Ixx[o3 + i]; tmpy = Iyy[o3 + i]; tmpxy = Ixy[o3 + i];
+      tmp2 = (Ixz[o3 + i] + tmpx * u) + tmpxy * v;
+      tmp3 = (Iyz[o3 + i] + tmpxy * u) + tmpy * v;
+      tmpxy = tmpxy * tmpxy;
+      n5 = (tmpxy + DNORM) + tmpx * tmpx;
+      n6 = (tmpxy + DNORM) + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n5 + (tmp3 * tmp3) / n6;
+      tmp = (m * hgo3) / sqrtf(EPS_GRAD + tmp);
+      /* channel 3 */
+      tmp2 = tmp / n6; tmp3 = tmp / n5;
+      A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+      A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+      tmpxy = Ixy[o3 + i];
+      A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+      B1 = (B1 - (tmp3 * tmpx) * Ixz[o3 + i]) - (tmp2 * tmpxy) * Iyz[o3 + i];
+      B2 = (B2 - (tmp2 * tmpy) * Iyz[o3 + i]) - (tmp3 * tmpxy) * Ixz[o3 + i];
+      /* channel 2 */
+      tmp2 = tmp / n4; tmp3 = tmp / n3;
+      tmpx = Ixx[o2 + i]; tmpy = Iyy[o2 + i]; tmpxy = Ixy[o2 + i];
+      A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+      B1 = (B1 - (tmp3 * tmpx) * Ixz[o2 + i]) - (tmp2 * tmpxy) * Iyz[o2 + i];
+      B2 = (B2 - (tmp2 * tmpy) * Iyz[o2 + i]) - (tmp3 * tmpxy) * Ixz[o2 + i];
+      tmpxy = tmpxy * tmpxy;
+      A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+      A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+      /* channel 1 */
+      tmpx = Ixx[i]; tmpy = Iyy[i];
+      tmp2 = tmp / n2; tmp3 = tmp / n1;
+      tmpxy = Ixy[i];
+      A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+      B1 = (B1 - (tmp3 * tmpx) * Ixz[i]) - (tmp2 * tmpxy) * Iyz[i];
+      B2 = (B2 - (tmp2 * tmpy) * Iyz[i]) - (tmp3 * tmpxy) * Ixz[i];
+      tmpxy = tmpxy * tmpxy;
+      A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+      A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+    }
+    a11[i] = A11; a12[i] = A12; a22[i] = A22; b1[i] = B1; b2[i] = B2;
+  }
+}
+
+/* compute_data_DE (opticalflow_aux.c:601-747) */
+void ofo_compute_data_de(float *a11, float *b1, const float *mask, const float *du, const float *Ix,
+                         const float *Iy, const float *Iz, const float *Ixx, const float *Ixy, const float *Iyy,
+                         const float *Ixz, const float *Iyz, int w, int h, int noc, float hdo3, float hgo3) {
+  const size_t n = (size_t)w * h;
+  for (size_t i = 0; i < n; ++i) {
+    float A11 = 0.0f, B1 = 0.0f;
+    const float u = du[i], m = mask[i];
+    float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
+    if (noc == 1) {
+      if (hdo3 != 0.0f) {
+        tmpx = Ix[i]; tmpy = Iy[i];
+        tmp2 = Iz[i] + tmpx * u;
+        n1 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+        tmp = (tmp2 * tmp2) / n1;
+        tmp = (m * hdo3) / sqrtf(EPS_COLOR + 3.0f * tmp);
+        tmp2 = (tmp / n1) * tmpx;
+        A11 = A11 + tmp2 * tmpx;
+        B1 = B1 - tmp2 * Iz[i];
+      }
+      tmpx = Ixx[i]; tmpy = Iyy[i]; tmpxy = Ixy[i];
+      tmp2 = Iyz[i] + tmpxy * u;
+      tmpxy = DNORM + tmpxy * tmpxy;
+      n1 = tmpxy + tmpx * tmpx;
+      n2 = tmpxy + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n2;
+      tmp2 = Ixz[i] + tmpx * u;
+      tmp = tmp + (tmp2 * tmp2) / n1;
+      tmp = (m * hgo3) / sqrtf(EPS_GRAD + 3.0f * tmp);
+      tmpxy = Ixy[i];
+      tmp2 = (tmp / n2) * tmpxy; tmp3 = (tmp / n1) * tmpx;
+      A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+      B1 = (B1 - tmp3 * Ixz[i]) - tmp2 * Iyz[i];
+      A11 = A11 * 3.0f; B1 = B1 * 3.0f;
+    } else {
+      const size_t o2 = n, o3 = 2 * n;
+      float n3, n4, n5, n6;
+      if (hdo3 != 0.0f) {
+        tmpx = Ix[i]; tmpy = Iy[i];
+        tmp2 = Iz[i] + tmpx * u;
+        n1 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+        tmp = (tmp2 * tmp2) / n1;
+        tmpx = Ix[o2 + i]; tmpy = Iy[o2 + i];
+        tmp2 = Iz[o2 + i] + tmpx * u;
+        n2 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+        tmp = tmp + (tmp2 * tmp2) / n2;
+        tmpx = Ix[o3 + i]; tmpy = Iy[o3 + i];
+        tmp2 = Iz[o3 + i] + tmpx * u;
+        n3 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+        tmp = tmp + (tmp2 * tmp2) / n3;
+        tmp = (m * hdo3) / sqrtf(EPS_COLOR + tmp);
+        tmp2 = (tmp / n3) * tmpx;
+        A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[o3 + i];
+        tmpx = Ix[o2 + i];
+        tmp2 = (tmp / n2) * tmpx;
+        A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[o2 + i];
+        tmpx = Ix[i];
+        tmp2 = (tmp / n1) * tmpx;
+        A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[i];
+      }
+      tmpx = Ixx[i]; tmpy = Iyy[i]; tmpxy = Ixy[i];
+      tmp2 = Iyz[i] + tmpxy * u;
+      tmpxy = DNORM + tmpxy * tmpxy;
+      n1 = tmpxy + tmpx * tmpx;
+      n2 = tmpxy + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n2;
+      tmp2 = Ixz[i] + tmpx * u;
+      tmp = tmp + (tmp2 * tmp2) / n1;
+      tmpx = Ixx[o2 + i]; tmpy = Iyy[o2 + i]; tmpxy = Ixy[o2 + i];
+      tmp2 = Iyz[o2 + i] + tmpxy * u;
+      tmpxy = DNORM + tmpxy * tmpxy;
+      n3 = tmpxy + tmpx * tmpx;
+      n4 = tmpxy + tmpy * tmpy;
+      tmp = tmp + (tmp2 * tmp2) / n4;
+      tmp2 = Ixz[o2 + i] + tmpx * u;
+      tmp = tmp + (tmp2 * tmp2) / n3;
+      tmpx = Ixx[o3 + i]; tmpy = Iyy[o3 + i]; tmpxy = Ixy[o3 + i];
+      tmp2 = Iyz[o3 + i] + tmpxy * u;
+      tmpxy = DNORM + tmpxy * tmpxy;
+      n5 = tmpxy + tmpx * tmpx;
+      n6 = tmpxy + tmpy * tmpy;
+      tmp = tmp + (tmp2 * tmp2) / n6;
+      tmp2 = Ixz[o3 + i] + tmpx * u;
+      tmp = tmp + (tmp2 * tmp2) / n5;
+      tmp = (m * hgo3) / sqrtf(EPS_GRAD + tmp);
+      tmpxy = Ixy[o3 + i];
+      tmp2 = (tmp / n6) * tmpxy; tmp3 = (tmp / n5) * tmpx;
+      A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+      B1 = (B1 - tmp3 * Ixz[o3 + i]) - tmp2 * Iyz[o3 + i];
+      tmpx = Ixx[o2 + i]; tmpxy = Ixy[o2 + i];
+      tmp2 = (tmp / n4) * tmpxy; tmp3 = (tmp / n3) * tmpx;
+      A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+      B1 = (B1 - tmp3 * Ixz[o2 + i]) - tmp2 * Iyz[o2 + i];
+      tmpx = Ixx[i]; tmpxy = Ixy[i];
+      tmp2 = (tmp / n2) * tmpxy; tmp3 = (tmp / n1) * tmpx;
+      A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+      B1 = (B1 - tmp3 * Ixz[i]) - tmp2 * Iyz[i];
+    }
+    a11[i] = A11; b1[i] = B1;
+  }
+}
+
+/* sor_coupled_slow_but_readable (solver.c:34-78): point SOR, used upstream for tiny images. */
+static void sor_point_of(float *du, float *dv, const float *a11, const float *a12, const float *a22,
+                         const float *b1, const float *b2, const float *hh, const float *vv, int w, int hgt,
+                         int iterations, float omega) {
+  for (int it = 0; it < iterations; ++it)
+    for (int j = 0; j < hgt; ++j)
+      for (int i = 0; i < w; ++i) {
+        float su = 0.0f, sv = 0.0f, sd = 0.0f;
+        size_t o = (size_t)j * w + i;
+        if (j > 0) { su -= vv[o - w] * du[o - w]; sv -= vv[o - w] * dv[o - w]; sd += vv[o - w]; }
+        if (i > 0) { su -= hh[o - 1] * du[o - 1]; sv -= hh[o - 1] * dv[o - 1]; sd += hh[o - 1]; }
+        if (j < hgt - 1) { su -= vv[o] * du[o + w]; sv -= vv[o] * dv[o + w]; sd += vv[o]; }
+        if (i < w - 1) { su -= hh[o] * du[o + 1]; sv -= hh[o] * dv[o + 1]; sd += hh[o]; }
+        float A11 = a11[o] + sd, A12 = a12[o], A22 = a22[o] + sd;
+        float B1 = b1[o] - su, B2 = b2[o] - sv;
+        du[o] = (1.0f - omega) * du[o] + omega / A11 * (B1 - A12 * dv[o]);
+        dv[o] = (1.0f - omega) * dv[o] + omega / A22 * (B2 - A12 * du[o]);
+      }
+}
+
+/* sor_coupled (solver.c:83-433): lexicographic block Gauss-Seidel SOR with in-place 2x2 inverse. */
+void ofo_sor_coupled(float *du, float *dv, float *a11, float *a12, float *a22, const float *b1, const float *b2,
+                     const float *hh, const float *vv, int w, int hgt, int iterations, float omega) {
+  if (w < 2 || hgt < 2 || iterations < 1) {
+    sor_point_of(du, dv, a11, a12, a22, b1, b2, hh, vv, w, hgt, iterations, omega);
+    return;
+  }
+  for (int it = 0; it < iterations; ++it)
+    for (int y = 0; y < hgt; ++y)
+      for (int x = 0; x < w; ++x) {
+        size_t o = (size_t)y * w + x;
+        const float hl = x > 0 ? hh[o - 1] : 0.0f, hr = hh[o];
+        const float ur = x < w - 1 ? du[o + 1] : 0.0f, vr = x < w - 1 ? dv[o + 1] : 0.0f;
+        float s1, s2, dpsis;
+        if (y == 0) {
+          dpsis = hl + (hr + vv[o]);
+          s1 = (b1[o] + hr * ur) + vv[o] * du[o + w];
+          s2 = (b2[o] + hr * vr) + vv[o] * dv[o + w];
+        } else if (y < hgt - 1) {
+          const float vt = vv[o - w];
+          dpsis = (hl + hr) + (vt + vv[o]);
+          s1 = ((hr * ur) + vt * du[o - w]) + (b1[o] + vv[o] * du[o + w]);
+          s2 = ((hr * vr) + vt * dv[o - w]) + (b2[o] + vv[o] * dv[o + w]);
+        } else {
+          const float vt = vv[o - w];
+          dpsis = hl + (hr + vt);
+          s1 = (b1[o] + hr * ur) + vt * du[o - w];
+          s2 = (b2[o] + hr * vr) + vt * dv[o - w];
+        }
+        if (it == 0) {
+          float A11 = a22[o] + dpsis, A22 = a11[o] + dpsis, m12 = a12[o];
+          float det = A11 * A22 - m12 * m12;
+          a11[o] = A11 / det;
+          a22[o] = A22 / det;
+          a12[o] = m12 / (0.0f - det);
+        }
+        float B1, B2;
+        if (x == 0) {
+          B1 = s1;
+          B2 = s2;
+        } else {
+          B1 = hl * du[o - 1] + s1;
+          B2 = hl * dv[o - 1] + s2;
+        }
+        const float u0 = du[o], v0 = dv[o];
+        du[o] = u0 + omega * (a11[o] * B1 + a12[o] * B2 - u0);
+        dv[o] = v0 + omega * (a12[o] * B1 + a22[o] * B2 - v0);
+      }
+}
+
+/* sor_coupled_slow_but_readable_DE (solver.c:439-471) */
+void ofo_sor_point_de(float *du, const float *a11, const float *b1, const float *hh, const float *vv, int w,
+                      int hgt, int iterations, float omega) {
+  for (int it = 0; it < iterations; ++it)
+    for (int j = 0; j < hgt; ++j)
+      for (int i = 0; i < w; ++i) {
+        float su = 0.0f, sd = 0.0f;
+        size_t o = (size_t)j * w + i;
+        if (j > 0) { su -= vv[o - w] * du[o - w]; sd += vv[o - w]; }
+        if (i > 0) { su -= hh[o - 1] * du[o - 1]; sd += hh[o - 1]; }
+        if (j < hgt - 1) { su -= vv[o] * du[o + w]; sd += vv[o]; }
+        if (i < w - 1) { su -= hh[o] * du[o + 1]; sd += hh[o]; }
+        float A11 = a11[o] + sd, B1 = b1[o] - su;
+        du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
+      }
+}
+
+/* ------------------------------------------------------------------ VarRefClass (refine_variational.cpp) */
+
+/* ------------------------------------------------------------------ VarRefClass (refine_variational.cpp) */
+
+/* VarRefClass ctor + RefLevelOF / RefLevelDE (refine_variational.cpp:25-116, 152-342).
+ * flow: w*h*nop interleaved, refined in place.  im_ao/im_bo: padded interleaved level images. */
+static int var_refine(const cam_t *c, const opt_t *o, const ofdis_params *p, const float *im_ao,
+                      const float *im_bo, float *flow) {
+  const int w = c->w, h = c->h, noc = o->noc, nop = o->nop;
+  const size_t n = (size_t)w * h;
+  const int n_inner = p->tv_innerit * (c->curr_lv + 1);
+  const float quarter_alpha = 0.25f * p->tv_alpha;
+  const float hgo3 = p->tv_gamma * 0.5f / 3.0f, hdo3 = p->tv_delta * 0.5f / 3.0f;
+  const float omega = p->tv_sor;
+  float *buf = (float *)calloc(n * (15 + 11 * (size_t)noc), sizeof(float));
+  if (!buf) return OFDIS_ERR_OUT_OF_MEMORY;
+  float *wx = buf, *wy = wx + n, *du = wy + n, *dv = du + n, *mask = dv + n, *sh = mask + n, *sv = sh + n;
+  float *uu = sv + n, *vv = uu + n, *a11 = vv + n, *a12 = a11 + n, *a22 = a12 + n, *b1 = a22 + n, *b2 = b1 + n;
+  float *im1 = b2 + n + n, *im2 = im1 + n * noc, *wim2 = im2 + n * noc, *Ix = wim2 + n * noc, *Iy = Ix + n * noc;
+  float *Iz = Iy + n * noc, *Ixx = Iz + n * noc, *Ixy = Ixx + n * noc, *Iyy = Ixy + n * noc, *Ixz = Iyy + n * noc;
+  float *Iyz = Ixz + n * noc; /* 11*noc planes end here; wy stays zero for DE (wy_dummy) */
+  for (size_t i = 0; i < n; ++i) {
+    wx[i] = flow[i * nop];
+    if (nop == 2) wy[i] = flow[i * nop + 1];
+  }
+  /* copyimage (refine_variational.cpp:119-149): padded interleaved -> planar unpadded */
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x)
+      for (int ch = 0; ch < noc; ++ch) {
+        size_t src = ((size_t)(y + c->pad) * c->tmp_w + (x + c->pad)) * noc + ch;
+        im1[ch * n + (size_t)y * w + x] = im_ao[src];
+        im2[ch * n + (size_t)y * w + x] = im_bo[src];
+      }
+  ofo_image_warp(wim2, mask, im2, wx, wy, w, h, noc);
+  ofo_get_derivatives(im1, wim2, w, h, noc, Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz);
+  memset(du, 0, sizeof(float) * n);
+  memset(dv, 0, sizeof(float) * n);
+  memcpy(uu, wx, sizeof(float) * n);
+  memcpy(vv, wy, sizeof(float) * n);
+  for (int it = 0; it < n_inner; ++it) {
+    ofo_compute_smoothness(sh, sv, uu, vv, w, h, quarter_alpha);
+    if (nop == 2) {
+      ofo_compute_data(a11, a12, a22, b1, b2, mask, du, dv, Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz, w, h, noc, hdo3,
+                       hgo3);
+      ofo_sub_laplacian(b1, wx, sh, sv, w, h);
+      ofo_sub_laplacian(b2, wy, sh, sv, w, h);
+      ofo_sor_coupled(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
+      for (size_t i = 0; i < n; ++i) {
+        uu[i] = wx[i] + du[i];
+        vv[i] = wy[i] + dv[i];
+      }
+    } else {
+      ofo_compute_data_de(a11, b1, mask, du, Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz, w, h, noc, hdo3, hgo3);
+      ofo_sub_laplacian(b1, wx, sh, sv, w, h);
+      ofo_sor_point_de(du, a11, b1, sh, sv, w, h, p->tv_solverit, omega);
+      for (size_t i = 0; i < n; ++i)
+        uu[i] = (c->camlr == 0) ? ssemin(wx[i] + du[i], 0.0f) : ssemax(wx[i] + du[i], 0.0f);
+    }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    flow[i * nop] = uu[i];
+    if (nop == 2) flow[i * nop + 1] = vv[i];
+  }
+  free(buf);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ OFClass (oflow.cpp:31-338) */
+
+static void fill_opt(const ofdis_params *p, opt_t *o) {
+  o->nop = p->mode == OFDIS_MODE_OF ? 2 : 1;
+  o->p = p->p_samp_s;
+  o->noc = p->noc;
+  o->novals = p->noc * p->p_samp_s * p->p_samp_s;
+  o->costfct = p->costfct;
+  o->patnorm = p->patnorm;
+  o->max_iter = p->max_iter;
+  o->min_iter = p->min_iter;
+  o->dp_thresh_sq = p->dp_thresh * p->dp_thresh;
+  o->dr_thresh = p->dr_thresh;
+  o->res_thresh = p->res_thresh;
+  o->outlierthresh = (float)p->p_samp_s / 2;
+  int st = (int)floorf((float)p->p_samp_s * (1 - p->patove));
+  o->steps = st > 1 ? st : 1;
+}
+
+static void fill_cam(const ofdis_params *p, int width, int height, int imgpadding, int sl, cam_t *c) {
+  float sc_fct = (float)pow(2.0, -sl);
+  c->w = (int)((float)width * sc_fct);
+  c->h = (int)((float)height * sc_fct);
+  c->pad = imgpadding;
+  c->tmp_lb = -(float)p->p_samp_s / 2;
+  c->tmp_ubw = (float)(c->w + p->p_samp_s / 2 - 2);
+  c->tmp_ubh = (float)(c->h + p->p_samp_s / 2 - 2);
+  c->tmp_w = c->w + 2 * imgpadding;
+  c->curr_lv = sl;
+  c->camlr = 0;
+}
+
+int ofo_oflow(const float *const *im_ao, const float *const *im_ao_dx, const float *const *im_ao_dy,
+              const float *const *im_bo, const float *const *im_bo_dx, const float *const *im_bo_dy,
+              int imgpadding, float *outflow, const float *initflow, int width, int height,
+              const ofdis_params *p, float *const *cap_dis, float *const *cap_tv) {
+  (void)im_bo_dx; (void)im_bo_dy;
+  if (p->usefbcon) return OFDIS_ERR_UNSUPPORTED;
+  if (p->costfct < 0 || p->costfct > 2) return OFDIS_ERR_UNSUPPORTED;
+  opt_t o;
+  fill_opt(p, &o);
+  const int nsc = p->sc_f - p->sc_l + 1;
+  float **flows = (float **)calloc(nsc, sizeof(float *));
+  int rc = 0;
+  for (int sl = p->sc_f; sl >= p->sc_l; --sl) {
+    const int ii = sl - p->sc_l;
+    cam_t c;
+    fill_cam(p, width, height, imgpadding, sl, &c);
+    grid_t g;
+    grid_geometry(&c, &o, &g);
+    flows[ii] = (float *)malloc(sizeof(float) * (size_t)c.w * c.h * o.nop);
+    patch_t *pats = (patch_t *)calloc(g.nopatches, sizeof(patch_t));
+    float *store = (float *)malloc(sizeof(float) * (size_t)g.nopatches * o.novals * 5);
+    for (int x = 0, i = 0; x < g.nopw; ++x)
+      for (int y = 0; y < g.noph; ++y, ++i) {
+        pats[i].pt_ref[0] = (float)(x * g.steps + g.offw);
+        pats[i].pt_ref[1] = (float)(y * g.steps + g.offh);
+        float *s = store + (size_t)i * o.novals * 5;
+        pats[i].tmp = s; pats[i].dxx = s + o.novals; pats[i].dyy = s + 2 * o.novals;
+        pats[i].pdiff = s + 3 * o.novals; pats[i].pweight = s + 4 * o.novals;
+      }
+    /* InitializeFromCoarserOF (patchgrid.cpp:195-211) or zero / initflow (oflow.cpp:206-217) */
+    const float *prev = (sl < p->sc_f) ? flows[ii + 1] : initflow;
+    for (int i = 0; i < g.nopatches; ++i) {
+      float pin[2] = {0.0f, 0.0f};
+      if (prev) {
+        int x = (int)floorf(pats[i].pt_ref[0] / 2), y = (int)floorf(pats[i].pt_ref[1] / 2);
+        int k = y * (c.w / 2) + x;
+        for (int d = 0; d < o.nop; ++d) pin[d] = prev[o.nop * k + d] * 2;
+      }
+      patch_run(&c, &o, im_ao[sl], im_ao_dx[sl], im_ao_dy[sl], im_bo[sl], pin, &pats[i]);
+    }
+    float *dst = (sl == p->sc_l) ? outflow : flows[ii];
+    aggregate(&c, &o, &g, pats, dst);
+    if (cap_dis && cap_dis[sl]) memcpy(cap_dis[sl], dst, sizeof(float) * (size_t)c.w * c.h * o.nop);
+    if (p->usetvref) rc = var_refine(&c, &o, p, im_ao[sl], im_bo[sl], dst);
+    if (cap_tv && cap_tv[sl]) memcpy(cap_tv[sl], dst, sizeof(float) * (size_t)c.w * c.h * o.nop);
+    if (sl == p->sc_l && dst != flows[ii]) memcpy(flows[ii], dst, sizeof(float) * (size_t)c.w * c.h * o.nop);
+    free(store);
+    free(pats);
+    if (rc) break;
+  }
+  for (int i = 0; i < nsc; ++i) free(flows[i]);
+  free(flows);
+  return rc;
+}
+
+/* ------------------------------------------------------------------ upsample + crop (run_dense.cpp:407-415) */
+
+/* cv::resize(INTER_LINEAR) on CV_32FC(nop), generic path (resizeGeneric_ + HResizeLinear + VResizeLinear). */
+int ofo_upsample_crop(const float *flow_l, int wl, int hl, int nop, int scale_log2, int padw, int padh,
+                      int width_org, int height_org, float *out) {
+  const int offx = padw / 2, offy = padh / 2;
+  if (scale_log2 == 0) {
+    for (int y = 0; y < height_org; ++y)
+      for (int x = 0; x < width_org; ++x)
+        for (int k = 0; k < nop; ++k)
+          out[((size_t)y * width_org + x) * nop + k] = flow_l[((size_t)(y + offy) * wl + (x + offx)) * nop + k];
+    return 0;
+  }
+  const float fct = (float)pow(2.0, scale_log2);
+  const int Wd = wl << scale_log2, Hd = hl << scale_log2;
+  const double scale = 1.0 / (double)fct;
+  float *row0 = (float *)malloc(sizeof(float) * (size_t)width_org * nop);
+  float *row1 = (float *)malloc(sizeof(float) * (size_t)width_org * nop);
+  int *xs = (int *)malloc(sizeof(int) * width_org);
+  float *xa = (float *)malloc(sizeof(float) * width_org);
+  int *xl = (int *)malloc(sizeof(int) * width_org);
+  int xmax = Wd;
+  for (int dx = 0; dx < Wd; ++dx) {
+    float fx = (float)((dx + 0.5) * scale - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= wl) {
+      if (dx < xmax) xmax = dx;
+      if (sx >= wl - 1) { fx = 0; sx = wl - 1; }
+    }
+    if (dx >= offx && dx < offx + width_org) {
+      xs[dx - offx] = sx; xa[dx - offx] = fx; xl[dx - offx] = dx < xmax;
+    }
+  }
+  /* xmax is monotone: re-derive the "linear" flag once the full scan is known */
+  for (int x = 0; x < width_org; ++x) xl[x] = (x + offx) < xmax;
+  for (int y = 0; y < height_org; ++y) {
+    int dy = y + offy;
+    float fy = (float)((dy + 0.5) * scale - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    int r0 = sy >= 0 ? (sy < hl ? sy : hl - 1) : 0;
+    int r1 = sy + 1 >= 0 ? (sy + 1 < hl ? sy + 1 : hl - 1) : 0;
+    const float b0 = 1.f - fy, b1 = fy;
+    for (int r = 0; r < 2; ++r) {
+      const float *S = flow_l + (size_t)(r == 0 ? r0 : r1) * wl * nop;
+      float *D = r == 0 ? row0 : row1;
+      for (int x = 0; x < width_org; ++x)
+        for (int k = 0; k < nop; ++k) {
+          float s0 = S[xs[x] * nop + k] * fct;
+          if (xl[x]) {
+            float s1 = S[(xs[x] + 1) * nop + k] * fct;
+            D[x * nop + k] = s0 * (1.f - xa[x]) + s1 * xa[x];
+          } else {
+            D[x * nop + k] = s0;
+          }
+        }
+    }
+    for (int x = 0; x < width_org * nop; ++x) out[(size_t)y * width_org * nop + x] = row0[x] * b0 + row1[x] * b1;
+  }
+  (void)Hd;
+  free(row0); free(row1); free(xs); free(xa); free(xl);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ whole pipeline (run_dense.cpp main) */
+
+int ofo_run_u8(const uint8_t *img_a, const uint8_t *img_b, int width, int height, const ofdis_params *p,
+               float *flow_out, float *const *cap_dis, float *const *cap_tv) {
+  const int noc = p->noc, nop = p->mode == OFDIS_MODE_OF ? 2 : 1, pad = p->p_samp_s;
+  int padw, padh;
+  ofo_divisibility_pad(width, height, p->sc_f, &padw, &padh);
+  const int Wp = width + padw, Hp = height + padh, l = padw / 2, t = padh / 2;
+  uint8_t *pa = (uint8_t *)malloc((size_t)Wp * Hp * noc), *pb = (uint8_t *)malloc((size_t)Wp * Hp * noc);
+  for (int y = 0; y < Hp; ++y)
+    for (int x = 0; x < Wp; ++x)
+      for (int c = 0; c < noc; ++c) {
+        size_t s = ((size_t)clampi(y - t, 0, height - 1) * width + clampi(x - l, 0, width - 1)) * noc + c;
+        pa[((size_t)y * Wp + x) * noc + c] = img_a[s];
+        pb[((size_t)y * Wp + x) * noc + c] = img_b[s];
+      }
+  float *pyr[6][32];
+  memset(pyr, 0, sizeof(pyr));
+  int rc = 0;
+  for (int s = p->sc_l; s <= p->sc_f; ++s) {
+    size_t n = (size_t)((Wp >> s) + 2 * pad) * ((Hp >> s) + 2 * pad) * noc;
+    for (int k = 0; k < 6; ++k) pyr[k][s] = (float *)malloc(sizeof(float) * n);
+  }
+  rc = ofo_build_pyramid(pa, Wp, Hp, noc, p->sc_f, p->sc_l, pad, pyr[0], pyr[1], pyr[2]);
+  if (!rc) rc = ofo_build_pyramid(pb, Wp, Hp, noc, p->sc_f, p->sc_l, pad, pyr[3], pyr[4], pyr[5]);
+  const int wl = Wp >> p->sc_l, hl = Hp >> p->sc_l;
+  float *fl = (float *)malloc(sizeof(float) * (size_t)wl * hl * nop);
+  if (!rc)
+    rc = ofo_oflow((const float *const *)pyr[0], (const float *const *)pyr[1], (const float *const *)pyr[2],
+                   (const float *const *)pyr[3], (const float *const *)pyr[4], (const float *const *)pyr[5], pad, fl,
+                   NULL, Wp, Hp, p, cap_dis, cap_tv);
+  if (!rc) rc = ofo_upsample_crop(fl, wl, hl, nop, p->sc_l, padw, padh, width, height, flow_out);
+  free(fl);
+  for (int s = p->sc_l; s <= p->sc_f; ++s)
+    for (int k = 0; k < 6; ++k) free(pyr[k][s]);
+  free(pa); free(pb);
+  return rc;
+}
+
+/* Exported for pinning tests: one VarRefClass run at scale `level` (refine_variational.cpp:25-116). */
+int ofo_refine_level(const float *im_ao, const float *im_bo, int w, int h, int imgpadding, int level,
+                     const ofdis_params *p, float *flow) {
+  opt_t o;
+  fill_opt(p, &o);
+  cam_t c;
+  memset(&c, 0, sizeof(c));
+  c.w = w; c.h = h; c.pad = imgpadding; c.tmp_w = w + 2 * imgpadding; c.curr_lv = level; c.camlr = 0;
+  return var_refine(&c, &o, p, im_ao, im_bo, flow);
+}
