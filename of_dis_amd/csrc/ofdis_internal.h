@@ -1,0 +1,102 @@
+// ofdis_internal.h -- kernel argument blocks and launchers shared by ofdis_kernels.hip and the runtime.
+//
+// Device data layout (per batch of n frame pairs, all float32 unless noted):
+//   pyramid level s   : [2n][H_s][W_s][noc]  padded by `pad` (W_s = w_s + 2 pad); frames 0..n-1 are
+//                       image a, n..2n-1 image b (same layout as OFClass's inputs, oflow.h:99-106)
+//   patch state       : p_iter [n][npatch][nop], pweight [n][npatch][novals]
+//   flow level s      : planar [n][nop][h_s][w_s]  (wx, wy)
+//   TV scratch        : planar [n][plane][h][w] for du, dv, mask, a11, a12, a22, b1, b2, sh, sv,
+//                       t/dt, and the 8 derivative images (noc planes each)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ofdis {
+
+struct LevelGeom {
+  int w, h;        // unpadded level size
+  int pad;         // imgpadding
+  int W, H;        // padded size
+  int nopw, noph, npatch, offw, offh;
+  float tmp_lb, tmp_ubw, tmp_ubh;
+  int level;       // scale index s
+};
+
+struct PyrBaseArgs {
+  const uint8_t *img_a, *img_b;  // [n][H0][W0][noc]
+  int n, W0, H0, noc;
+  int padl, padt;                // divisibility padding offsets (floor halves)
+  int log2s;                     // level of the output (sc_l)
+  int w, h;                      // output level size
+  float *out;                    // unpadded level [2n][h][w][noc]
+};
+
+struct PyrDownArgs {
+  const float *src;  // [2n][2h][2w][noc]
+  float *dst;        // [2n][h][w][noc]
+  int n2, w, h, noc;
+};
+
+struct PyrPadGradArgs {
+  const float *lvl;        // unpadded [2n][h][w][noc]
+  float *img, *dx, *dy;    // padded [2n][H][W][noc]
+  int n2, w, h, noc, pad;
+};
+
+struct PatchArgs {
+  const float *img_a, *dx_a, *dy_a, *img_b;  // padded level, frame stride = W*H*noc
+  const float *prev;                          // coarse flow or NULL
+  long prev_frame_stride;                     // floats per frame
+  int prev_comp_stride, prev_elem_stride, prev_w;
+  float *p_iter;                              // [n][npatch][nop]
+  float *pweight;                             // [n][npatch][novals]
+  int n, nop, noc, p, novals, steps;
+  int costfct, patnorm, max_iter, min_iter;
+  float dp_thresh_sq, dr_thresh, res_thresh, outlierthresh;
+  int camlr;
+  LevelGeom g;
+};
+
+struct AggArgs {
+  const float *p_iter, *pweight;
+  float *flow;  // planar [n][nop][h][w]
+  int n, nop, noc, p, novals, steps;
+  LevelGeom g;
+};
+
+struct TvArgs {
+  // level images (padded interleaved) and flow
+  const float *img_a, *img_b;
+  float *flow;                 // planar [n][nop][h][w]  (wx, wy)
+  float *du, *dv, *mask;       // [n][h][w]
+  float *a11, *a12, *a22, *b1, *b2, *sh, *sv;
+  float *t, *dt;               // [n][noc][h][w]
+  float *Ix, *Iy, *Iz, *Ixx, *Ixy, *Iyy, *Ixz, *Iyz;  // [n][noc][h][w]
+  int n, nop, noc, w, h, pad, W;
+  float quarter_alpha, hdo3, hgo3, omega;
+  int first_iter;              // uu = wx (memcpy) on the first inner iteration
+  int solverit;
+  int camlr;
+};
+
+struct UpArgs {
+  const float *flow;  // planar [n][nop][hl][wl]
+  float *out;         // [n][H0][W0][nop]
+  int n, nop, wl, hl, log2s, W0, H0, offx, offy;
+};
+
+void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s);
+void launch_pyr_down(const PyrDownArgs &a, hipStream_t s);
+void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s);
+void launch_patch(const PatchArgs &a, hipStream_t s);
+void launch_aggregate(const AggArgs &a, hipStream_t s);
+void launch_tv_prep(const TvArgs &a, hipStream_t s);
+void launch_tv_deriv1(const TvArgs &a, hipStream_t s);
+void launch_tv_deriv2(const TvArgs &a, hipStream_t s);
+void launch_tv_system(const TvArgs &a, hipStream_t s);
+void launch_tv_sor(const TvArgs &a, hipStream_t s);
+void launch_tv_final(const TvArgs &a, hipStream_t s);
+void launch_upsample(const UpArgs &a, hipStream_t s);
+
+}  // namespace ofdis

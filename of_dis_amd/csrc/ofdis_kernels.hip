@@ -1,0 +1,1064 @@
+// ofdis_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the DIS optical-flow hot path.
+//
+// Every kernel keeps the reference's floating-point evaluation order (no FMA contraction: the file is
+// built with -ffp-contract=off and the pragma below; division and sqrt are the correctly rounded HIP
+// defaults), so results are bit-identical to the CPU restatement in oracle/ and hence, for the
+// variational part, to the reference's own FDF1.0.1 code.
+//
+// Kernels (reference function they replace):
+//   k_pyr_base      run_dense.cpp:299-312 + :151 (divisibility pad + 2^l box mean, exact in fp32)
+//   k_pyr_down      run_dense.cpp:151 (cv::resize .5 = 2x2 mean)
+//   k_pyr_pad_grad  run_dense.cpp:157-178 (Sobel/8 reflect-101 + replicate / zero padding)
+//   k_patch         patch.cpp:55-295 (one wave64 per patch; Eigen-order reductions through LDS)
+//   k_aggregate     patchgrid.cpp:213-275,377-397 (gather form, serial patch order, no atomics)
+//   k_tv_prep       opticalflow_aux.c:31-75 + :88-99 (warp, mask, mean / temporal images)
+//   k_tv_deriv1/2   opticalflow_aux.c:101-107 (5-tap derivative filters)
+//   k_tv_system     opticalflow_aux.c:138-223,408-747 (smoothness + data term + laplacian, LDS tile)
+//   k_tv_sor        solver.c:83-433 / :34-78 / :439-471 (exact lexicographic order as a wavefront)
+//   k_tv_final      refine_variational.cpp:209-227,305-323
+//   k_upsample      run_dense.cpp:407-415 (x2^l, cv::resize INTER_LINEAR, crop)
+#include "ofdis_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace ofdis {
+
+namespace {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ float stdmaxf(float a, float b) { return (a < b) ? b : a; }
+__device__ __forceinline__ float stdminf(float a, float b) { return (b < a) ? b : a; }
+__device__ __forceinline__ float ssemin(float a, float b) { return (a < b) ? a : b; }
+__device__ __forceinline__ float ssemax(float a, float b) { return (a > b) ? a : b; }
+
+inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// ------------------------------------------------------------------------------------------------ pyramid
+
+__global__ __launch_bounds__(256) void k_pyr_base(PyrBaseArgs a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 2L * a.n * a.h * a.w;
+  if (idx >= total) return;
+  const int x = (int)(idx % a.w);
+  const long r = idx / a.w;
+  const int y = (int)(r % a.h);
+  const int f = (int)(r / a.h);
+  const long fs = (long)a.H0 * a.W0 * a.noc;
+  const uint8_t *src = f < a.n ? a.img_a + (long)f * fs : a.img_b + (long)(f - a.n) * fs;
+  const int B = 1 << a.log2s;
+  // 2^l x 2^l box mean of the replicate-padded u8 image.  The sum is an integer < 2^24 and the scale
+  // is a power of two, so this equals the reference's repeated ((a+b)+(c+d))*0.25 exactly (l <= 8).
+  const float scale = 1.0f / (float)(1 << (2 * a.log2s));
+  for (int c = 0; c < a.noc; ++c) {
+    unsigned sum = 0;
+    for (int by = 0; by < B; ++by) {
+      const int yy = clampi(y * B + by - a.padt, 0, a.H0 - 1);
+      const uint8_t *row = src + (long)yy * a.W0 * a.noc + c;
+      for (int bx = 0; bx < B; ++bx) sum += row[clampi(x * B + bx - a.padl, 0, a.W0 - 1) * a.noc];
+    }
+    a.out[idx * a.noc + c] = (float)sum * scale;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.n2 * a.h * a.w * a.noc;
+  if (idx >= total) return;
+  const int c = (int)(idx % a.noc);
+  long r = idx / a.noc;
+  const int x = (int)(r % a.w);
+  r /= a.w;
+  const int y = (int)(r % a.h);
+  const int f = (int)(r / a.h);
+  const int sw = 2 * a.w;
+  const float *s = a.src + (long)f * (2 * a.h) * sw * a.noc;
+  const float p = s[((2 * y) * sw + 2 * x) * a.noc + c], q = s[((2 * y) * sw + 2 * x + 1) * a.noc + c];
+  const float u = s[((2 * y + 1) * sw + 2 * x) * a.noc + c], v = s[((2 * y + 1) * sw + 2 * x + 1) * a.noc + c];
+  a.dst[idx] = ((p + q) + (u + v)) * 0.25f;
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  if (i < 0) return -i;
+  if (i >= n) return 2 * n - 2 - i;
+  return i;
+}
+
+__global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
+  const int W = a.w + 2 * a.pad, H = a.h + 2 * a.pad;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.n2 * H * W;
+  if (idx >= total) return;
+  const int X = (int)(idx % W);
+  const long r = idx / W;
+  const int Y = (int)(r % H);
+  const int f = (int)(r / H);
+  const int sx = X - a.pad, sy = Y - a.pad;
+  const int noc = a.noc, w = a.w;
+  const float *L = a.lvl + (long)f * a.h * a.w * noc;
+  const bool inside = sx >= 0 && sx < a.w && sy >= 0 && sy < a.h;
+  for (int c = 0; c < noc; ++c) {
+    const long o = idx * noc + c;
+    if (inside) {
+      const int xm = reflect101(sx - 1, a.w), xp = reflect101(sx + 1, a.w);
+      const int ym = reflect101(sy - 1, a.h), yp = reflect101(sy + 1, a.h);
+#define PX(xx, yy) L[((yy) * w + (xx)) * noc + c]
+      const float tm = PX(xp, ym) - PX(xm, ym);
+      const float t0 = PX(xp, sy) - PX(xm, sy);
+      const float tp = PX(xp, yp) - PX(xm, yp);
+      const float sm = (PX(xm, ym) + PX(xp, ym)) * 0.125f + PX(sx, ym) * 0.25f;
+      const float sp = (PX(xm, yp) + PX(xp, yp)) * 0.125f + PX(sx, yp) * 0.25f;
+      a.img[o] = PX(sx, sy);
+      a.dx[o] = (tm + tp) * 0.125f + t0 * 0.25f;
+      a.dy[o] = sp - sm;
+#undef PX
+    } else {
+      a.img[o] = L[(clampi(sy, 0, a.h - 1) * w + clampi(sx, 0, a.w - 1)) * noc + c];
+      a.dx[o] = 0.0f;
+      a.dy[o] = 0.0f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ DIS patches
+
+constexpr int kPatchWaves = 4;
+constexpr int kJmax = 7;  // values per lane: novals <= 448 (p = 12, RGB: 432)
+
+// Eigen's SSE redux order (two 4-lane packet accumulators over packet pairs, res0 + res1, odd trailing
+// packet, predux (l0 + l2) + (l1 + l3)).  The R arrays were stored to lds[r * rs + v]; lane (r = lane/8,
+// slot = lane%8) walks its slot's chain v = slot, slot + 8, ... in order, then the 8 lanes of a group
+// combine exactly like the reference's packet tree.  Result r is returned to every lane.
+template <int R>
+__device__ __forceinline__ void eigen_reduce(const float *lds, int rs, int n, int lane, float (&out)[R]) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int r = lane >> 3, s = lane & 7;
+  const int pairs = n >> 3;
+  const bool odd = ((n >> 2) & 1) != 0;
+  float acc = 0.0f, first = 0.0f, tail = 0.0f;
+  if (r < R) {
+    const float *x = lds + r * rs;
+    first = x[s];
+    acc = first;
+    for (int c = 1; c < pairs; ++c) acc = acc + x[s + 8 * c];
+    tail = x[pairs * 8 + s];
+  }
+  const float other = __shfl_down(acc, 4, 64);
+  float rl = pairs > 0 ? acc + other : first;
+  if (odd && pairs > 0) rl = rl + tail;
+  const float t = rl + __shfl_down(rl, 2, 64);
+  const float tot = t + __shfl_down(t, 1, 64);
+#pragma unroll
+  for (int k = 0; k < R; ++k) out[k] = __shfl(tot, k * 8, 64);
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void lds_store(float *lds, int n, int lane, const float (&v)[kJmax], int J) {
+#pragma unroll
+  for (int j = 0; j < kJmax; ++j)
+    if (j < J) {
+      const int e = lane + 64 * j;
+      if (e < n) lds[e] = v[j];
+    }
+}
+
+// Eigen LLT<2x2>::solve: unblocked llt_inplace (stops at a non-positive pivot, leaving raw entries)
+// followed by the unrolled lower and upper triangular solves.
+__device__ __forceinline__ void llt2_solve(float H00, float H01, float H11, float b0, float b1, float &x0,
+                                           float &x1) {
+  float L00 = H00, L10 = H01, L11 = H11;
+  if (!(H00 <= 0.0f)) {
+    L00 = sqrtf(H00);
+    L10 = H01 / L00;
+    const float t = H11 - L10 * L10;
+    if (!(t <= 0.0f)) L11 = sqrtf(t);
+  }
+  const float y0 = b0 / L00;
+  const float y1 = (b1 - L10 * y0) / L11;
+  x1 = y1 / L11;
+  x0 = (y0 - L10 * x1) / L00;
+}
+
+__device__ __forceinline__ float llt1_solve(float H, float b) {
+  float L = H;
+  if (!(H <= 0.0f)) L = sqrtf(H);
+  const float y = b / L;
+  return y / L;
+}
+
+struct PatchCtx {
+  const float *B;
+  int W, noc, p, pad, novals, J, lane, rs, costfct, patnorm, nop;
+  float *lds;
+  int offs[kJmax];
+};
+
+// getPatchStaticBil (patch.cpp:345-413) + mean normalisation + LossComputeErrorImage (patch.cpp:221-273).
+// Leaves pdiff/pweight per lane and returns Eigen sums of |pweight|, dx*pdiff, dy*pdiff.
+template <int NOP>
+__device__ __forceinline__ void patch_eval(const PatchCtx &c, float mx, float my, const float (&tmp)[kJmax],
+                                           const float (&gx)[kJmax], const float (&gy)[kJmax],
+                                           float (&pd)[kJmax], float (&pw)[kJmax], float (&red)[NOP + 1]) {
+  const int pos0 = (int)ceilf(mx + 0.00001f) + c.pad;
+  const int pos1 = (int)ceilf(my + 0.00001f) + c.pad;
+  const int pos2 = (int)floorf(mx), pos3 = (int)floorf(my);
+  const float rx = mx - (float)pos2, ry = my - (float)pos3;
+  const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+  const long base = ((long)(pos1 - c.p / 2) * c.W + (pos0 - c.p / 2)) * c.noc;
+  const long rowstep = (long)c.W * c.noc;
+#pragma unroll
+  for (int j = 0; j < kJmax; ++j)
+    if (j < c.J) {
+      if (c.lane + 64 * j < c.novals) {
+        const float *q = c.B + base + c.offs[j];
+        const float A = q[0], Bv = q[-c.noc], C = q[-rowstep], D = q[-rowstep - c.noc];
+        pd[j] = w0 * A + w1 * Bv + w2 * C + w3 * D;
+      } else {
+        pd[j] = 0.0f;
+      }
+    }
+  if (c.patnorm > 0) {
+    lds_store(c.lds, c.novals, c.lane, pd, c.J);
+    float s[1];
+    eigen_reduce<1>(c.lds, c.rs, c.novals, c.lane, s);
+    const float mean = s[0] / (float)c.novals;
+#pragma unroll
+    for (int j = 0; j < kJmax; ++j)
+      if (j < c.J) pd[j] = pd[j] - mean;
+  }
+  float ab[kJmax], px[kJmax], py[kJmax];
+#pragma unroll
+  for (int j = 0; j < kJmax; ++j)
+    if (j < c.J) {
+      const float d = pd[j] - tmp[j];
+      float w;
+      if (c.costfct == 0) {
+        pd[j] = d;
+        w = fabsf(d);
+      } else if (c.costfct == 1) {
+        w = sqrtf(fabsf(d));
+        pd[j] = copysignf(w, d);
+      } else {
+        w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        pd[j] = copysignf(w, d);
+      }
+      pw[j] = w;
+      ab[j] = fabsf(w);
+      px[j] = gx[j] * pd[j];
+      py[j] = gy[j] * pd[j];
+    }
+  lds_store(c.lds, c.novals, c.lane, ab, c.J);
+  lds_store(c.lds + c.rs, c.novals, c.lane, px, c.J);
+  if (NOP == 2) lds_store(c.lds + 2 * c.rs, c.novals, c.lane, py, c.J);
+  eigen_reduce<NOP + 1>(c.lds, c.rs, c.novals, c.lane, red);
+}
+
+template <int NOP>
+__global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_all[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const LevelGeom &g = a.g;
+  const long gp = (long)blockIdx.x * kPatchWaves + wid;
+  if (gp >= (long)a.n * g.npatch) return;  // whole wave exits; kernel uses no block barrier
+  const int f = (int)(gp / g.npatch), ip = (int)(gp % g.npatch);
+  const int pxi = ip / g.noph, pyi = ip % g.noph;
+  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+  const long fs = (long)g.W * g.H * a.noc;
+
+  PatchCtx c;
+  c.B = a.img_b + f * fs;
+  c.W = g.W; c.noc = a.noc; c.p = a.p; c.pad = g.pad; c.novals = a.novals;
+  c.J = (a.novals + 63) >> 6; c.lane = lane; c.costfct = a.costfct; c.patnorm = a.patnorm; c.nop = NOP;
+  c.rs = ((a.novals + 31) / 32) * 32 + 8;
+  c.lds = lds_all + wid * 3 * c.rs;
+#pragma unroll
+  for (int j = 0; j < kJmax; ++j) {
+    const int e = lane + 64 * j;
+    const int ch = e % a.noc, q = e / a.noc;
+    c.offs[j] = ((q / a.p) * g.W + (q % a.p)) * a.noc + ch;
+  }
+
+  // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
+  float tmp[kJmax], gx[kJmax], gy[kJmax], pd[kJmax], pw[kJmax];
+  {
+    const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
+    const long base = ((long)(py - a.p / 2) * g.W + (px - a.p / 2)) * a.noc;
+    const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
+#pragma unroll
+    for (int j = 0; j < kJmax; ++j) {
+      const bool ok = j < c.J && lane + 64 * j < a.novals;
+      tmp[j] = ok ? A[c.offs[j]] : 0.0f;
+      gx[j] = ok ? DX[c.offs[j]] : 0.0f;
+      gy[j] = ok ? DY[c.offs[j]] : 0.0f;
+      pd[j] = 0.0f;
+      pw[j] = 0.0f;
+    }
+  }
+  if (a.patnorm > 0) {
+    lds_store(c.lds, a.novals, lane, tmp, c.J);
+    float s[1];
+    eigen_reduce<1>(c.lds, c.rs, a.novals, lane, s);
+    const float mean = s[0] / (float)a.novals;
+#pragma unroll
+    for (int j = 0; j < kJmax; ++j)
+      if (j < c.J) tmp[j] = tmp[j] - mean;
+  }
+  // ---- ComputeHessian (patch.cpp:69-86)
+  float H00, H01 = 0.0f, H11 = 0.0f;
+  {
+    float q0[kJmax], q1[kJmax], q2[kJmax];
+#pragma unroll
+    for (int j = 0; j < kJmax; ++j) {
+      q0[j] = gx[j] * gx[j];
+      q1[j] = gx[j] * gy[j];
+      q2[j] = gy[j] * gy[j];
+    }
+    lds_store(c.lds, a.novals, lane, q0, c.J);
+    if (NOP == 2) {
+      lds_store(c.lds + c.rs, a.novals, lane, q1, c.J);
+      lds_store(c.lds + 2 * c.rs, a.novals, lane, q2, c.J);
+      float h[3];
+      eigen_reduce<3>(c.lds, c.rs, a.novals, lane, h);
+      H00 = h[0]; H01 = h[1]; H11 = h[2];
+      if (H00 * H11 - H01 * H01 == 0.0f) {
+        H00 = (float)((double)H00 + 1e-10);
+        H11 = (float)((double)H11 + 1e-10);
+      }
+    } else {
+      float h[1];
+      eigen_reduce<1>(c.lds, c.rs, a.novals, lane, h);
+      H00 = h[0];
+      if (H00 == 0.0f) H00 = (float)((double)H00 + 1e-10);
+    }
+  }
+  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
+  float pin0 = 0.0f, pin1 = 0.0f;
+  if (a.prev) {
+    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
+    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
+    pin0 = pv[0] * 2;
+    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  // ---- OptimizeStart (patch.cpp:117-154)
+  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
+  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
+  const float st0 = pt0, st1 = pt1;
+  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
+  int cnt = 0;
+  bool converged = false;
+  float b0 = 0.0f, b1 = 0.0f;
+  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  auto err = [&]() {  // OptimizeComputeErrImg (patch.cpp:275-295)
+    float red[NOP + 1];
+    patch_eval<NOP>(c, pt0, pt1, tmp, gx, gy, pd, pw, red);
+    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+    if (cnt == 1) sq_init = sq;
+    mares_old = mares;
+    mares = red[0] / (float)a.novals;
+    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+    if (!keep) converged = true;
+    b0 = red[1];
+    if (NOP == 2) b1 = red[NOP];
+  };
+  if (oob(pt0, pt1)) {
+    converged = true;
+#pragma unroll
+    for (int j = 0; j < kJmax; ++j) pw[j] = 0.0f;  // never written upstream; defined as 0
+  } else {
+    mares = 1e5f;
+    err();
+  }
+  // ---- OptimizeIter loop (patch.cpp:156-210)
+  while (!converged) {
+    ++cnt;
+    if (NOP == 2) {
+      llt2_solve(H00, H01, H11, b0, b1, d0, d1);
+      p0 = p0 - d0;
+      p1 = p1 - d1;
+    } else {
+      d0 = llt1_solve(H00, b0);
+      p0 = p0 - d0;
+      p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+    }
+    pt0 = ptr0 + p0;
+    if (NOP == 2) pt1 = ptr1 + p1;
+    const float ex = st0 - pt0, ey = st1 - pt1;
+    if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+      p0 = pin0;
+      p1 = pin1;
+      pt0 = ptr0 + p0;
+      if (NOP == 2) pt1 = ptr1 + p1;
+      converged = true;
+    }
+    err();
+  }
+  // ---- outputs
+  if (lane < NOP) a.p_iter[gp * NOP + lane] = lane == 0 ? p0 : p1;
+  float *pwo = a.pweight + gp * a.novals;
+#pragma unroll
+  for (int j = 0; j < kJmax; ++j)
+    if (j < c.J && lane + 64 * j < a.novals) pwo[lane + 64 * j] = pw[j];
+}
+
+// ------------------------------------------------------------------------------------------------ aggregation
+
+__device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+__global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
+  const LevelGeom &g = a.g;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.n * g.w * g.h;
+  if (idx >= total) return;
+  const int x = (int)(idx % g.w);
+  const long r = idx / g.w;
+  const int y = (int)(r % g.h);
+  const int f = (int)(r / g.h);
+  const int hp = a.p / 2;
+  // patches whose footprint [pt - p/2, pt + p/2 - 1] covers x, visited in ascending patch id
+  const int pxlo = max(0, -floordiv(-(x - hp + 1 - g.offw), a.steps));
+  const int pxhi = min(g.nopw - 1, floordiv(x + hp - g.offw, a.steps));
+  const int pylo = max(0, -floordiv(-(y - hp + 1 - g.offh), a.steps));
+  const int pyhi = min(g.noph - 1, floordiv(y + hp - g.offh, a.steps));
+  float we = 0.0f, f0 = 0.0f, f1 = 0.0f;
+  const float *PI = a.p_iter + (long)f * g.npatch * a.nop;
+  const float *PW = a.pweight + (long)f * g.npatch * a.novals;
+  for (int px = pxlo; px <= pxhi; ++px) {
+    const int ptx = px * a.steps + g.offw;
+    const int lx = x - ptx + hp;
+    for (int py = pylo; py <= pyhi; ++py) {
+      const int pty = py * a.steps + g.offh;
+      const int ly = y - pty + hp;
+      const int ip = px * g.noph + py;
+      const float *pw = PW + (long)ip * a.novals;
+      float absw;
+      if (a.noc == 1) {
+        absw = 1.0f / stdmaxf(2.0f, pw[ly * a.p + lx]);
+      } else {
+        // upstream weight pointer advances by 1 for out-of-image pixels and by 3 inside (patchgrid.cpp:243,256-258)
+        const int lx0 = max(0, hp - ptx), lx1 = min(a.p, g.w - ptx + hp);
+        const int ly0 = max(0, hp - pty), ly1 = min(a.p, g.h - pty + hp);
+        const int nin = lx1 - lx0;
+        int before_in = max(0, min(ly, ly1) - ly0) * nin;
+        if (ly >= ly0 && ly < ly1) before_in += max(0, min(lx, lx1) - lx0);
+        const int off = ly * a.p + lx + 2 * before_in;
+        absw = stdmaxf(2.0f, pw[off]);
+        absw = absw + stdmaxf(2.0f, pw[off + 1]);
+        absw = absw + stdmaxf(2.0f, pw[off + 2]);
+        absw = 1.0f / absw;
+      }
+      we = we + absw;
+      f0 = f0 + PI[ip * a.nop] * absw;
+      if (a.nop == 2) f1 = f1 + PI[ip * a.nop + 1] * absw;
+    }
+  }
+  if (we > 0) {
+    f0 = f0 / we;
+    f1 = f1 / we;
+  }
+  const long plane = (long)g.w * g.h;
+  float *fl = a.flow + (long)f * a.nop * plane + (long)y * g.w + x;
+  fl[0] = f0;
+  if (a.nop == 2) fl[plane] = f1;
+}
+
+// ------------------------------------------------------------------------------------------------ variational
+
+__global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long plane = (long)a.w * a.h;
+  if (idx >= (long)a.n * plane) return;
+  const int f = (int)(idx / plane);
+  const long o = idx % plane;
+  const int x = (int)(o % a.w), y = (int)(o / a.w);
+  const float wx = a.flow[(long)f * a.nop * plane + o];
+  const float wy = a.nop == 2 ? a.flow[(long)f * a.nop * plane + plane + o] : 0.0f;
+  const float xx = (float)x + wx, yy = (float)y + wy;
+  const int xi = (int)floorf(xx), yi = (int)floorf(yy);
+  const float dx = xx - (float)xi, dy = yy - (float)yi;
+  a.mask[idx] = (xx >= 0 && xx <= (float)(a.w - 1) && yy >= 0 && yy <= (float)(a.h - 1)) ? 1.0f : 0.0f;
+  const int x1 = clampi(xi, 0, a.w - 1), x2 = clampi(xi + 1, 0, a.w - 1);
+  const int y1 = clampi(yi, 0, a.h - 1), y2 = clampi(yi + 1, 0, a.h - 1);
+  const long fs = (long)a.W * (a.h + 2 * a.pad) * a.noc;
+  const float *B = a.img_b + f * fs, *A = a.img_a + f * fs;
+#define SB(xq, yq) B[((long)((yq) + a.pad) * a.W + (xq) + a.pad) * a.noc + ch]
+  for (int ch = 0; ch < a.noc; ++ch) {
+    const float w2 = SB(x1, y1) * (1.0f - dx) * (1.0f - dy) + SB(x2, y1) * dx * (1.0f - dy) +
+                     SB(x1, y2) * (1.0f - dx) * dy + SB(x2, y2) * dx * dy;
+    const float i1 = A[((long)(y + a.pad) * a.W + x + a.pad) * a.noc + ch];
+    const long q = ((long)f * a.noc + ch) * plane + o;
+    a.t[q] = 0.5f * (w2 + i1);
+    a.dt[q] = w2 - i1;
+  }
+#undef SB
+  a.du[idx] = 0.0f;
+  if (a.nop == 2) a.dv[idx] = 0.0f;
+}
+
+__constant__ float kK5[5] = {1.0f / 12.0f, -8.0f / 12.0f, -0.0f, 8.0f / 12.0f, -1.0f / 12.0f};
+__constant__ float kK3[3] = {-0.5f, -0.0f, 0.5f};
+
+__device__ __forceinline__ float conv5h(const float *s, int x, int y, int w) {
+  const float *r = s + (long)y * w;
+  const float s0 = r[clampi(x - 2, 0, w - 1)], s1 = r[clampi(x - 1, 0, w - 1)], s2 = r[x];
+  const float s3 = r[clampi(x + 1, 0, w - 1)], s4 = r[clampi(x + 2, 0, w - 1)];
+  return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
+}
+__device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int h) {
+  const float s0 = s[(long)clampi(y - 2, 0, h - 1) * w + x], s1 = s[(long)clampi(y - 1, 0, h - 1) * w + x];
+  const float s2 = s[(long)y * w + x];
+  const float s3 = s[(long)clampi(y + 1, 0, h - 1) * w + x], s4 = s[(long)clampi(y + 2, 0, h - 1) * w + x];
+  return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
+}
+
+__global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
+  const long plane = (long)a.w * a.h;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)a.n * a.noc * plane) return;
+  const long pl = idx / plane, o = idx % plane;
+  const int x = (int)(o % a.w), y = (int)(o / a.w);
+  const float *t = a.t + pl * plane, *dt = a.dt + pl * plane;
+  a.Ix[idx] = conv5h(t, x, y, a.w);
+  a.Iy[idx] = conv5v(t, x, y, a.w, a.h);
+  a.Ixz[idx] = conv5h(dt, x, y, a.w);
+  a.Iyz[idx] = conv5v(dt, x, y, a.w, a.h);
+}
+
+__global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
+  const long plane = (long)a.w * a.h;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)a.n * a.noc * plane) return;
+  const long pl = idx / plane, o = idx % plane;
+  const int x = (int)(o % a.w), y = (int)(o / a.w);
+  a.Ixx[idx] = conv5h(a.Ix + pl * plane, x, y, a.w);
+  a.Ixy[idx] = conv5v(a.Ix + pl * plane, x, y, a.w, a.h);
+  a.Iyy[idx] = conv5v(a.Iy + pl * plane, x, y, a.w, a.h);
+}
+
+#define DNORM (0.1f * 0.1f)
+#define EPSC (0.001f * 0.001f)
+
+// compute_data (opticalflow_aux.c:408-594), one pixel; p* point at the pixel in channel plane 0.
+__device__ __forceinline__ void data_of(int noc, long plane, float u, float v, float m, const float *Ix,
+                                        const float *Iy, const float *Iz, const float *Ixx, const float *Ixy,
+                                        const float *Iyy, const float *Ixz, const float *Iyz, float hdo3, float hgo3,
+                                        float &A11, float &A12, float &A22, float &B1, float &B2) {
+  A11 = 0.0f; A12 = 0.0f; A22 = 0.0f; B1 = 0.0f; B2 = 0.0f;
+  float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
+  if (noc == 1) {
+    if (hdo3 != 0.0f) {
+      tmpx = Ix[0]; tmpy = Iy[0];
+      tmp2 = (Iz[0] + tmpx * u) + tmpy * v;
+      n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+      tmp = (tmp2 * tmp2) / n1;
+      tmp = (m * hdo3) / sqrtf(EPSC + 3.0f * tmp);
+      tmp3 = tmp / n1;
+      tmp2 = tmp3 * tmpx;
+      tmp3 = tmp3 * tmpy;
+      A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+      B1 = B1 - tmp2 * Iz[0]; B2 = B2 - tmp3 * Iz[0];
+    }
+    tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
+    tmp2 = (Ixz[0] + tmpx * u) + tmpxy * v;
+    tmp3 = (Iyz[0] + tmpxy * u) + tmpy * v;
+    tmpxy = tmpxy * tmpxy;
+    n1 = (tmpxy + DNORM) + tmpx * tmpx;
+    n2 = (tmpxy + DNORM) + tmpy * tmpy;
+    tmp = (tmp2 * tmp2) / n1 + (tmp3 * tmp3) / n2;
+    tmp = (m * hgo3) / sqrtf(EPSC + 3.0f * tmp);
+    tmp2 = tmp / n2; tmp3 = tmp / n1;
+    tmpxy = Ixy[0];
+    A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+    B1 = (B1 - (tmp3 * tmpx) * Ixz[0]) - (tmp2 * tmpxy) * Iyz[0];
+    B2 = (B2 - (tmp2 * tmpy) * Iyz[0]) - (tmp3 * tmpxy) * Ixz[0];
+    tmpxy = tmpxy * tmpxy;
+    A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+    A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+    A11 = A11 * 3.0f; A12 = A12 * 3.0f; A22 = A22 * 3.0f; B1 = B1 * 3.0f; B2 = B2 * 3.0f;
+    return;
+  }
+  const long o2 = plane, o3 = 2 * plane;
+  float n3, n4, n5, n6;
+  if (hdo3 != 0.0f) {
+    tmpx = Ix[0]; tmpy = Iy[0];
+    tmp2 = (Iz[0] + tmpx * u) + tmpy * v;
+    n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+    tmp = (tmp2 * tmp2) / n1;
+    tmpx = Ix[o2]; tmpy = Iy[o2];
+    tmp2 = (Iz[o2] + tmpx * u) + tmpy * v;
+    n2 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+    tmp = tmp + (tmp2 * tmp2) / n2;
+    tmpx = Ix[o3]; tmpy = Iy[o3];
+    tmp2 = (Iz[o3] + tmpx * u) + tmpy * v;
+    n3 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
+    tmp = tmp + (tmp2 * tmp2) / n3;
+    tmp = (m * hdo3) / sqrtf(EPSC + tmp);
+    tmp3 = tmp / n3; tmp2 = tmp3 * tmpx; tmp3 = tmp3 * tmpy;
+    A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+    B1 = B1 - tmp2 * Iz[o3]; B2 = B2 - tmp3 * Iz[o3];
+    tmpx = Ix[o2]; tmpy = Iy[o2];
+    tmp3 = tmp / n2; tmp2 = tmp3 * tmpx; tmp3 = tmp3 * tmpy;
+    A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+    B1 = B1 - tmp2 * Iz[o2]; B2 = B2 - tmp3 * Iz[o2];
+    tmpx = Ix[0]; tmpy = Iy[o2];  // upstream slip: channel 2's Iy (opticalflow_aux.c:495-496)
+    tmp3 = tmp / n1; tmp2 = tmp3 * tmpx; tmp3 = tmp3 * tmpy;
+    A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
+    B1 = B1 - tmp2 * Iz[0]; B2 = B2 - tmp3 * Iz[0];
+  }
+  tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
+  tmp2 = (Ixz[0] + tmpx * u) + tmpxy * v;
+  tmp3 = (Iyz[0] + tmpxy * u) + tmpy * v;
+  tmpxy = tmpxy * tmpxy;
+  n1 = (tmpxy + DNORM) + tmpx * tmpx;
+  n2 = (tmpxy + DNORM) + tmpy * tmpy;
+  tmp = (tmp2 * tmp2) / n1 + (tmp3 * tmp3) / n2;
+  tmpx = Ixx[o2]; tmpy = Iyy[o2]; tmpxy = Ixy[o2];
+  tmp2 = (Ixz[o2] + tmpx * u) + tmpxy * v;
+  tmp3 = (Iyz[o2] + tmpxy * u) + tmpy * v;
+  tmpxy = tmpxy * tmpxy;
+  n3 = (tmpxy + DNORM) + tmpx * tmpx;
+  n4 = (tmpxy + DNORM) + tmpy * tmpy;
+  tmp = (tmp2 * tmp2) / n3 + (tmp3 * tmp3) / n4;  // upstream overwrite (opticalflow_aux.c:519,529,538)
+  tmpx = Ixx[o3]; tmpy = Iyy[o3]; tmpxy = Ixy[o3];
+  tmp2 = (Ixz[o3] + tmpx * u) + tmpxy * v;
+  tmp3 = (Iyz[o3] + tmpxy * u) + tmpy * v;
+  tmpxy = tmpxy * tmpxy;
+  n5 = (tmpxy + DNORM) + tmpx * tmpx;
+  n6 = (tmpxy + DNORM) + tmpy * tmpy;
+  tmp = (tmp2 * tmp2) / n5 + (tmp3 * tmp3) / n6;
+  tmp = (m * hgo3) / sqrtf(EPSC + tmp);
+  tmp2 = tmp / n6; tmp3 = tmp / n5;
+  A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+  A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+  tmpxy = Ixy[o3];
+  A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+  B1 = (B1 - (tmp3 * tmpx) * Ixz[o3]) - (tmp2 * tmpxy) * Iyz[o3];
+  B2 = (B2 - (tmp2 * tmpy) * Iyz[o3]) - (tmp3 * tmpxy) * Ixz[o3];
+  tmp2 = tmp / n4; tmp3 = tmp / n3;
+  tmpx = Ixx[o2]; tmpy = Iyy[o2]; tmpxy = Ixy[o2];
+  A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+  B1 = (B1 - (tmp3 * tmpx) * Ixz[o2]) - (tmp2 * tmpxy) * Iyz[o2];
+  B2 = (B2 - (tmp2 * tmpy) * Iyz[o2]) - (tmp3 * tmpxy) * Ixz[o2];
+  tmpxy = tmpxy * tmpxy;
+  A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+  A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+  tmpx = Ixx[0]; tmpy = Iyy[0];
+  tmp2 = tmp / n2; tmp3 = tmp / n1;
+  tmpxy = Ixy[0];
+  A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
+  B1 = (B1 - (tmp3 * tmpx) * Ixz[0]) - (tmp2 * tmpxy) * Iyz[0];
+  B2 = (B2 - (tmp2 * tmpy) * Iyz[0]) - (tmp3 * tmpxy) * Ixz[0];
+  tmpxy = tmpxy * tmpxy;
+  A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
+  A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
+}
+
+// compute_data_DE (opticalflow_aux.c:601-747), one pixel.
+__device__ __forceinline__ void data_de(int noc, long plane, float u, float m, const float *Ix, const float *Iy,
+                                        const float *Iz, const float *Ixx, const float *Ixy, const float *Iyy,
+                                        const float *Ixz, const float *Iyz, float hdo3, float hgo3, float &A11,
+                                        float &B1) {
+  A11 = 0.0f; B1 = 0.0f;
+  float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
+  if (noc == 1) {
+    if (hdo3 != 0.0f) {
+      tmpx = Ix[0]; tmpy = Iy[0];
+      tmp2 = Iz[0] + tmpx * u;
+      n1 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+      tmp = (tmp2 * tmp2) / n1;
+      tmp = (m * hdo3) / sqrtf(EPSC + 3.0f * tmp);
+      tmp2 = (tmp / n1) * tmpx;
+      A11 = A11 + tmp2 * tmpx;
+      B1 = B1 - tmp2 * Iz[0];
+    }
+    tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
+    tmp2 = Iyz[0] + tmpxy * u;
+    tmpxy = DNORM + tmpxy * tmpxy;
+    n1 = tmpxy + tmpx * tmpx;
+    n2 = tmpxy + tmpy * tmpy;
+    tmp = (tmp2 * tmp2) / n2;
+    tmp2 = Ixz[0] + tmpx * u;
+    tmp = tmp + (tmp2 * tmp2) / n1;
+    tmp = (m * hgo3) / sqrtf(EPSC + 3.0f * tmp);
+    tmpxy = Ixy[0];
+    tmp2 = (tmp / n2) * tmpxy; tmp3 = (tmp / n1) * tmpx;
+    A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+    B1 = (B1 - tmp3 * Ixz[0]) - tmp2 * Iyz[0];
+    A11 = A11 * 3.0f; B1 = B1 * 3.0f;
+    return;
+  }
+  const long o2 = plane, o3 = 2 * plane;
+  float n3, n4, n5, n6;
+  if (hdo3 != 0.0f) {
+    tmpx = Ix[0]; tmpy = Iy[0];
+    tmp2 = Iz[0] + tmpx * u;
+    n1 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+    tmp = (tmp2 * tmp2) / n1;
+    tmpx = Ix[o2]; tmpy = Iy[o2];
+    tmp2 = Iz[o2] + tmpx * u;
+    n2 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+    tmp = tmp + (tmp2 * tmp2) / n2;
+    tmpx = Ix[o3]; tmpy = Iy[o3];
+    tmp2 = Iz[o3] + tmpx * u;
+    n3 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
+    tmp = tmp + (tmp2 * tmp2) / n3;
+    tmp = (m * hdo3) / sqrtf(EPSC + tmp);
+    tmp2 = (tmp / n3) * tmpx;
+    A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[o3];
+    tmpx = Ix[o2];
+    tmp2 = (tmp / n2) * tmpx;
+    A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[o2];
+    tmpx = Ix[0];
+    tmp2 = (tmp / n1) * tmpx;
+    A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[0];
+  }
+  tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
+  tmp2 = Iyz[0] + tmpxy * u;
+  tmpxy = DNORM + tmpxy * tmpxy;
+  n1 = tmpxy + tmpx * tmpx;
+  n2 = tmpxy + tmpy * tmpy;
+  tmp = (tmp2 * tmp2) / n2;
+  tmp2 = Ixz[0] + tmpx * u;
+  tmp = tmp + (tmp2 * tmp2) / n1;
+  tmpx = Ixx[o2]; tmpy = Iyy[o2]; tmpxy = Ixy[o2];
+  tmp2 = Iyz[o2] + tmpxy * u;
+  tmpxy = DNORM + tmpxy * tmpxy;
+  n3 = tmpxy + tmpx * tmpx;
+  n4 = tmpxy + tmpy * tmpy;
+  tmp = tmp + (tmp2 * tmp2) / n4;
+  tmp2 = Ixz[o2] + tmpx * u;
+  tmp = tmp + (tmp2 * tmp2) / n3;
+  tmpx = Ixx[o3]; tmpy = Iyy[o3]; tmpxy = Ixy[o3];
+  tmp2 = Iyz[o3] + tmpxy * u;
+  tmpxy = DNORM + tmpxy * tmpxy;
+  n5 = tmpxy + tmpx * tmpx;
+  n6 = tmpxy + tmpy * tmpy;
+  tmp = tmp + (tmp2 * tmp2) / n6;
+  tmp2 = Ixz[o3] + tmpx * u;
+  tmp = tmp + (tmp2 * tmp2) / n5;
+  tmp = (m * hgo3) / sqrtf(EPSC + tmp);
+  tmpxy = Ixy[o3];
+  tmp2 = (tmp / n6) * tmpxy; tmp3 = (tmp / n5) * tmpx;
+  A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+  B1 = (B1 - tmp3 * Ixz[o3]) - tmp2 * Iyz[o3];
+  tmpx = Ixx[o2]; tmpxy = Ixy[o2];
+  tmp2 = (tmp / n4) * tmpxy; tmp3 = (tmp / n3) * tmpx;
+  A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+  B1 = (B1 - tmp3 * Ixz[o2]) - tmp2 * Iyz[o2];
+  tmpx = Ixx[0]; tmpxy = Ixy[0];
+  tmp2 = (tmp / n2) * tmpxy; tmp3 = (tmp / n1) * tmpx;
+  A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
+  B1 = (B1 - tmp3 * Ixz[0]) - tmp2 * Iyz[0];
+}
+
+constexpr int kTX = 32, kTY = 8;
+
+// One TV inner iteration's system assembly (refine_variational.cpp:195-199): smoothness weights
+// (compute_smoothness) from an LDS tile of uu/vv with a 2-pixel halo, data term, and laplacian.
+template <int NOP>
+__global__ __launch_bounds__(kTX *kTY) void k_tv_system(TvArgs a) {
+  __shared__ float su[kTY + 4][kTX + 4], svv[kTY + 4][kTX + 4];
+  __shared__ float ss[kTY + 2][kTX + 2];
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY, f = blockIdx.z;
+  const int w = a.w, h = a.h;
+  const long plane = (long)w * h, fo = (long)f * plane;
+  const float *WX = a.flow + (long)f * NOP * plane, *WY = WX + plane;
+  const int tid = threadIdx.x;
+  for (int k = tid; k < (kTY + 4) * (kTX + 4); k += kTX * kTY) {
+    const int i = k % (kTX + 4), j = k / (kTX + 4);
+    const int gx = clampi(x0 - 2 + i, 0, w - 1), gy = clampi(y0 - 2 + j, 0, h - 1);
+    const long o = (long)gy * w + gx;
+    const float wx = WX[o];
+    float uu, vv;
+    if (NOP == 2) {
+      const float wy = WY[o];
+      uu = a.first_iter ? wx : wx + a.du[fo + o];
+      vv = a.first_iter ? wy : wy + a.dv[fo + o];
+    } else {
+      uu = a.first_iter ? wx : (a.camlr == 0 ? ssemin(wx + a.du[fo + o], 0.0f) : ssemax(wx + a.du[fo + o], 0.0f));
+      vv = 0.0f;  // wy_dummy (refine_variational.cpp:268,294)
+    }
+    su[j][i] = uu;
+    svv[j][i] = vv;
+  }
+  __syncthreads();
+  const float eps = 0.001f * 0.001f;
+  for (int k = tid; k < (kTY + 2) * (kTX + 2); k += kTX * kTY) {
+    const int i = k % (kTX + 2), j = k / (kTX + 2);
+    // s at (x0 - 1 + i, y0 - 1 + j): 3-tap central differences of the replicate-clamped tile
+    const float ux = kK3[0] * su[j + 1][i] + (kK3[1] * su[j + 1][i + 1] + kK3[2] * su[j + 1][i + 2]);
+    const float uy = kK3[0] * su[j][i + 1] + (kK3[1] * su[j + 1][i + 1] + kK3[2] * su[j + 2][i + 1]);
+    const float vx = kK3[0] * svv[j + 1][i] + (kK3[1] * svv[j + 1][i + 1] + kK3[2] * svv[j + 1][i + 2]);
+    const float vy = kK3[0] * svv[j][i + 1] + (kK3[1] * svv[j + 1][i + 1] + kK3[2] * svv[j + 2][i + 1]);
+    ss[j][i] = a.quarter_alpha / sqrtf(eps + ((ux * ux + uy * uy) + (vx * vx + vy * vy)));
+  }
+  __syncthreads();
+  const int tx = tid % kTX, ty = tid / kTX;
+  const int x = x0 + tx, y = y0 + ty;
+  if (x >= w || y >= h) return;
+  const long o = (long)y * w + x;
+  const float sc = ss[ty + 1][tx + 1];
+  const float shv = x < w - 1 ? sc + ss[ty + 1][tx + 2] : 0.0f;
+  const float svv_ = y < h - 1 ? sc + ss[ty + 2][tx + 1] : 0.0f;
+  const float shl = ss[ty + 1][tx] + sc;   // h[x-1] = s[x-1] + s[x]
+  const float svu = ss[ty][tx + 1] + sc;   // v[y-1] = s[y-1] + s[y]
+  const long q = (long)f * a.noc * plane + o;
+  const float m = a.mask[fo + o];
+  float A11, A12 = 0.0f, A22 = 0.0f, B1, B2 = 0.0f;
+  if (NOP == 2)
+    data_of(a.noc, plane, a.du[fo + o], a.dv[fo + o], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q,
+            a.Iyy + q, a.Ixz + q, a.Iyz + q, a.hdo3, a.hgo3, A11, A12, A22, B1, B2);
+  else
+    data_de(a.noc, plane, a.du[fo + o], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q, a.Iyy + q,
+            a.Ixz + q, a.Iyz + q, a.hdo3, a.hgo3, A11, B1);
+  // sub_laplacian (opticalflow_aux.c:194-223): b = ((((b - th[x-1]) + th[x]) - tv[y-1]) + tv[y])
+  {
+    const float c0 = WX[o];
+    if (x >= 1) B1 = B1 - shl * (c0 - WX[o - 1]);
+    if (x <= w - 2) B1 = B1 + shv * (WX[o + 1] - c0);
+    if (y >= 1) B1 = B1 - svu * (c0 - WX[o - w]);
+    if (y <= h - 2) B1 = B1 + svv_ * (WX[o + w] - c0);
+  }
+  if (NOP == 2) {
+    const float c0 = WY[o];
+    if (x >= 1) B2 = B2 - shl * (c0 - WY[o - 1]);
+    if (x <= w - 2) B2 = B2 + shv * (WY[o + 1] - c0);
+    if (y >= 1) B2 = B2 - svu * (c0 - WY[o - w]);
+    if (y <= h - 2) B2 = B2 + svv_ * (WY[o + w] - c0);
+  }
+  a.a11[fo + o] = A11;
+  a.b1[fo + o] = B1;
+  if (NOP == 2) {
+    a.a12[fo + o] = A12;
+    a.a22[fo + o] = A22;
+    a.b2[fo + o] = B2;
+  }
+  a.sh[fo + o] = shv;
+  a.sv[fo + o] = svv_;
+}
+
+// Exact lexicographic Gauss-Seidel SOR as an anti-diagonal wavefront (one workgroup per frame).
+// Pixel (x, y) of sweep s runs at step t = x + y + 2 s: its left/top neighbours of the same sweep ran at
+// t-1, its right/bottom neighbours of the previous sweep at t-1, and no two pixels of one step touch
+// each other (parity), so in-place updates with one barrier per step reproduce solver.c's raster order
+// bit for bit.  MODE 0: sor_coupled block SOR (solver.c:83-433); 1: its point-SOR fallback for
+// width < 2 or height < 2 (solver.c:34-78); 2: sor_coupled_slow_but_readable_DE (solver.c:439-471).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
+  const int f = blockIdx.x;
+  const int w = a.w, h = a.h, S = a.solverit;
+  const long fo = (long)f * w * h;
+  float *du = a.du + fo, *dv = a.dv + fo, *a11 = a.a11 + fo, *a12 = a.a12 + fo, *a22 = a.a22 + fo;
+  const float *b1 = a.b1 + fo, *b2 = a.b2 + fo, *hh = a.sh + fo, *vv = a.sv + fo;
+  const float omega = a.omega;
+  const int items = S * h;
+  const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
+  for (int t = 0; t < T; ++t) {
+    for (int k = threadIdx.x; k < items; k += blockDim.x) {
+      const int s = k / h, y = k - s * h;
+      const int x = t - y - 2 * s;
+      if (x < 0 || x >= w) continue;
+      const long o = (long)y * w + x;
+      if (MODE == 0) {
+        const float hl = x > 0 ? hh[o - 1] : 0.0f, hr = hh[o];
+        const float ur = x < w - 1 ? du[o + 1] : 0.0f, vr = x < w - 1 ? dv[o + 1] : 0.0f;
+        float s1, s2, dpsis;
+        if (y == 0) {
+          dpsis = hl + (hr + vv[o]);
+          s1 = (b1[o] + hr * ur) + vv[o] * du[o + w];
+          s2 = (b2[o] + hr * vr) + vv[o] * dv[o + w];
+        } else if (y < h - 1) {
+          const float vt = vv[o - w];
+          dpsis = (hl + hr) + (vt + vv[o]);
+          s1 = ((hr * ur) + vt * du[o - w]) + (b1[o] + vv[o] * du[o + w]);
+          s2 = ((hr * vr) + vt * dv[o - w]) + (b2[o] + vv[o] * dv[o + w]);
+        } else {
+          const float vt = vv[o - w];
+          dpsis = hl + (hr + vt);
+          s1 = (b1[o] + hr * ur) + vt * du[o - w];
+          s2 = (b2[o] + hr * vr) + vt * dv[o - w];
+        }
+        float i11, i12, i22;
+        if (s == 0) {
+          const float A11 = a22[o] + dpsis, A22 = a11[o] + dpsis, m12 = a12[o];
+          const float det = A11 * A22 - m12 * m12;
+          i11 = A11 / det;
+          i22 = A22 / det;
+          i12 = m12 / (0.0f - det);
+          a11[o] = i11;
+          a22[o] = i22;
+          a12[o] = i12;
+        } else {
+          i11 = a11[o];
+          i12 = a12[o];
+          i22 = a22[o];
+        }
+        float B1 = s1, B2 = s2;
+        if (x > 0) {
+          B1 = hl * du[o - 1] + s1;
+          B2 = hl * dv[o - 1] + s2;
+        }
+        const float u0 = du[o], v0 = dv[o];
+        du[o] = u0 + omega * (i11 * B1 + i12 * B2 - u0);
+        dv[o] = v0 + omega * (i12 * B1 + i22 * B2 - v0);
+      } else if (MODE == 1) {
+        float su = 0.0f, sv = 0.0f, sd = 0.0f;
+        if (y > 0) { su -= vv[o - w] * du[o - w]; sv -= vv[o - w] * dv[o - w]; sd += vv[o - w]; }
+        if (x > 0) { su -= hh[o - 1] * du[o - 1]; sv -= hh[o - 1] * dv[o - 1]; sd += hh[o - 1]; }
+        if (y < h - 1) { su -= vv[o] * du[o + w]; sv -= vv[o] * dv[o + w]; sd += vv[o]; }
+        if (x < w - 1) { su -= hh[o] * du[o + 1]; sv -= hh[o] * dv[o + 1]; sd += hh[o]; }
+        const float A11 = a11[o] + sd, A12 = a12[o], A22 = a22[o] + sd;
+        const float B1 = b1[o] - su, B2 = b2[o] - sv;
+        du[o] = (1.0f - omega) * du[o] + omega / A11 * (B1 - A12 * dv[o]);
+        dv[o] = (1.0f - omega) * dv[o] + omega / A22 * (B2 - A12 * du[o]);
+      } else {
+        float su = 0.0f, sd = 0.0f;
+        if (y > 0) { su -= vv[o - w] * du[o - w]; sd += vv[o - w]; }
+        if (x > 0) { su -= hh[o - 1] * du[o - 1]; sd += hh[o - 1]; }
+        if (y < h - 1) { su -= vv[o] * du[o + w]; sd += vv[o]; }
+        if (x < w - 1) { su -= hh[o] * du[o + 1]; sd += hh[o]; }
+        const float A11 = a11[o] + sd, B1 = b1[o] - su;
+        du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
+  const long plane = (long)a.w * a.h;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)a.n * plane) return;
+  const int f = (int)(idx / plane);
+  const long o = idx % plane;
+  float *WX = a.flow + (long)f * a.nop * plane;
+  if (a.nop == 2) {
+    WX[o] = WX[o] + a.du[idx];
+    WX[plane + o] = WX[plane + o] + a.dv[idx];
+  } else {
+    const float s = WX[o] + a.du[idx];
+    WX[o] = a.camlr == 0 ? ssemin(s, 0.0f) : ssemax(s, 0.0f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ output
+
+// flow *= 2^l ; cv::resize(INTER_LINEAR) generic float path (HResizeLinear + VResizeLinear) ; crop.
+__global__ __launch_bounds__(256) void k_upsample(UpArgs a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.n * a.W0 * a.H0;
+  if (idx >= total) return;
+  const int x = (int)(idx % a.W0);
+  const long r = idx / a.W0;
+  const int y = (int)(r % a.H0);
+  const int f = (int)(r / a.H0);
+  const long plane = (long)a.wl * a.hl;
+  const float *F = a.flow + (long)f * a.nop * plane;
+  float *out = a.out + idx * a.nop;
+  if (a.log2s == 0) {
+    const long o = (long)(y + a.offy) * a.wl + (x + a.offx);
+    out[0] = F[o];
+    if (a.nop == 2) out[1] = F[plane + o];
+    return;
+  }
+  const float fct = (float)(1 << a.log2s);
+  const double scale = 1.0 / (double)(1 << a.log2s);
+  const int dx = x + a.offx, dy = y + a.offy;
+  float fx = (float)((dx + 0.5) * scale - 0.5);
+  int sx = (int)floorf(fx);
+  fx -= (float)sx;
+  if (sx < 0) { fx = 0; sx = 0; }
+  bool lin = true;
+  if (sx + 1 >= a.wl) {
+    lin = false;
+    if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
+  }
+  float fy = (float)((dy + 0.5) * scale - 0.5);
+  const int sy = (int)floorf(fy);
+  fy -= (float)sy;
+  const int r0 = sy >= 0 ? (sy < a.hl ? sy : a.hl - 1) : 0;
+  const int r1 = sy + 1 >= 0 ? (sy + 1 < a.hl ? sy + 1 : a.hl - 1) : 0;
+  const float b0 = 1.f - fy, b1 = fy;
+  for (int k = 0; k < a.nop; ++k) {
+    const float *P = F + k * plane;
+    float h0, h1;
+    {
+      const float *S = P + (long)r0 * a.wl;
+      const float s0 = S[sx] * fct;
+      h0 = lin ? s0 * (1.f - fx) + (S[sx + 1] * fct) * fx : s0;
+    }
+    {
+      const float *S = P + (long)r1 * a.wl;
+      const float s0 = S[sx] * fct;
+      h1 = lin ? s0 * (1.f - fx) + (S[sx + 1] * fct) * fx : s0;
+    }
+    out[k] = h0 * b0 + h1 * b1;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------ launchers
+
+void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s) {
+  const long total = 2L * a.n * a.h * a.w;
+  k_pyr_base<<<ceil_div(total, 256), 256, 0, s>>>(a);
+}
+void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {
+  const long total = (long)a.n2 * a.h * a.w * a.noc;
+  k_pyr_down<<<ceil_div(total, 256), 256, 0, s>>>(a);
+}
+void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s) {
+  const long total = (long)a.n2 * (a.h + 2 * a.pad) * (a.w + 2 * a.pad);
+  k_pyr_pad_grad<<<ceil_div(total, 256), 256, 0, s>>>(a);
+}
+void launch_patch(const PatchArgs &a, hipStream_t s) {
+  const long waves = (long)a.n * a.g.npatch;
+  const int rs = ((a.novals + 31) / 32) * 32 + 8;
+  const size_t lds = sizeof(float) * 3 * rs * kPatchWaves;
+  if (a.nop == 2)
+    k_patch<2><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
+  else
+    k_patch<1><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
+}
+void launch_aggregate(const AggArgs &a, hipStream_t s) {
+  const long total = (long)a.n * a.g.w * a.g.h;
+  k_aggregate<<<ceil_div(total, 256), 256, 0, s>>>(a);
+}
+void launch_tv_prep(const TvArgs &a, hipStream_t s) {
+  k_tv_prep<<<ceil_div((long)a.n * a.w * a.h, 256), 256, 0, s>>>(a);
+}
+void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
+  k_tv_deriv1<<<ceil_div((long)a.n * a.noc * a.w * a.h, 256), 256, 0, s>>>(a);
+}
+void launch_tv_deriv2(const TvArgs &a, hipStream_t s) {
+  k_tv_deriv2<<<ceil_div((long)a.n * a.noc * a.w * a.h, 256), 256, 0, s>>>(a);
+}
+void launch_tv_system(const TvArgs &a, hipStream_t s) {
+  dim3 grid(ceil_div(a.w, kTX), ceil_div(a.h, kTY), a.n);
+  if (a.nop == 2)
+    k_tv_system<2><<<grid, kTX * kTY, 0, s>>>(a);
+  else
+    k_tv_system<1><<<grid, kTX * kTY, 0, s>>>(a);
+}
+void launch_tv_sor(const TvArgs &a, hipStream_t s) {
+  if (a.solverit < 1) return;
+  if (a.nop == 1)
+    k_tv_sor<2><<<a.n, 256, 0, s>>>(a);
+  else if (a.w < 2 || a.h < 2)
+    k_tv_sor<1><<<a.n, 256, 0, s>>>(a);
+  else
+    k_tv_sor<0><<<a.n, 256, 0, s>>>(a);
+}
+void launch_tv_final(const TvArgs &a, hipStream_t s) {
+  k_tv_final<<<ceil_div((long)a.n * a.w * a.h, 256), 256, 0, s>>>(a);
+}
+void launch_upsample(const UpArgs &a, hipStream_t s) {
+  const long total = (long)a.n * a.W0 * a.H0;
+  k_upsample<<<ceil_div(total, 256), 256, 0, s>>>(a);
+}
+
+}  // namespace ofdis

@@ -1,0 +1,709 @@
+// ofdis_runtime.cpp -- contexts, device workspace planning and the coarse-to-fine driver
+// (the OFClass constructor, oflow.cpp:31-338, restated for batches of frame pairs on one MI355X).
+//
+// One context per GPU.  A batch of n frame pairs is processed level by level; every kernel carries
+// the frame index in its grid, so even the 30x17 coarsest level of a 1080p frame fills the chip when
+// n is large.  All launches go to one stream; nothing synchronises the host unless a capture, the
+// verbosity timers or a host-buffer entry point asks for it.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ofdis.h"
+#include "ofdis_internal.h"
+
+using namespace ofdis;
+
+namespace {
+
+const char *const kKernelNames[] = {"pyr_base", "pyr_down",  "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample"};
+
+struct Plan {
+  int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
+  int nop = 2, noc = 1, pad = 8, sc_f = 0, sc_l = 0;
+  std::vector<LevelGeom> lv;                       // index s - sc_l
+  std::vector<size_t> off_lvl, off_img, off_dx, off_dy, off_flow;
+  size_t off_piter = 0, off_pw = 0, off_tv = 0, tv_plane = 0;
+  size_t total = 0;
+};
+
+inline size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct ofdis_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  char *ws = nullptr;
+  size_t ws_cap = 0;
+  // stage capture (frame 0), indexed by scale
+  std::vector<float *> cap_dis, cap_tv;
+  // kernel timing
+  bool timing = false;
+  struct Pending {
+    int kernel;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  std::map<int, std::pair<double, long>> acc;
+  std::mutex mu;
+};
+
+namespace {
+
+#define HIP_OK(x)                                                                                \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess) {                                                                      \
+      std::fprintf(stderr, "ofdis: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+                   __LINE__);                                                                    \
+      return e_ == hipErrorOutOfMemory ? OFDIS_ERR_OUT_OF_MEMORY : OFDIS_ERR_DEVICE;             \
+    }                                                                                            \
+  } while (0)
+
+int kernel_index(const char *name) {
+  for (int i = 0; i < (int)(sizeof(kKernelNames) / sizeof(kKernelNames[0])); ++i)
+    if (std::strcmp(kKernelNames[i], name) == 0) return i;
+  return -1;
+}
+
+hipEvent_t get_event(ofdis_context *c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+template <class F>
+void timed(ofdis_context *c, int kernel, hipStream_t s, F &&f) {
+  if (!c->timing) {
+    f();
+    return;
+  }
+  hipEvent_t a = get_event(c), b = get_event(c);
+  hipEventRecord(a, s);
+  f();
+  hipEventRecord(b, s);
+  c->pending.push_back({kernel, a, b});
+}
+
+void drain_timing(ofdis_context *c) {
+  for (auto &p : c->pending) {
+    hipEventSynchronize(p.b);
+    float ms = 0.0f;
+    hipEventElapsedTime(&ms, p.a, p.b);
+    auto &e = c->acc[p.kernel];
+    e.first += ms;
+    e.second += 1;
+    c->pool.push_back(p.a);
+    c->pool.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+void fill_level(const ofdis_params *p, int Wp, int Hp, int pad, int s, LevelGeom &g) {
+  const float sc_fct = (float)std::pow(2.0, -s);  // oflow.cpp:142-153
+  g.w = (int)((float)Wp * sc_fct);
+  g.h = (int)((float)Hp * sc_fct);
+  g.pad = pad;
+  g.W = g.w + 2 * pad;
+  g.H = g.h + 2 * pad;
+  g.level = s;
+  g.tmp_lb = -(float)p->p_samp_s / 2;
+  g.tmp_ubw = (float)(g.w + p->p_samp_s / 2 - 2);
+  g.tmp_ubh = (float)(g.h + p->p_samp_s / 2 - 2);
+  const int st0 = (int)std::floor((float)p->p_samp_s * (1 - p->patove));  // oflow.cpp:90
+  const int steps = st0 > 1 ? st0 : 1;
+  g.nopw = (int)std::ceil((float)g.w / (float)steps);  // patchgrid.cpp:43-46
+  g.noph = (int)std::ceil((float)g.h / (float)steps);
+  g.offw = (g.w - (g.nopw - 1) * steps) / 2;
+  g.offh = (g.h - (g.noph - 1) * steps) / 2;
+  g.npatch = g.nopw * g.noph;
+}
+
+int steps_of(const ofdis_params *p) {
+  const int st0 = (int)std::floor((float)p->p_samp_s * (1 - p->patove));
+  return st0 > 1 ? st0 : 1;
+}
+
+Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
+  Plan P;
+  P.n = n;
+  P.Wp = Wp;
+  P.Hp = Hp;
+  P.nop = p->mode == OFDIS_MODE_OF ? 2 : 1;
+  P.noc = p->noc;
+  P.pad = pad;
+  P.sc_f = p->sc_f;
+  P.sc_l = p->sc_l;
+  const int nsc = p->sc_f - p->sc_l + 1;
+  P.lv.resize(nsc);
+  P.off_lvl.resize(nsc);
+  P.off_img.resize(nsc);
+  P.off_dx.resize(nsc);
+  P.off_dy.resize(nsc);
+  P.off_flow.resize(nsc);
+  size_t off = 0;
+  const int novals = p->noc * p->p_samp_s * p->p_samp_s;
+  size_t max_np = 0, max_plane = 0;
+  for (int s = p->sc_l; s <= p->sc_f; ++s) {
+    const int i = s - p->sc_l;
+    fill_level(p, Wp, Hp, pad, s, P.lv[i]);
+    const LevelGeom &g = P.lv[i];
+    P.off_lvl[i] = off;
+    off = align_up(off + sizeof(float) * 2 * (size_t)n * g.w * g.h * P.noc);
+    P.off_img[i] = off;
+    off = align_up(off + sizeof(float) * 2 * (size_t)n * g.W * g.H * P.noc);
+    P.off_dx[i] = off;
+    off = align_up(off + sizeof(float) * 2 * (size_t)n * g.W * g.H * P.noc);
+    P.off_dy[i] = off;
+    off = align_up(off + sizeof(float) * 2 * (size_t)n * g.W * g.H * P.noc);
+    P.off_flow[i] = off;
+    off = align_up(off + sizeof(float) * (size_t)n * P.nop * g.w * g.h);
+    if ((size_t)g.npatch > max_np) max_np = g.npatch;
+    if ((size_t)g.w * g.h > max_plane) max_plane = (size_t)g.w * g.h;
+  }
+  P.off_piter = off;
+  off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
+  P.off_pw = off;
+  off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
+  P.off_tv = off;
+  P.tv_plane = max_plane;
+  if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_plane * (10 + 9 * (size_t)P.noc));
+  P.total = off;
+  return P;
+}
+
+int ensure_ws(ofdis_context *c, size_t bytes) {
+  if (bytes <= c->ws_cap) return OFDIS_OK;
+  if (c->ws) {
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipFree(c->ws));
+    c->ws = nullptr;
+    c->ws_cap = 0;
+  }
+  HIP_OK(hipMalloc(&c->ws, bytes));
+  c->ws_cap = bytes;
+  return OFDIS_OK;
+}
+
+int capture(ofdis_context *c, hipStream_t s, const std::vector<float *> &cap, int scale, const Plan &P,
+            const float *flow_planar) {
+  if ((int)cap.size() <= scale || !cap[scale]) return OFDIS_OK;
+  const LevelGeom &g = P.lv[scale - P.sc_l];
+  const size_t plane = (size_t)g.w * g.h;
+  std::vector<float> tmp(plane * P.nop);
+  HIP_OK(hipMemcpyAsync(tmp.data(), flow_planar, tmp.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  for (size_t i = 0; i < plane; ++i)
+    for (int k = 0; k < P.nop; ++k) cap[scale][i * P.nop + k] = tmp[k * plane + i];
+  return OFDIS_OK;
+}
+
+struct StageTimes {
+  double poptim = 0, cflow = 0, tvopt = 0;
+};
+
+// The coarse-to-fine loop (oflow.cpp:182-330) over device pyramids already in the workspace.
+// init: optional coarse initial flow (device, interleaved, (w_f/2)*(h_f/2)*nop per frame).
+int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream_t s, const float *init,
+               std::vector<StageTimes> *times) {
+  const int nop = P.nop, noc = P.noc, n = P.n;
+  const int novals = noc * p->p_samp_s * p->p_samp_s;
+  const int steps = steps_of(p);
+  char *ws = c->ws;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (times)
+    for (auto &e : ev) HIP_OK(hipEventCreate(&e));
+  for (int sl = p->sc_f; sl >= p->sc_l; --sl) {
+    const int i = sl - p->sc_l;
+    const LevelGeom &g = P.lv[i];
+    const size_t fsp = (size_t)g.W * g.H * noc;  // floats per padded frame
+    const float *img = (const float *)(ws + P.off_img[i]);
+    const float *dxp = (const float *)(ws + P.off_dx[i]);
+    const float *dyp = (const float *)(ws + P.off_dy[i]);
+    float *flow = (float *)(ws + P.off_flow[i]);
+    if (times) HIP_OK(hipEventRecord(ev[0], s));
+
+    PatchArgs pa{};
+    pa.img_a = img;
+    pa.dx_a = dxp;
+    pa.dy_a = dyp;
+    pa.img_b = img + (size_t)n * fsp;
+    if (sl < p->sc_f) {
+      const LevelGeom &gc = P.lv[i + 1];
+      pa.prev = (const float *)(ws + P.off_flow[i + 1]);
+      pa.prev_frame_stride = (long)nop * gc.w * gc.h;
+      pa.prev_comp_stride = gc.w * gc.h;
+      pa.prev_elem_stride = 1;
+      pa.prev_w = g.w / 2;
+    } else if (init) {
+      pa.prev = init;
+      pa.prev_frame_stride = (long)nop * (g.w / 2) * (g.h / 2);
+      pa.prev_comp_stride = 1;
+      pa.prev_elem_stride = nop;
+      pa.prev_w = g.w / 2;
+    }
+    pa.p_iter = (float *)(ws + P.off_piter);
+    pa.pweight = (float *)(ws + P.off_pw);
+    pa.n = n;
+    pa.nop = nop;
+    pa.noc = noc;
+    pa.p = p->p_samp_s;
+    pa.novals = novals;
+    pa.steps = steps;
+    pa.costfct = p->costfct;
+    pa.patnorm = p->patnorm;
+    pa.max_iter = p->max_iter;
+    pa.min_iter = p->min_iter;
+    pa.dp_thresh_sq = p->dp_thresh * p->dp_thresh;
+    pa.dr_thresh = p->dr_thresh;
+    pa.res_thresh = p->res_thresh;
+    pa.outlierthresh = (float)p->p_samp_s / 2;
+    pa.camlr = 0;
+    pa.g = g;
+    timed(c, 3, s, [&] { launch_patch(pa, s); });
+
+    AggArgs ag{};
+    ag.p_iter = pa.p_iter;
+    ag.pweight = pa.pweight;
+    ag.flow = flow;
+    ag.n = n;
+    ag.nop = nop;
+    ag.noc = noc;
+    ag.p = p->p_samp_s;
+    ag.novals = novals;
+    ag.steps = steps;
+    ag.g = g;
+    if (times) HIP_OK(hipEventRecord(ev[1], s));
+    timed(c, 4, s, [&] { launch_aggregate(ag, s); });
+    if (times) HIP_OK(hipEventRecord(ev[2], s));
+    int rc = capture(c, s, c->cap_dis, sl, P, flow);
+    if (rc) return rc;
+
+    const int n_inner = p->tv_innerit * (sl + 1);  // refine_variational.cpp:36
+    if (p->usetvref && n_inner > 0) {
+      const size_t pl = (size_t)n * g.w * g.h;
+      float *t0 = (float *)(ws + P.off_tv);
+      TvArgs tv{};
+      tv.img_a = img;
+      tv.img_b = img + (size_t)n * fsp;
+      tv.flow = flow;
+      tv.du = t0;
+      tv.dv = t0 + pl;
+      tv.mask = t0 + 2 * pl;
+      tv.a11 = t0 + 3 * pl;
+      tv.a12 = t0 + 4 * pl;
+      tv.a22 = t0 + 5 * pl;
+      tv.b1 = t0 + 6 * pl;
+      tv.b2 = t0 + 7 * pl;
+      tv.sh = t0 + 8 * pl;
+      tv.sv = t0 + 9 * pl;
+      float *cp = t0 + 10 * pl;
+      const size_t cpl = pl * noc;
+      tv.t = cp;
+      tv.dt = cp + cpl;
+      tv.Iz = tv.dt;
+      tv.Ix = cp + 2 * cpl;
+      tv.Iy = cp + 3 * cpl;
+      tv.Ixx = cp + 4 * cpl;
+      tv.Ixy = cp + 5 * cpl;
+      tv.Iyy = cp + 6 * cpl;
+      tv.Ixz = cp + 7 * cpl;
+      tv.Iyz = cp + 8 * cpl;
+      tv.n = n;
+      tv.nop = nop;
+      tv.noc = noc;
+      tv.w = g.w;
+      tv.h = g.h;
+      tv.pad = g.pad;
+      tv.W = g.W;
+      tv.quarter_alpha = 0.25f * p->tv_alpha;  // refine_variational.cpp:40-43
+      tv.hgo3 = p->tv_gamma * 0.5f / 3.0f;
+      tv.hdo3 = p->tv_delta * 0.5f / 3.0f;
+      tv.omega = p->tv_sor;
+      tv.solverit = p->tv_solverit;
+      tv.camlr = 0;
+      timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
+      timed(c, 6, s, [&] {
+        launch_tv_deriv1(tv, s);
+        launch_tv_deriv2(tv, s);
+      });
+      for (int it = 0; it < n_inner; ++it) {
+        tv.first_iter = it == 0;
+        timed(c, 7, s, [&] { launch_tv_system(tv, s); });
+        timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
+      }
+      timed(c, 9, s, [&] { launch_tv_final(tv, s); });
+    }
+    if (times) {
+      HIP_OK(hipEventRecord(ev[3], s));
+      HIP_OK(hipEventSynchronize(ev[3]));
+      StageTimes st;
+      float ms;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      st.poptim = ms;
+      hipEventElapsedTime(&ms, ev[1], ev[2]);
+      st.cflow = ms;
+      hipEventElapsedTime(&ms, ev[2], ev[3]);
+      st.tvopt = ms;
+      times->push_back(st);
+    }
+    rc = capture(c, s, c->cap_tv, sl, P, flow);
+    if (rc) return rc;
+  }
+  if (times)
+    for (auto &e : ev) hipEventDestroy(e);
+  return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+}
+
+void print_times(const Plan &P, const std::vector<StageTimes> &t, double total_ms, int verbosity) {
+  if (verbosity > 1) {
+    for (size_t k = 0; k < t.size(); ++k) {
+      const int sl = P.sc_f - (int)k;
+      const LevelGeom &g = P.lv[sl - P.sc_l];
+      const double all = t[k].poptim + t[k].cflow + t[k].tvopt;
+      std::printf("TIME (Sc: %i, #p:%6i, pconst, pinit, poptim, cflow, tvopt, total): %8.2f %8.2f %8.2f %8.2f %8.2f -> %8.2f ms.\n",
+                  sl, g.npatch, 0.0, 0.0, t[k].poptim, t[k].cflow, t[k].tvopt, all);
+    }
+  }
+  if (verbosity > 0) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", total_ms);
+}
+
+int check_device(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return OFDIS_ERR_NO_DEVICE;
+  if (device < 0 || device >= count) return OFDIS_ERR_INVALID_ARGUMENT;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return OFDIS_ERR_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    std::fprintf(stderr, "ofdis: device %d is %s, this build targets gfx950 only\n", device, prop.gcnArchName);
+    return OFDIS_ERR_NO_DEVICE;
+  }
+  return OFDIS_OK;
+}
+
+// Pyramid of the batch (run_dense.cpp:299-312,327-328,131-179) into the workspace.
+int run_pyramid(ofdis_context *c, const Plan &P, const uint8_t *a, const uint8_t *b, hipStream_t s) {
+  char *ws = c->ws;
+  const int n2 = 2 * P.n;
+  {
+    PyrBaseArgs pb{};
+    pb.img_a = a;
+    pb.img_b = b;
+    pb.n = P.n;
+    pb.W0 = P.W0;
+    pb.H0 = P.H0;
+    pb.noc = P.noc;
+    pb.padl = P.padl;
+    pb.padt = P.padt;
+    pb.log2s = P.sc_l;
+    pb.w = P.lv[0].w;
+    pb.h = P.lv[0].h;
+    pb.out = (float *)(ws + P.off_lvl[0]);
+    timed(c, 0, s, [&] { launch_pyr_base(pb, s); });
+  }
+  for (size_t i = 1; i < P.lv.size(); ++i) {
+    PyrDownArgs pd{};
+    pd.src = (const float *)(ws + P.off_lvl[i - 1]);
+    pd.dst = (float *)(ws + P.off_lvl[i]);
+    pd.n2 = n2;
+    pd.w = P.lv[i].w;
+    pd.h = P.lv[i].h;
+    pd.noc = P.noc;
+    timed(c, 1, s, [&] { launch_pyr_down(pd, s); });
+  }
+  for (size_t i = 0; i < P.lv.size(); ++i) {
+    PyrPadGradArgs pg{};
+    pg.lvl = (const float *)(ws + P.off_lvl[i]);
+    pg.img = (float *)(ws + P.off_img[i]);
+    pg.dx = (float *)(ws + P.off_dx[i]);
+    pg.dy = (float *)(ws + P.off_dy[i]);
+    pg.n2 = n2;
+    pg.w = P.lv[i].w;
+    pg.h = P.lv[i].h;
+    pg.noc = P.noc;
+    pg.pad = P.pad;
+    timed(c, 2, s, [&] { launch_pyr_pad_grad(pg, s); });
+  }
+  return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+}
+
+Plan batch_plan(const ofdis_params *p, int n, int width, int height) {
+  const int d = 1 << p->sc_f;
+  const int padw = (width % d) ? d - width % d : 0, padh = (height % d) ? d - height % d : 0;
+  Plan P = make_plan(p, n, width + padw, height + padh, p->p_samp_s);
+  P.W0 = width;
+  P.H0 = height;
+  P.padw = padw;
+  P.padh = padh;
+  P.padl = padw / 2;  // copyMakeBorder(floor(padw/2), ceil(padw/2)) (run_dense.cpp:309)
+  P.padt = padh / 2;
+  return P;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ofdis_context_create(int device, ofdis_context **out) {
+  if (!out) return OFDIS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(device));
+  ofdis_context *c = new ofdis_context();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return OFDIS_ERR_DEVICE;
+  }
+  *out = c;
+  return OFDIS_OK;
+}
+
+void ofdis_context_destroy(ofdis_context *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  drain_timing(c);
+  for (auto e : c->pool) hipEventDestroy(e);
+  if (c->ws) hipFree(c->ws);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width, int height,
+                       const ofdis_params *p, float *flow_out, void *stream) {
+  if (!c || !img_a || !img_b || !flow_out || n <= 0 || width <= 0 || height <= 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  int rc = ofdis_params_validate(p, -1, -1, -1);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  Plan P = batch_plan(p, n, width, height);
+  rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
+  if (rc) return rc;
+  rc = ensure_ws(c, P.total);
+  if (rc) return rc;
+  rc = run_pyramid(c, P, img_a, img_b, s);
+  if (rc) return rc;
+  rc = run_levels(c, P, p, s, nullptr, nullptr);
+  if (rc) return rc;
+  UpArgs up{};
+  up.flow = (const float *)(c->ws + P.off_flow[0]);
+  up.out = flow_out;
+  up.n = n;
+  up.nop = P.nop;
+  up.wl = P.lv[0].w;
+  up.hl = P.lv[0].h;
+  up.log2s = p->sc_l;
+  up.W0 = width;
+  up.H0 = height;
+  up.offx = P.padl;
+  up.offy = P.padt;
+  timed(c, 10, s, [&] { launch_upsample(up, s); });
+  return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+}
+
+int ofdis_run_batch_u8_host(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
+                            int height, const ofdis_params *p, float *flow_out) {
+  if (!c || !img_a || !img_b || !flow_out || n <= 0 || width <= 0 || height <= 0 || !p)
+    return OFDIS_ERR_INVALID_ARGUMENT;
+  HIP_OK(hipSetDevice(c->device));
+  const size_t in = (size_t)n * width * height * p->noc;
+  const size_t out = (size_t)n * width * height * (p->mode == OFDIS_MODE_OF ? 2 : 1);
+  uint8_t *da = nullptr, *db = nullptr;
+  float *dout = nullptr;
+  HIP_OK(hipMalloc(&da, in));
+  HIP_OK(hipMalloc(&db, in));
+  HIP_OK(hipMalloc(&dout, out * sizeof(float)));
+  HIP_OK(hipMemcpyAsync(da, img_a, in, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(db, img_b, in, hipMemcpyHostToDevice, c->stream));
+  auto t0 = std::chrono::steady_clock::now();
+  int rc = ofdis_run_batch_u8(c, da, db, n, width, height, p, dout, c->stream);
+  if (rc == OFDIS_OK) {
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (p->verbosity > 0) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", ms);
+    HIP_OK(hipMemcpy(flow_out, dout, out * sizeof(float), hipMemcpyDeviceToHost));
+  }
+  hipFree(da);
+  hipFree(db);
+  hipFree(dout);
+  return rc;
+}
+
+int ofdis_pyramid_u8_host(ofdis_context *c, const uint8_t *img, int width, int height, const ofdis_params *p,
+                          int imgpadding, float *const *img_pyr, float *const *dx_pyr, float *const *dy_pyr) {
+  if (!c || !img || !p || width <= 0 || height <= 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lock(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  ofdis_params q = *p;
+  q.p_samp_s = imgpadding;  // pad by imgpadding
+  Plan P = batch_plan(p, 1, width, height);
+  P = make_plan(p, 1, P.Wp, P.Hp, imgpadding);
+  {
+    const int d = 1 << p->sc_f;
+    P.W0 = width;
+    P.H0 = height;
+    P.padw = (width % d) ? d - width % d : 0;
+    P.padh = (height % d) ? d - height % d : 0;
+    P.padl = P.padw / 2;
+    P.padt = P.padh / 2;
+  }
+  int rc = ensure_ws(c, P.total);
+  if (rc) return rc;
+  const size_t in = (size_t)width * height * p->noc;
+  uint8_t *d = nullptr;
+  HIP_OK(hipMalloc(&d, in));
+  HIP_OK(hipMemcpy(d, img, in, hipMemcpyHostToDevice));
+  rc = run_pyramid(c, P, d, d, c->stream);
+  if (rc == OFDIS_OK) {
+    HIP_OK(hipStreamSynchronize(c->stream));
+    for (int s = p->sc_l; s <= p->sc_f; ++s) {
+      const LevelGeom &g = P.lv[s - p->sc_l];
+      const size_t bytes = sizeof(float) * (size_t)g.W * g.H * p->noc;
+      if (img_pyr && img_pyr[s]) HIP_OK(hipMemcpy(img_pyr[s], c->ws + P.off_img[s - p->sc_l], bytes, hipMemcpyDeviceToHost));
+      if (dx_pyr && dx_pyr[s]) HIP_OK(hipMemcpy(dx_pyr[s], c->ws + P.off_dx[s - p->sc_l], bytes, hipMemcpyDeviceToHost));
+      if (dy_pyr && dy_pyr[s]) HIP_OK(hipMemcpy(dy_pyr[s], c->ws + P.off_dy[s - p->sc_l], bytes, hipMemcpyDeviceToHost));
+    }
+  }
+  hipFree(d);
+  (void)q;
+  return rc;
+}
+
+int ofdis_context_set_stage_capture(ofdis_context *c, float *const *dis_flow, float *const *tv_flow, int nscales) {
+  if (!c || nscales < 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  c->cap_dis.assign(nscales, nullptr);
+  c->cap_tv.assign(nscales, nullptr);
+  for (int i = 0; i < nscales; ++i) {
+    if (dis_flow) c->cap_dis[i] = dis_flow[i];
+    if (tv_flow) c->cap_tv[i] = tv_flow[i];
+  }
+  return OFDIS_OK;
+}
+
+int ofdis_context_enable_kernel_timing(ofdis_context *c, int enable) {
+  if (!c) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lock(c->mu);
+  drain_timing(c);
+  c->acc.clear();
+  c->timing = enable != 0;
+  return OFDIS_OK;
+}
+
+int ofdis_context_kernel_time(ofdis_context *c, const char *name, double *total_ms, long *launches) {
+  if (!c || !name) return OFDIS_ERR_INVALID_ARGUMENT;
+  const int k = kernel_index(name);
+  if (k < 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lock(c->mu);
+  drain_timing(c);
+  auto it = c->acc.find(k);
+  if (total_ms) *total_ms = it == c->acc.end() ? 0.0 : it->second.first;
+  if (launches) *launches = it == c->acc.end() ? 0 : it->second.second;
+  return OFDIS_OK;
+}
+
+const char *ofdis_kernel_names(void) {
+  return "pyr_base,pyr_down,pyr_pad_grad,patch,aggregate,tv_prep,tv_deriv,tv_system,tv_sor,tv_final,upsample";
+}
+
+// Byte model of SURVEY §8(d), per frame pair, for the roofline of each kernel family.
+int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const char *kernel, double *bytes) {
+  if (!p || !kernel || !bytes) return OFDIS_ERR_INVALID_ARGUMENT;
+  Plan P = batch_plan(p, 1, width, height);
+  const int nop = P.nop, noc = P.noc;
+  const int novals = noc * p->p_samp_s * p->p_samp_s;
+  double b = 0.0;
+  const std::string k(kernel);
+  for (const LevelGeom &g : P.lv) {
+    const double px = (double)g.w * g.h;
+    const int n_inner = p->usetvref ? p->tv_innerit * (g.level + 1) : 0;
+    if (k == "tv_sor") b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
+    if (k == "tv_system") b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
+    if (k == "patch") b += (double)g.npatch * (12.0 * novals + 4.0 * (p->p_samp_s + 1) * (p->p_samp_s + 1) * noc *
+                                                                   (double)(p->max_iter + 1) + 4.0 * (nop + novals));
+    if (k == "aggregate") b += px * 4.0 * nop + (double)g.npatch * 4.0 * (nop + novals);
+    if (k == "pyr_pad_grad") b += 2.0 * (px * 4.0 * noc + 3.0 * g.W * g.H * 4.0 * noc);
+  }
+  if (k == "pyr_base") b = 2.0 * width * height * noc + 2.0 * 4.0 * P.lv[0].w * P.lv[0].h * noc;
+  if (k == "upsample") b = (double)width * height * nop * 4.0;
+  *bytes = b;
+  return OFDIS_OK;
+}
+
+// OFC::OFClass (oflow.h:99-126) with host pointers; one frame pair on device 0.
+int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx, const float *const *im_ao_dy,
+                        const float *const *im_bo, const float *const *im_bo_dx, const float *const *im_bo_dy,
+                        int imgpadding, float *outflow, const float *initflow, int width, int height,
+                        const ofdis_params *p) {
+  (void)im_bo_dx;
+  (void)im_bo_dy;  // used upstream only by the backward grid of usefbcon (oflow.cpp:193-196)
+  if (!im_ao || !im_ao_dx || !im_ao_dy || !im_bo || !outflow) return OFDIS_ERR_INVALID_ARGUMENT;
+  int rc = ofdis_params_validate(p, width, height, imgpadding);
+  if (rc) return rc;
+  for (int s = p->sc_l; s <= p->sc_f; ++s)
+    if (!im_ao[s] || !im_ao_dx[s] || !im_ao_dy[s] || !im_bo[s]) return OFDIS_ERR_INVALID_ARGUMENT;
+  static std::mutex gmu;
+  static ofdis_context *gctx = nullptr;
+  std::lock_guard<std::mutex> glock(gmu);
+  if (!gctx) {
+    rc = ofdis_context_create(0, &gctx);
+    if (rc) return rc;
+  }
+  ofdis_context *c = gctx;
+  std::lock_guard<std::mutex> lock(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  auto t0 = std::chrono::steady_clock::now();
+  Plan P = make_plan(p, 1, width, height, imgpadding);
+  rc = ensure_ws(c, P.total);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  for (int sl = p->sc_l; sl <= p->sc_f; ++sl) {
+    const LevelGeom &g = P.lv[sl - p->sc_l];
+    const size_t fb = sizeof(float) * (size_t)g.W * g.H * p->noc;
+    char *img = c->ws + P.off_img[sl - p->sc_l];
+    HIP_OK(hipMemcpyAsync(img, im_ao[sl], fb, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(img + fb, im_bo[sl], fb, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->ws + P.off_dx[sl - p->sc_l], im_ao_dx[sl], fb, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->ws + P.off_dy[sl - p->sc_l], im_ao_dy[sl], fb, hipMemcpyHostToDevice, s));
+  }
+  float *dinit = nullptr;
+  if (initflow) {
+    const size_t nb = sizeof(float) * (size_t)(width >> (p->sc_f + 1)) * (height >> (p->sc_f + 1)) * P.nop;
+    HIP_OK(hipMalloc(&dinit, nb > 0 ? nb : 4));
+    if (nb) HIP_OK(hipMemcpyAsync(dinit, initflow, nb, hipMemcpyHostToDevice, s));
+  }
+  std::vector<StageTimes> times;
+  rc = run_levels(c, P, p, s, dinit, p->verbosity > 1 ? &times : nullptr);
+  if (rc == OFDIS_OK) {
+    const LevelGeom &g = P.lv[0];
+    const size_t plane = (size_t)g.w * g.h;
+    std::vector<float> tmp(plane * P.nop);
+    HIP_OK(hipMemcpyAsync(tmp.data(), c->ws + P.off_flow[0], tmp.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < plane; ++i)
+      for (int k = 0; k < P.nop; ++k) outflow[i * P.nop + k] = tmp[k * plane + i];
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    print_times(P, times, ms, p->verbosity);
+  }
+  if (dinit) hipFree(dinit);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,96 @@
+// run_dense.cpp -- the run_{OF,DE}_{INT,RGB} command lines (drop-in for the reference's run_dense.cpp).
+//
+//   run_OF_INT img1 img2 out.flo            operating point 2, coarsest scale chosen automatically
+//   run_OF_INT img1 img2 out.flo X          operating point X = 1..4
+//   run_OF_INT img1 img2 out.flo p1 .. p20  all 20 parameters explicitly (README.md:54-86)
+//
+// SELECTMODE (1 flow -> .flo, 2 depth -> .pfm) and SELECTCHANNEL (1 gray, 3 BGR) are compile-time, as in
+// the reference's CMakeLists.txt:36-61.  Images: binary PGM (P5) / PPM (P6); OpenCV's imread is not
+// available in this image (PNG decoding is out of scope).  Unlike the reference, argv is
+// validated (the reference reads past argv for 6 <= argc < 24, run_dense.cpp:270-295).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../include/ofdis.h"
+
+#ifndef SELECTMODE
+#define SELECTMODE 1
+#endif
+#ifndef SELECTCHANNEL
+#define SELECTCHANNEL 1
+#endif
+
+static std::vector<uint8_t> load(const char *path, int &w, int &h) {
+  int noc = 0;
+  if (ofdis_read_pnm(path, nullptr, &w, &h, &noc, 0) != OFDIS_OK) {
+    std::fprintf(stderr, "cannot read %s (binary PGM/PPM expected)\n", path);
+    std::exit(1);
+  }
+  std::vector<uint8_t> raw((size_t)w * h * noc);
+  ofdis_read_pnm(path, raw.data(), &w, &h, &noc, raw.size());
+  if (noc == SELECTCHANNEL) return raw;
+  std::vector<uint8_t> out((size_t)w * h * SELECTCHANNEL);
+  for (size_t i = 0; i < (size_t)w * h; ++i) {
+    if (SELECTCHANNEL == 1) {  // cv::COLOR_BGR2GRAY weights (ITU-R 601), rounded
+      const double g = 0.114 * raw[3 * i] + 0.587 * raw[3 * i + 1] + 0.299 * raw[3 * i + 2];
+      out[i] = (uint8_t)(g + 0.5);
+    } else {
+      out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = raw[i];
+    }
+  }
+  return out;
+}
+
+int main(int argc, char **argv) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (argc != 4 && argc != 5 && argc != 24) {
+    std::fprintf(stderr, "usage: %s img1 img2 out [oppoint 1-4 | 20 parameters]\n", argv[0]);
+    return 1;
+  }
+  int w = 0, h = 0, w2 = 0, h2 = 0;
+  std::vector<uint8_t> a = load(argv[1], w, h), b = load(argv[2], w2, h2);
+  if (w != w2 || h != h2) {
+    std::fprintf(stderr, "image sizes differ\n");
+    return 1;
+  }
+  ofdis_params p;
+  int rc;
+  if (argc <= 5)
+    rc = ofdis_params_oppoint(&p, argc == 5 ? std::atoi(argv[4]) : 2, w, SELECTMODE, SELECTCHANNEL);
+  else
+    rc = ofdis_params_from_strings(&p, 20, (const char *const *)(argv + 4), SELECTMODE, SELECTCHANNEL);
+  if (rc == OFDIS_OK) rc = ofdis_params_validate(&p, -1, -1, -1);
+  if (rc != OFDIS_OK) {
+    std::fprintf(stderr, "invalid parameters: %s\n", ofdis_status_string(rc));
+    return 1;
+  }
+  if (p.verbosity > 1)
+    std::printf("TIME (Image loading     ) (ms): %3g\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  ofdis_context *ctx = nullptr;
+  rc = ofdis_context_create(0, &ctx);
+  if (rc != OFDIS_OK) {
+    std::fprintf(stderr, "no usable gfx950 device: %s\n", ofdis_status_string(rc));
+    return 1;
+  }
+  const int nop = SELECTMODE == 1 ? 2 : 1;
+  std::vector<float> flow((size_t)w * h * nop);
+  rc = ofdis_run_batch_u8_host(ctx, a.data(), b.data(), 1, w, h, &p, flow.data());
+  ofdis_context_destroy(ctx);
+  if (rc != OFDIS_OK) {
+    std::fprintf(stderr, "flow computation failed: %s\n", ofdis_status_string(rc));
+    return 1;
+  }
+  t0 = std::chrono::steady_clock::now();
+  rc = SELECTMODE == 1 ? ofdis_write_flo(argv[3], flow.data(), w, h, 2) : ofdis_write_pfm(argv[3], flow.data(), w, h);
+  if (rc != OFDIS_OK) {
+    std::fprintf(stderr, "cannot write %s\n", argv[3]);
+    return 1;
+  }
+  if (p.verbosity > 1)
+    std::printf("TIME (Saving flow file  ) (ms): %3g\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return 0;
+}

@@ -1,0 +1,147 @@
+"""GPU parity: the HIP path (libofdis.so through its C-ABI) against the CPU oracle on identical inputs.
+
+The kernels keep the reference evaluation order, so the bar is bit-exactness (compared as uint32 bit
+patterns), stage by stage: pyramid, flow after patch aggregation per scale, flow after TV refinement per
+scale, and the full-resolution output.  At BASELINE's full 1080p size the check is the same (the oracle
+finishes in well under a second per pair).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(x):
+    return np.ascontiguousarray(x, np.float32).view(np.uint32)
+
+
+def assert_bitexact(got, want, what):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    if not np.array_equal(_bits(got), _bits(want)):
+        d = np.abs(got.astype(np.float64) - want.astype(np.float64))
+        bad = np.argwhere(_bits(got) != _bits(want))
+        raise AssertionError(f"{what}: {len(bad)} / {got.size} values differ; max |d| = {np.nanmax(d):.3g}; "
+                             f"first at {tuple(bad[0])}: got {got[tuple(bad[0])]!r} want {want[tuple(bad[0])]!r}")
+
+
+@pytest.fixture(scope="module")
+def od():
+    import of_dis_amd
+    return of_dis_amd
+
+
+@pytest.fixture(scope="module")
+def ctx(od):
+    c = od.Context(0)
+    yield c
+    c.close()
+
+
+CASES = [
+    # (w, h, noc, mode, oppoint, overrides)
+    (160, 120, 1, 1, 2, {}),
+    (640, 480, 1, 1, 2, {}),
+    (200, 150, 1, 1, 1, {}),                                  # op1: no TV refinement, overlap .3
+    (173, 97, 1, 1, 2, {}),                                   # divisibility padding on both axes
+    (192, 128, 3, 1, 3, {}),                                  # RGB op3 (p = 12, L2 as defined)
+    (192, 128, 3, 1, 3, {"costfct": 1}),                      # RGB op3 with the L1 cost of BASELINE config C
+    (160, 120, 1, 1, 2, {"costfct": 2}),                      # pseudo-Huber
+    (160, 120, 1, 1, 2, {"min_iter": 2, "dp_thresh": 0.3, "dr_thresh": 0.9}),  # early stopping active
+    (160, 120, 1, 1, 2, {"patnorm": 0, "tv_innerit": 2, "tv_solverit": 4, "tv_sor": 1.3}),
+    (240, 120, 1, 2, 4, {"max_iter": 16, "min_iter": 16}),    # depth from stereo, op4
+    (240, 120, 3, 2, 2, {}),                                  # RGB depth
+]
+
+
+def _params(od, O, w, noc, mode, op, over):
+    p = od.oppoint(op, w, mode, noc)
+    q = O.oppoint(op, w, mode, noc)
+    for k, v in over.items():
+        setattr(p, k, v)
+        setattr(q, k, v)
+    return p, q
+
+
+@pytest.mark.parametrize("w,h,noc,mode,op,over", CASES)
+def test_pipeline_bitexact(oracle, od, ctx, w, h, noc, mode, op, over):
+    O = oracle
+    a, b = od.synth_pair(w, h, noc, 3, mode)
+    p, q = _params(od, O, w, noc, mode, op, over)
+    ref, cap_d, cap_t = O.run_u8(a, b, q, capture=True)
+    dis = {s: np.zeros_like(v) for s, v in cap_d.items()}
+    tv = {s: np.zeros_like(v) for s, v in cap_t.items()}
+    ctx.set_capture(dis, tv)
+    try:
+        got = ctx.run_host(a, b, p)
+    finally:
+        ctx.set_capture(None, None)
+    for s in sorted(cap_d, reverse=True):
+        assert_bitexact(dis[s], cap_d[s], f"scale {s} after aggregation")
+        assert_bitexact(tv[s], cap_t[s], f"scale {s} after TV refinement")
+    assert_bitexact(got, ref, "full-resolution flow")
+
+
+@pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2)])
+def test_pyramid_bitexact(oracle, od, ctx, w, h, noc, op):
+    O = oracle
+    a, _ = od.synth_pair(w, h, noc, 1, 1)
+    p, q = _params(od, O, w, noc, 1, op, {})
+    pw, ph = O.divisibility_pad(w, h, q.sc_f)
+    padded = np.pad(a, ((ph // 2, ph - ph // 2), (pw // 2, pw - pw // 2), (0, 0)), mode="edge")
+    want = O.build_pyramid(padded, q, q.p_samp_s)
+    got = ctx.pyramid_host(a, p)
+    for s in want:
+        for k, name in enumerate(("img", "dx", "dy")):
+            assert_bitexact(got[s][k], want[s][k], f"level {s} {name}")
+
+
+def test_ofclass_host_api_bitexact(oracle, od):
+    """OFC::OFClass mirror (oflow.h:99-126) with caller-built pyramids, incl. an initflow."""
+    O = oracle
+    w, h = 320, 240
+    a, b = od.synth_pair(w, h, 1, 5, 1)
+    q = O.oppoint(2, w, 1, 1)
+    pa, pb = O.build_pyramid(a, q, 8), O.build_pyramid(b, q, 8)
+    L = [None] * 32
+    lists = []
+    for pyr in (pa, pb):
+        for k in range(3):
+            lst = list(L)
+            for s, v in pyr.items():
+                lst[s] = v[k]
+            lists.append(lst)
+    rng = np.random.default_rng(0)
+    init = (rng.standard_normal(((h >> (q.sc_f + 1)), (w >> (q.sc_f + 1)), 2)) * 0.5).astype(np.float32)
+    for initflow in (None, init):
+        out = np.zeros((h >> q.sc_l) * (w >> q.sc_l) * 2, np.float32)
+        od.OFClass(*lists, 8, out, initflow, w, h, q.sc_f, q.sc_l, q.max_iter, q.min_iter, q.dp_thresh,
+                   q.dr_thresh, q.res_thresh, q.p_samp_s, q.patove, False, q.costfct, 1, q.patnorm, True,
+                   q.tv_alpha, q.tv_gamma, q.tv_delta, q.tv_innerit, q.tv_solverit, q.tv_sor, 0)
+        want = O.oflow(pa, pb, w, h, q, 8, initflow=initflow)
+        assert_bitexact(out.reshape(want.shape), want, f"OFClass initflow={initflow is not None}")
+
+
+def test_batch_equals_singles(od, ctx):
+    """Frame i of a batch equals the same pair run alone (no cross-frame leakage)."""
+    import torch
+    w, h, n = 320, 240, 5
+    pairs = [od.synth_pair(w, h, 1, f, 1) for f in range(n)]
+    a = torch.from_numpy(np.stack([x[0] for x in pairs])).cuda()
+    b = torch.from_numpy(np.stack([x[1] for x in pairs])).cuda()
+    p = od.oppoint(2, w, 1, 1)
+    out = ctx.run(a, b, p)
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    for f in range(n):
+        single = ctx.run_host(pairs[f][0], pairs[f][1], p)
+        assert_bitexact(out[f], single, f"batch frame {f}")
+
+
+def test_full_1080p_bitexact(oracle, od, ctx):
+    """BASELINE config B size (1920x1080, op-point 2): GPU == oracle bit-for-bit."""
+    a, b = od.synth_pair(1920, 1080, 1, 0, 1)
+    p = od.oppoint(2, 1920, 1, 1)
+    got = ctx.run_host(a, b, p)
+    ref = oracle.run_u8(a, b, oracle.oppoint(2, 1920, 1, 1))
+    assert_bitexact(got, ref, "1080p op2")
