@@ -128,6 +128,10 @@ int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int
  * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL). */
 int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, float *const *tv_flow, int nscales);
 
+/* Tuning / A-B switches: "sor_generic" (0/1) forces the generic global-memory SOR wavefront instead of
+ * the register-pipelined one (both are exact-order; used by the parity tests). */
+int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);
+
 /* HIP-event timing of individual kernels on the launch stream (used by bench.py for the roofline). */
 int ofdis_context_enable_kernel_timing(ofdis_context *ctx, int enable);
 /* Accumulated device time (ms) and launch count for kernel `name` since timing was enabled. */

@@ -102,6 +102,7 @@ def lib():
         "ofdis_run_batch_u8_host": ([vp, vp, vp, i, i, i, P, vp], i),
         "ofdis_pyramid_u8_host": ([vp, vp, i, i, P, i, vp, vp, vp], i),
         "ofdis_context_set_stage_capture": ([vp, vp, vp, i], i),
+        "ofdis_context_set_option": ([vp, C.c_char_p, i], i),
         "ofdis_context_enable_kernel_timing": ([vp, i], i),
         "ofdis_context_kernel_time": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_long)], i),
         "ofdis_kernel_names": ([], C.c_char_p),

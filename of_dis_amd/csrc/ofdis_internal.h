@@ -65,19 +65,26 @@ struct AggArgs {
   LevelGeom g;
 };
 
+// TV arrays use a SKEWED (anti-diagonal-major) layout: pixel (x, y) of a w x h level lives at
+// (x + y) * h + y of a plane of sp = (w + h - 1) * h floats, so the pixels of one wavefront step
+// t = x + y are contiguous (lane = row y).  Both the stencil kernels (neighbours at +-h, +-(h+1)) and the
+// exact-order SOR wavefront read it fully coalesced.
 struct TvArgs {
   // level images (padded interleaved) and flow
   const float *img_a, *img_b;
-  float *flow;                 // planar [n][nop][h][w]  (wx, wy)
-  float *du, *dv, *mask;       // [n][h][w]
+  float *flow;                 // planar row-major [n][nop][h][w]  (wx, wy)
+  float *wxs, *wys;            // skewed copies of the flow at the start of the level [n][sp]
+  float *du, *dv, *mask, *s;   // skewed [n][sp]
   float *a11, *a12, *a22, *b1, *b2, *sh, *sv;
-  float *t, *dt;               // [n][noc][h][w]
-  float *Ix, *Iy, *Iz, *Ixx, *Ixy, *Iyy, *Ixz, *Iyz;  // [n][noc][h][w]
+  float *t, *dt;               // skewed [n][noc][sp]
+  float *Ix, *Iy, *Iz, *Ixx, *Ixy, *Iyy, *Ixz, *Iyz;  // skewed [n][noc][sp]
+  long sp;                     // skewed plane size (w + h - 1) * h
   int n, nop, noc, w, h, pad, W;
   float quarter_alpha, hdo3, hgo3, omega;
   int first_iter;              // uu = wx (memcpy) on the first inner iteration
   int solverit;
   int camlr;
+  int sor_generic;             // force the generic global-memory SOR wavefront (A/B testing)
 };
 
 struct UpArgs {
@@ -94,6 +101,7 @@ void launch_aggregate(const AggArgs &a, hipStream_t s);
 void launch_tv_prep(const TvArgs &a, hipStream_t s);
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s);
 void launch_tv_deriv2(const TvArgs &a, hipStream_t s);
+void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);

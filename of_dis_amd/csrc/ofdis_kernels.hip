@@ -13,11 +13,15 @@
 //   k_aggregate     patchgrid.cpp:213-275,377-397 (gather form, serial patch order, no atomics)
 //   k_tv_prep       opticalflow_aux.c:31-75 + :88-99 (warp, mask, mean / temporal images)
 //   k_tv_deriv1/2   opticalflow_aux.c:101-107 (5-tap derivative filters)
-//   k_tv_system     opticalflow_aux.c:138-223,408-747 (smoothness + data term + laplacian, LDS tile)
-//   k_tv_sor        solver.c:83-433 / :34-78 / :439-471 (exact lexicographic order as a wavefront)
+//   k_tv_smooth     opticalflow_aux.c:138-160 (robust smoothness weight)
+//   k_tv_system     opticalflow_aux.c:161-223,408-747 (diffusivities + data term + laplacian)
+//   k_tv_sor_pipe   solver.c:83-433 / :439-471 (exact lexicographic order: register-pipelined wavefront)
+//   k_tv_sor        same, generic global-memory wavefront (any size; also solver.c:34-78 fallback)
 //   k_tv_final      refine_variational.cpp:209-227,305-323
 //   k_upsample      run_dense.cpp:407-415 (x2^l, cv::resize INTER_LINEAR, crop)
 #include "ofdis_internal.h"
+
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -32,6 +36,8 @@ __device__ __forceinline__ float ssemin(float a, float b) { return (a < b) ? a :
 __device__ __forceinline__ float ssemax(float a, float b) { return (a > b) ? a : b; }
 
 inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+
 
 // ------------------------------------------------------------------------------------------------ pyramid
 
@@ -467,6 +473,10 @@ __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
 
 // ------------------------------------------------------------------------------------------------ variational
 
+__device__ __forceinline__ long skw(int x, int y, int h) { return (long)(x + y) * h + y; }
+
+// image_warp (opticalflow_aux.c:31-75) + the mean / temporal images of get_derivatives (:88-99), plus the
+// skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
 __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long plane = (long)a.w * a.h;
@@ -474,12 +484,13 @@ __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
   const int f = (int)(idx / plane);
   const long o = idx % plane;
   const int x = (int)(o % a.w), y = (int)(o / a.w);
+  const long fk = (long)f * a.sp + skw(x, y, a.h);
   const float wx = a.flow[(long)f * a.nop * plane + o];
   const float wy = a.nop == 2 ? a.flow[(long)f * a.nop * plane + plane + o] : 0.0f;
   const float xx = (float)x + wx, yy = (float)y + wy;
   const int xi = (int)floorf(xx), yi = (int)floorf(yy);
   const float dx = xx - (float)xi, dy = yy - (float)yi;
-  a.mask[idx] = (xx >= 0 && xx <= (float)(a.w - 1) && yy >= 0 && yy <= (float)(a.h - 1)) ? 1.0f : 0.0f;
+  a.mask[fk] = (xx >= 0 && xx <= (float)(a.w - 1) && yy >= 0 && yy <= (float)(a.h - 1)) ? 1.0f : 0.0f;
   const int x1 = clampi(xi, 0, a.w - 1), x2 = clampi(xi + 1, 0, a.w - 1);
   const int y1 = clampi(yi, 0, a.h - 1), y2 = clampi(yi + 1, 0, a.h - 1);
   const long fs = (long)a.W * (a.h + 2 * a.pad) * a.noc;
@@ -489,53 +500,65 @@ __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
     const float w2 = SB(x1, y1) * (1.0f - dx) * (1.0f - dy) + SB(x2, y1) * dx * (1.0f - dy) +
                      SB(x1, y2) * (1.0f - dx) * dy + SB(x2, y2) * dx * dy;
     const float i1 = A[((long)(y + a.pad) * a.W + x + a.pad) * a.noc + ch];
-    const long q = ((long)f * a.noc + ch) * plane + o;
+    const long q = ((long)f * a.noc + ch) * a.sp + skw(x, y, a.h);
     a.t[q] = 0.5f * (w2 + i1);
     a.dt[q] = w2 - i1;
   }
 #undef SB
-  a.du[idx] = 0.0f;
-  if (a.nop == 2) a.dv[idx] = 0.0f;
+  a.wxs[fk] = wx;
+  a.du[fk] = 0.0f;
+  if (a.nop == 2) {
+    a.wys[fk] = wy;
+    a.dv[fk] = 0.0f;
+  }
 }
 
 __constant__ float kK5[5] = {1.0f / 12.0f, -8.0f / 12.0f, -0.0f, 8.0f / 12.0f, -1.0f / 12.0f};
 __constant__ float kK3[3] = {-0.5f, -0.0f, 0.5f};
 
-__device__ __forceinline__ float conv5h(const float *s, int x, int y, int w) {
-  const float *r = s + (long)y * w;
-  const float s0 = r[clampi(x - 2, 0, w - 1)], s1 = r[clampi(x - 1, 0, w - 1)], s2 = r[x];
-  const float s3 = r[clampi(x + 1, 0, w - 1)], s4 = r[clampi(x + 2, 0, w - 1)];
+// 5-tap filters (image.cpp:419-624 fast paths) with replicate border, on a skewed plane.
+__device__ __forceinline__ float conv5h(const float *s, int x, int y, int w, int h) {
+  const float s0 = s[skw(clampi(x - 2, 0, w - 1), y, h)], s1 = s[skw(clampi(x - 1, 0, w - 1), y, h)];
+  const float s2 = s[skw(x, y, h)];
+  const float s3 = s[skw(clampi(x + 1, 0, w - 1), y, h)], s4 = s[skw(clampi(x + 2, 0, w - 1), y, h)];
   return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
 }
 __device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int h) {
-  const float s0 = s[(long)clampi(y - 2, 0, h - 1) * w + x], s1 = s[(long)clampi(y - 1, 0, h - 1) * w + x];
-  const float s2 = s[(long)y * w + x];
-  const float s3 = s[(long)clampi(y + 1, 0, h - 1) * w + x], s4 = s[(long)clampi(y + 2, 0, h - 1) * w + x];
+  const float s0 = s[skw(x, clampi(y - 2, 0, h - 1), h)], s1 = s[skw(x, clampi(y - 1, 0, h - 1), h)];
+  const float s2 = s[skw(x, y, h)];
+  const float s3 = s[skw(x, clampi(y + 1, 0, h - 1), h)], s4 = s[skw(x, clampi(y + 2, 0, h - 1), h)];
   return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
 }
 
+// decode a skewed-plane thread index; false for the padding triangles
+__device__ __forceinline__ bool skew_xy(long kk, int w, int h, int &x, int &y) {
+  y = (int)(kk % h);
+  x = (int)(kk / h) - y;
+  return x >= 0 && x < w;
+}
+
 __global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
-  const long plane = (long)a.w * a.h;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * a.noc * plane) return;
-  const long pl = idx / plane, o = idx % plane;
-  const int x = (int)(o % a.w), y = (int)(o / a.w);
-  const float *t = a.t + pl * plane, *dt = a.dt + pl * plane;
-  a.Ix[idx] = conv5h(t, x, y, a.w);
+  if (idx >= (long)a.n * a.noc * a.sp) return;
+  const long pl = idx / a.sp, kk = idx % a.sp;
+  int x, y;
+  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  const float *t = a.t + pl * a.sp, *dt = a.dt + pl * a.sp;
+  a.Ix[idx] = conv5h(t, x, y, a.w, a.h);
   a.Iy[idx] = conv5v(t, x, y, a.w, a.h);
-  a.Ixz[idx] = conv5h(dt, x, y, a.w);
+  a.Ixz[idx] = conv5h(dt, x, y, a.w, a.h);
   a.Iyz[idx] = conv5v(dt, x, y, a.w, a.h);
 }
 
 __global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
-  const long plane = (long)a.w * a.h;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * a.noc * plane) return;
-  const long pl = idx / plane, o = idx % plane;
-  const int x = (int)(o % a.w), y = (int)(o / a.w);
-  a.Ixx[idx] = conv5h(a.Ix + pl * plane, x, y, a.w);
-  a.Ixy[idx] = conv5v(a.Ix + pl * plane, x, y, a.w, a.h);
-  a.Iyy[idx] = conv5v(a.Iy + pl * plane, x, y, a.w, a.h);
+  if (idx >= (long)a.n * a.noc * a.sp) return;
+  const long pl = idx / a.sp, kk = idx % a.sp;
+  int x, y;
+  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  a.Ixx[idx] = conv5h(a.Ix + pl * a.sp, x, y, a.w, a.h);
+  a.Ixy[idx] = conv5v(a.Ix + pl * a.sp, x, y, a.w, a.h);
+  a.Iyy[idx] = conv5v(a.Iy + pl * a.sp, x, y, a.w, a.h);
 }
 
 #define DNORM (0.1f * 0.1f)
@@ -754,132 +777,133 @@ __device__ __forceinline__ void data_de(int noc, long plane, float u, float m, c
   B1 = (B1 - tmp3 * Ixz[0]) - tmp2 * Iyz[0];
 }
 
-constexpr int kTX = 32, kTY = 8;
-
-// One TV inner iteration's system assembly (refine_variational.cpp:195-199): smoothness weights
-// (compute_smoothness) from an LDS tile of uu/vv with a 2-pixel halo, data term, and laplacian.
+// uu / vv of the current inner iteration (refine_variational.cpp:189-190,209-222,305-320)
 template <int NOP>
-__global__ __launch_bounds__(kTX *kTY) void k_tv_system(TvArgs a) {
-  __shared__ float su[kTY + 4][kTX + 4], svv[kTY + 4][kTX + 4];
-  __shared__ float ss[kTY + 2][kTX + 2];
-  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY, f = blockIdx.z;
-  const int w = a.w, h = a.h;
-  const long plane = (long)w * h, fo = (long)f * plane;
-  const float *WX = a.flow + (long)f * NOP * plane, *WY = WX + plane;
-  const int tid = threadIdx.x;
-  for (int k = tid; k < (kTY + 4) * (kTX + 4); k += kTX * kTY) {
-    const int i = k % (kTX + 4), j = k / (kTX + 4);
-    const int gx = clampi(x0 - 2 + i, 0, w - 1), gy = clampi(y0 - 2 + j, 0, h - 1);
-    const long o = (long)gy * w + gx;
-    const float wx = WX[o];
-    float uu, vv;
-    if (NOP == 2) {
-      const float wy = WY[o];
-      uu = a.first_iter ? wx : wx + a.du[fo + o];
-      vv = a.first_iter ? wy : wy + a.dv[fo + o];
-    } else {
-      uu = a.first_iter ? wx : (a.camlr == 0 ? ssemin(wx + a.du[fo + o], 0.0f) : ssemax(wx + a.du[fo + o], 0.0f));
-      vv = 0.0f;  // wy_dummy (refine_variational.cpp:268,294)
-    }
-    su[j][i] = uu;
-    svv[j][i] = vv;
-  }
-  __syncthreads();
-  const float eps = 0.001f * 0.001f;
-  for (int k = tid; k < (kTY + 2) * (kTX + 2); k += kTX * kTY) {
-    const int i = k % (kTX + 2), j = k / (kTX + 2);
-    // s at (x0 - 1 + i, y0 - 1 + j): 3-tap central differences of the replicate-clamped tile
-    const float ux = kK3[0] * su[j + 1][i] + (kK3[1] * su[j + 1][i + 1] + kK3[2] * su[j + 1][i + 2]);
-    const float uy = kK3[0] * su[j][i + 1] + (kK3[1] * su[j + 1][i + 1] + kK3[2] * su[j + 2][i + 1]);
-    const float vx = kK3[0] * svv[j + 1][i] + (kK3[1] * svv[j + 1][i + 1] + kK3[2] * svv[j + 1][i + 2]);
-    const float vy = kK3[0] * svv[j][i + 1] + (kK3[1] * svv[j + 1][i + 1] + kK3[2] * svv[j + 2][i + 1]);
-    ss[j][i] = a.quarter_alpha / sqrtf(eps + ((ux * ux + uy * uy) + (vx * vx + vy * vy)));
-  }
-  __syncthreads();
-  const int tx = tid % kTX, ty = tid / kTX;
-  const int x = x0 + tx, y = y0 + ty;
-  if (x >= w || y >= h) return;
-  const long o = (long)y * w + x;
-  const float sc = ss[ty + 1][tx + 1];
-  const float shv = x < w - 1 ? sc + ss[ty + 1][tx + 2] : 0.0f;
-  const float svv_ = y < h - 1 ? sc + ss[ty + 2][tx + 1] : 0.0f;
-  const float shl = ss[ty + 1][tx] + sc;   // h[x-1] = s[x-1] + s[x]
-  const float svu = ss[ty][tx + 1] + sc;   // v[y-1] = s[y-1] + s[y]
-  const long q = (long)f * a.noc * plane + o;
-  const float m = a.mask[fo + o];
-  float A11, A12 = 0.0f, A22 = 0.0f, B1, B2 = 0.0f;
-  if (NOP == 2)
-    data_of(a.noc, plane, a.du[fo + o], a.dv[fo + o], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q,
-            a.Iyy + q, a.Ixz + q, a.Iyz + q, a.hdo3, a.hgo3, A11, A12, A22, B1, B2);
-  else
-    data_de(a.noc, plane, a.du[fo + o], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q, a.Iyy + q,
-            a.Ixz + q, a.Iyz + q, a.hdo3, a.hgo3, A11, B1);
-  // sub_laplacian (opticalflow_aux.c:194-223): b = ((((b - th[x-1]) + th[x]) - tv[y-1]) + tv[y])
-  {
-    const float c0 = WX[o];
-    if (x >= 1) B1 = B1 - shl * (c0 - WX[o - 1]);
-    if (x <= w - 2) B1 = B1 + shv * (WX[o + 1] - c0);
-    if (y >= 1) B1 = B1 - svu * (c0 - WX[o - w]);
-    if (y <= h - 2) B1 = B1 + svv_ * (WX[o + w] - c0);
-  }
-  if (NOP == 2) {
-    const float c0 = WY[o];
-    if (x >= 1) B2 = B2 - shl * (c0 - WY[o - 1]);
-    if (x <= w - 2) B2 = B2 + shv * (WY[o + 1] - c0);
-    if (y >= 1) B2 = B2 - svu * (c0 - WY[o - w]);
-    if (y <= h - 2) B2 = B2 + svv_ * (WY[o + w] - c0);
-  }
-  a.a11[fo + o] = A11;
-  a.b1[fo + o] = B1;
-  if (NOP == 2) {
-    a.a12[fo + o] = A12;
-    a.a22[fo + o] = A22;
-    a.b2[fo + o] = B2;
-  }
-  a.sh[fo + o] = shv;
-  a.sv[fo + o] = svv_;
+__device__ __forceinline__ float uu_at(const TvArgs &a, long fk) {
+  const float wx = a.wxs[fk];
+  if (a.first_iter) return wx;
+  if (NOP == 2) return wx + a.du[fk];
+  return a.camlr == 0 ? ssemin(wx + a.du[fk], 0.0f) : ssemax(wx + a.du[fk], 0.0f);
 }
 
-// Exact lexicographic Gauss-Seidel SOR as an anti-diagonal wavefront (one workgroup per frame).
-// Pixel (x, y) of sweep s runs at step t = x + y + 2 s: its left/top neighbours of the same sweep ran at
-// t-1, its right/bottom neighbours of the previous sweep at t-1, and no two pixels of one step touch
-// each other (parity), so in-place updates with one barrier per step reproduce solver.c's raster order
-// bit for bit.  MODE 0: sor_coupled block SOR (solver.c:83-433); 1: its point-SOR fallback for
-// width < 2 or height < 2 (solver.c:34-78); 2: sor_coupled_slow_but_readable_DE (solver.c:439-471).
+// compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
+template <int NOP>
+__global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)a.n * a.sp) return;
+  const long f0 = (idx / a.sp) * a.sp, kk = idx % a.sp;
+  int x, y;
+  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  const int w = a.w, h = a.h;
+  const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h);
+  const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h);
+  const float uc = uu_at<NOP>(a, idx);
+  const float ux = kK3[0] * uu_at<NOP>(a, kl) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kr));
+  const float uy = kK3[0] * uu_at<NOP>(a, ku) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kd));
+  float vx, vy;
+  if (NOP == 2) {
+    auto vv = [&](long k) { return a.first_iter ? a.wys[k] : a.wys[k] + a.dv[k]; };
+    const float vc = vv(idx);
+    vx = kK3[0] * vv(kl) + (kK3[1] * vc + kK3[2] * vv(kr));
+    vy = kK3[0] * vv(ku) + (kK3[1] * vc + kK3[2] * vv(kd));
+  } else {  // wy_dummy = 0 (refine_variational.cpp:268,294)
+    vx = kK3[0] * 0.0f + (kK3[1] * 0.0f + kK3[2] * 0.0f);
+    vy = vx;
+  }
+  const float eps = 0.001f * 0.001f;
+  a.s[idx] = a.quarter_alpha / sqrtf(eps + ((ux * ux + uy * uy) + (vx * vx + vy * vy)));
+}
+
+// One TV inner iteration's system (refine_variational.cpp:195-199): diffusivities from s
+// (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
+template <int NOP>
+__global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)a.n * a.sp) return;
+  const long fr = idx / a.sp, kk = idx % a.sp;
+  int x, y;
+  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  const int w = a.w, h = a.h;
+  const float *S = a.s;
+  const float sc = S[idx];
+  const float shv = x < w - 1 ? sc + S[idx + h] : 0.0f;        // h[x] = s[x] + s[x+1]
+  const float svv = y < h - 1 ? sc + S[idx + h + 1] : 0.0f;    // v[y] = s[y] + s[y+1]
+  const long q = fr * a.noc * a.sp + kk;
+  const float m = a.mask[idx];
+  float A11, A12 = 0.0f, A22 = 0.0f, B1, B2 = 0.0f;
+  if (NOP == 2)
+    data_of(a.noc, a.sp, a.du[idx], a.dv[idx], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q, a.Iyy + q,
+            a.Ixz + q, a.Iyz + q, a.hdo3, a.hgo3, A11, A12, A22, B1, B2);
+  else
+    data_de(a.noc, a.sp, a.du[idx], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q, a.Iyy + q, a.Ixz + q,
+            a.Iyz + q, a.hdo3, a.hgo3, A11, B1);
+  // b = ((((b - th[x-1]) + th[x]) - tv[y-1]) + tv[y]) with th[x] = h[x] (wx[x+1] - wx[x]) etc.
+  {
+    const float *WX = a.wxs;
+    const float c0 = WX[idx];
+    if (x >= 1) B1 = B1 - (S[idx - h] + sc) * (c0 - WX[idx - h]);
+    if (x <= w - 2) B1 = B1 + shv * (WX[idx + h] - c0);
+    if (y >= 1) B1 = B1 - (S[idx - h - 1] + sc) * (c0 - WX[idx - h - 1]);
+    if (y <= h - 2) B1 = B1 + svv * (WX[idx + h + 1] - c0);
+  }
+  if (NOP == 2) {
+    const float *WY = a.wys;
+    const float c0 = WY[idx];
+    if (x >= 1) B2 = B2 - (S[idx - h] + sc) * (c0 - WY[idx - h]);
+    if (x <= w - 2) B2 = B2 + shv * (WY[idx + h] - c0);
+    if (y >= 1) B2 = B2 - (S[idx - h - 1] + sc) * (c0 - WY[idx - h - 1]);
+    if (y <= h - 2) B2 = B2 + svv * (WY[idx + h + 1] - c0);
+    a.a12[idx] = A12;
+    a.a22[idx] = A22;
+    a.b2[idx] = B2;
+  }
+  a.a11[idx] = A11;
+  a.b1[idx] = B1;
+  a.sh[idx] = shv;
+  a.sv[idx] = svv;
+}
+
+// Generic exact-order SOR (any size / sweep count): one workgroup per frame, in-place skewed arrays in
+// global memory, one barrier per wavefront step.  Pixel (x, y) of sweep s runs at step t = x + y + 2 s:
+// its left/top neighbours of the same sweep ran at t-1, its right/bottom neighbours of the previous
+// sweep at t-1, and no two pixels of one step touch each other (parity), so this reproduces
+// solver.c's raster order bit for bit.  MODE 0: sor_coupled (solver.c:83-433); 1: its point-SOR
+// fallback for width < 2 or height < 2 (solver.c:34-78); 2: sor_coupled_slow_but_readable_DE (:439-471).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
   const int f = blockIdx.x;
   const int w = a.w, h = a.h, S = a.solverit;
-  const long fo = (long)f * w * h;
+  const long fo = (long)f * a.sp;
   float *du = a.du + fo, *dv = a.dv + fo, *a11 = a.a11 + fo, *a12 = a.a12 + fo, *a22 = a.a22 + fo;
   const float *b1 = a.b1 + fo, *b2 = a.b2 + fo, *hh = a.sh + fo, *vv = a.sv + fo;
   const float omega = a.omega;
   const int items = S * h;
   const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
+  const int L = h, U = h + 1;  // skewed offsets of the left (x-1) and upper (y-1) neighbours
   for (int t = 0; t < T; ++t) {
     for (int k = threadIdx.x; k < items; k += blockDim.x) {
       const int s = k / h, y = k - s * h;
       const int x = t - y - 2 * s;
       if (x < 0 || x >= w) continue;
-      const long o = (long)y * w + x;
+      const long o = skw(x, y, h);
       if (MODE == 0) {
-        const float hl = x > 0 ? hh[o - 1] : 0.0f, hr = hh[o];
-        const float ur = x < w - 1 ? du[o + 1] : 0.0f, vr = x < w - 1 ? dv[o + 1] : 0.0f;
+        const float hl = x > 0 ? hh[o - L] : 0.0f, hr = hh[o];
+        const float ur = x < w - 1 ? du[o + L] : 0.0f, vr = x < w - 1 ? dv[o + L] : 0.0f;
         float s1, s2, dpsis;
         if (y == 0) {
           dpsis = hl + (hr + vv[o]);
-          s1 = (b1[o] + hr * ur) + vv[o] * du[o + w];
-          s2 = (b2[o] + hr * vr) + vv[o] * dv[o + w];
+          s1 = (b1[o] + hr * ur) + vv[o] * du[o + U];
+          s2 = (b2[o] + hr * vr) + vv[o] * dv[o + U];
         } else if (y < h - 1) {
-          const float vt = vv[o - w];
+          const float vt = vv[o - U];
           dpsis = (hl + hr) + (vt + vv[o]);
-          s1 = ((hr * ur) + vt * du[o - w]) + (b1[o] + vv[o] * du[o + w]);
-          s2 = ((hr * vr) + vt * dv[o - w]) + (b2[o] + vv[o] * dv[o + w]);
+          s1 = ((hr * ur) + vt * du[o - U]) + (b1[o] + vv[o] * du[o + U]);
+          s2 = ((hr * vr) + vt * dv[o - U]) + (b2[o] + vv[o] * dv[o + U]);
         } else {
-          const float vt = vv[o - w];
+          const float vt = vv[o - U];
           dpsis = hl + (hr + vt);
-          s1 = (b1[o] + hr * ur) + vt * du[o - w];
-          s2 = (b2[o] + hr * vr) + vt * dv[o - w];
+          s1 = (b1[o] + hr * ur) + vt * du[o - U];
+          s2 = (b2[o] + hr * vr) + vt * dv[o - U];
         }
         float i11, i12, i22;
         if (s == 0) {
@@ -898,33 +922,238 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
         }
         float B1 = s1, B2 = s2;
         if (x > 0) {
-          B1 = hl * du[o - 1] + s1;
-          B2 = hl * dv[o - 1] + s2;
+          B1 = hl * du[o - L] + s1;
+          B2 = hl * dv[o - L] + s2;
         }
         const float u0 = du[o], v0 = dv[o];
         du[o] = u0 + omega * (i11 * B1 + i12 * B2 - u0);
         dv[o] = v0 + omega * (i12 * B1 + i22 * B2 - v0);
       } else if (MODE == 1) {
         float su = 0.0f, sv = 0.0f, sd = 0.0f;
-        if (y > 0) { su -= vv[o - w] * du[o - w]; sv -= vv[o - w] * dv[o - w]; sd += vv[o - w]; }
-        if (x > 0) { su -= hh[o - 1] * du[o - 1]; sv -= hh[o - 1] * dv[o - 1]; sd += hh[o - 1]; }
-        if (y < h - 1) { su -= vv[o] * du[o + w]; sv -= vv[o] * dv[o + w]; sd += vv[o]; }
-        if (x < w - 1) { su -= hh[o] * du[o + 1]; sv -= hh[o] * dv[o + 1]; sd += hh[o]; }
+        if (y > 0) { su -= vv[o - U] * du[o - U]; sv -= vv[o - U] * dv[o - U]; sd += vv[o - U]; }
+        if (x > 0) { su -= hh[o - L] * du[o - L]; sv -= hh[o - L] * dv[o - L]; sd += hh[o - L]; }
+        if (y < h - 1) { su -= vv[o] * du[o + U]; sv -= vv[o] * dv[o + U]; sd += vv[o]; }
+        if (x < w - 1) { su -= hh[o] * du[o + L]; sv -= hh[o] * dv[o + L]; sd += hh[o]; }
         const float A11 = a11[o] + sd, A12 = a12[o], A22 = a22[o] + sd;
         const float B1 = b1[o] - su, B2 = b2[o] - sv;
         du[o] = (1.0f - omega) * du[o] + omega / A11 * (B1 - A12 * dv[o]);
         dv[o] = (1.0f - omega) * dv[o] + omega / A22 * (B2 - A12 * du[o]);
       } else {
         float su = 0.0f, sd = 0.0f;
-        if (y > 0) { su -= vv[o - w] * du[o - w]; sd += vv[o - w]; }
-        if (x > 0) { su -= hh[o - 1] * du[o - 1]; sd += hh[o - 1]; }
-        if (y < h - 1) { su -= vv[o] * du[o + w]; sd += vv[o]; }
-        if (x < w - 1) { su -= hh[o] * du[o + 1]; sd += hh[o]; }
+        if (y > 0) { su -= vv[o - U] * du[o - U]; sd += vv[o - U]; }
+        if (x > 0) { su -= hh[o - L] * du[o - L]; sd += hh[o - L]; }
+        if (y < h - 1) { su -= vv[o] * du[o + U]; sd += vv[o]; }
+        if (x < w - 1) { su -= hh[o] * du[o + L]; sd += hh[o]; }
         const float A11 = a11[o] + sd, B1 = b1[o] - su;
         du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
       }
     }
     __syncthreads();
+  }
+}
+
+__device__ __forceinline__ float dpp_from_prev_lane(float v) {  // lane i <- lane i-1 (wave_shr:1)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_from_next_lane(float v) {  // lane i <- lane i+1 (wave_shl:1)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
+}
+
+// Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later (register ring).
+struct SorPix {
+  float i11, i12, i22, b1, b2, hl, hr, vv, vt;
+};
+
+// Register-pipelined exact-order SOR: thread = row y (h <= 1024), one workgroup per frame.  At step t the
+// thread runs sweep s on pixel x_s = t - y - 2 s for every s < S.  Left/right/own values come from its
+// own registers (the results of steps t-1 / t-2), top/bottom values from the neighbouring lanes by DPP
+// (and through LDS across wave boundaries), coefficients from the skewed arrays (one coalesced load per
+// array per step), so a wavefront step costs a few hundred cycles instead of a round trip to L2.
+// Same arithmetic, same order as k_tv_sor -> bit-identical results.  MODE 0: OF block SOR, 2: DE point SOR.
+template <int S, int MODE>
+__global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
+  constexpr int D = S > 1 ? 2 * (S - 1) : 1;  // ring depth
+  constexpr int NV = 2 * S + 1;                 // values exchanged per wave boundary
+  __shared__ float xtop[2][16][NV];             // published by each wave's lane 63: cu[*], cv[*], sv
+  __shared__ float xbot[2][16][NV];             // published by each wave's lane 0: cu[*], cv[*]
+  const int f = blockIdx.x, w = a.w, h = a.h;
+  const int y = threadIdx.x, lane = y & 63, wv = y >> 6, nw = (int)(blockDim.x >> 6);
+  const long fo = (long)f * a.sp;
+  float *du = a.du + fo, *dv = a.dv + fo;
+  const float *A11p = a.a11 + fo, *A12p = a.a12 + fo, *A22p = a.a22 + fo, *B1p = a.b1 + fo, *B2p = a.b2 + fo;
+  const float *SH = a.sh + fo, *SV = a.sv + fo;
+  const float omega = a.omega;
+  const bool has_top = y > 0, has_bot = y < h - 1;
+  float cu[S], cv[S], pu[S], pv[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) cu[s] = cv[s] = pu[s] = pv[s] = 0.0f;
+  SorPix ring[D];
+  float own_u = 0.0f, own_v = 0.0f;  // du/dv initial value at (y, x0): the "right" load of the previous step
+  if (y == 0 && w > 0) {  // row 0 starts at step 0: its first own value has no previous-step load
+    own_u = du[0];
+    if (MODE == 0) own_v = dv[0];
+  }
+  float hprev = 0.0f, svprev = 0.0f;
+  const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
+  // prefetched loads for the current step
+  float n11 = 0, n12 = 0, n22 = 0, nb1 = 0, nb2 = 0, nsh = 0, nsv = 0, nru = 0, nrv = 0, nbu = 0, nbv = 0;
+  auto load = [&](int t) {
+    const int x0 = t - y;
+    const long o = (long)t * h + y;  // skewed index of (x0, y)
+    const bool in = y < h && x0 >= 0 && x0 < w;
+    if (in) {
+      n11 = A11p[o]; nb1 = B1p[o]; nsh = SH[o]; nsv = SV[o];
+      if (MODE == 0) { n12 = A12p[o]; n22 = A22p[o]; nb2 = B2p[o]; }
+      if (has_bot) { nbu = du[o + h + 1]; if (MODE == 0) nbv = dv[o + h + 1]; }
+    }
+    if (y < h && x0 + 1 >= 0 && x0 + 1 < w) { nru = du[o + h]; if (MODE == 0) nrv = dv[o + h]; }
+  };
+  load(0);
+  for (int t = 0; t < T; ++t) {
+    const int par = t & 1;
+    const float c11 = n11, c12 = n12, c22 = n22, cb1 = nb1, cb2 = nb2, csh = nsh, csv = nsv;
+    const float cru = nru, crv = nrv, cbu = nbu, cbv = nbv;
+    if (t + 1 < T) load(t + 1);
+    // neighbour values from the previous step
+    float tu[S], tv[S], bu[S], bv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      tu[s] = dpp_from_prev_lane(cu[s]);
+      tv[s] = MODE == 0 ? dpp_from_prev_lane(cv[s]) : 0.0f;
+      bu[s] = dpp_from_next_lane(cu[s]);
+      bv[s] = MODE == 0 ? dpp_from_next_lane(cv[s]) : 0.0f;
+    }
+    float svt = dpp_from_prev_lane(svprev);
+    if (t > 0) {
+      if (lane == 0 && wv > 0) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) { tu[s] = xtop[par ^ 1][wv - 1][s]; tv[s] = xtop[par ^ 1][wv - 1][S + s]; }
+        svt = xtop[par ^ 1][wv - 1][2 * S];
+      }
+      if (lane == 63 && wv < nw - 1) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) { bu[s] = xbot[par ^ 1][wv + 1][s]; bv[s] = xbot[par ^ 1][wv + 1][S + s]; }
+      }
+    }
+    float nu[S], nvv[S];
+    const int x0 = t - y;
+    // ---- sweep 0 on pixel x0 (computes and stores the 2x2 inverse, solver.c:122-128)
+    SorPix d;
+    d.b1 = cb1; d.b2 = cb2; d.hr = csh; d.hl = x0 > 0 ? hprev : 0.0f; d.vv = csv; d.vt = has_top ? svt : 0.0f;
+    {
+      const float ur = x0 < w - 1 ? cru : 0.0f, vr = x0 < w - 1 ? crv : 0.0f;
+      if (MODE == 0) {
+        float s1, s2, dpsis;
+        if (!has_top) {
+          dpsis = d.hl + (d.hr + d.vv);
+          s1 = (d.b1 + d.hr * ur) + d.vv * cbu;
+          s2 = (d.b2 + d.hr * vr) + d.vv * cbv;
+        } else if (has_bot) {
+          dpsis = (d.hl + d.hr) + (d.vt + d.vv);
+          s1 = ((d.hr * ur) + d.vt * tu[0]) + (d.b1 + d.vv * cbu);
+          s2 = ((d.hr * vr) + d.vt * tv[0]) + (d.b2 + d.vv * cbv);
+        } else {
+          dpsis = d.hl + (d.hr + d.vt);
+          s1 = (d.b1 + d.hr * ur) + d.vt * tu[0];
+          s2 = (d.b2 + d.hr * vr) + d.vt * tv[0];
+        }
+        const float A11 = c22 + dpsis, A22 = c11 + dpsis;
+        const float det = A11 * A22 - c12 * c12;
+        d.i11 = A11 / det;
+        d.i22 = A22 / det;
+        d.i12 = c12 / (0.0f - det);
+        float B1 = s1, B2 = s2;
+        if (x0 > 0) {
+          B1 = d.hl * cu[0] + s1;
+          B2 = d.hl * cv[0] + s2;
+        }
+        nu[0] = own_u + omega * (d.i11 * B1 + d.i12 * B2 - own_u);
+        nvv[0] = own_v + omega * (d.i12 * B1 + d.i22 * B2 - own_v);
+      } else {
+        d.i11 = c11;
+        float su = 0.0f, sd = 0.0f;
+        if (has_top) { su -= d.vt * tu[0]; sd += d.vt; }
+        if (x0 > 0) { su -= d.hl * cu[0]; sd += d.hl; }
+        if (has_bot) { su -= d.vv * cbu; sd += d.vv; }
+        if (x0 < w - 1) { su -= d.hr * ur; sd += d.hr; }
+        const float A = c11 + sd, B = d.b1 - su;
+        nu[0] = (1.0f - omega) * own_u + omega * (B / A);
+        nvv[0] = 0.0f;
+      }
+    }
+    // ---- sweeps 1..S-1 on pixel x0 - 2 s, with the data sweep 0 saw 2 s steps ago
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+      const SorPix &e = ring[2 * s - 1];
+      const int xs = x0 - 2 * s;
+      const float ou = pu[s - 1], ov = pv[s - 1];             // own value after sweep s-1
+      const float ur = xs < w - 1 ? cu[s - 1] : 0.0f;         // right neighbour after sweep s-1
+      const float vr = xs < w - 1 ? cv[s - 1] : 0.0f;
+      if (MODE == 0) {
+        float s1, s2;
+        if (!has_top) {
+          s1 = (e.b1 + e.hr * ur) + e.vv * bu[s - 1];
+          s2 = (e.b2 + e.hr * vr) + e.vv * bv[s - 1];
+        } else if (has_bot) {
+          s1 = ((e.hr * ur) + e.vt * tu[s]) + (e.b1 + e.vv * bu[s - 1]);
+          s2 = ((e.hr * vr) + e.vt * tv[s]) + (e.b2 + e.vv * bv[s - 1]);
+        } else {
+          s1 = (e.b1 + e.hr * ur) + e.vt * tu[s];
+          s2 = (e.b2 + e.hr * vr) + e.vt * tv[s];
+        }
+        float B1 = s1, B2 = s2;
+        if (xs > 0) {
+          B1 = e.hl * cu[s] + s1;
+          B2 = e.hl * cv[s] + s2;
+        }
+        nu[s] = ou + omega * (e.i11 * B1 + e.i12 * B2 - ou);
+        nvv[s] = ov + omega * (e.i12 * B1 + e.i22 * B2 - ov);
+      } else {
+        float su = 0.0f, sd = 0.0f;
+        if (has_top) { su -= e.vt * tu[s]; sd += e.vt; }
+        if (xs > 0) { su -= e.hl * cu[s]; sd += e.hl; }
+        if (has_bot) { su -= e.vv * bu[s - 1]; sd += e.vv; }
+        if (xs < w - 1) { su -= e.hr * ur; sd += e.hr; }
+        const float A = e.i11 + sd, B = e.b1 - su;
+        nu[s] = (1.0f - omega) * ou + omega * (B / A);
+        nvv[s] = 0.0f;
+      }
+    }
+    // ---- the last sweep's result is final
+    {
+      const int xl = x0 - 2 * (S - 1);
+      if (y < h && xl >= 0 && xl < w) {
+        const long o = (long)(t - 2 * (S - 1)) * h + y;
+        du[o] = nu[S - 1];
+        if (MODE == 0) dv[o] = nvv[S - 1];
+      }
+    }
+    // ---- rotate registers
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      pu[s] = cu[s]; pv[s] = cv[s];
+      cu[s] = nu[s]; cv[s] = nvv[s];
+    }
+    if (S > 1) {
+#pragma unroll
+      for (int j = D - 1; j > 0; --j) ring[j] = ring[j - 1];
+      ring[0] = d;
+    }
+    own_u = cru; own_v = crv;
+    hprev = csh; svprev = csv;
+    // ---- publish wave-boundary values, one barrier per step
+    if (nw > 1) {
+      if (lane == 63) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) { xtop[par][wv][s] = cu[s]; xtop[par][wv][S + s] = cv[s]; }
+        xtop[par][wv][2 * S] = svprev;
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) { xbot[par][wv][s] = cu[s]; xbot[par][wv][S + s] = cv[s]; }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -934,12 +1163,13 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
   if (idx >= (long)a.n * plane) return;
   const int f = (int)(idx / plane);
   const long o = idx % plane;
+  const long fk = (long)f * a.sp + skw((int)(o % a.w), (int)(o / a.w), a.h);
   float *WX = a.flow + (long)f * a.nop * plane;
   if (a.nop == 2) {
-    WX[o] = WX[o] + a.du[idx];
-    WX[plane + o] = WX[plane + o] + a.dv[idx];
+    WX[o] = a.wxs[fk] + a.du[fk];
+    WX[plane + o] = a.wys[fk] + a.dv[fk];
   } else {
-    const float s = WX[o] + a.du[idx];
+    const float s = a.wxs[fk] + a.du[fk];
     WX[o] = a.camlr == 0 ? ssemin(s, 0.0f) : ssemax(s, 0.0f);
   }
 }
@@ -1032,23 +1262,45 @@ void launch_tv_prep(const TvArgs &a, hipStream_t s) {
   k_tv_prep<<<ceil_div((long)a.n * a.w * a.h, 256), 256, 0, s>>>(a);
 }
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
-  k_tv_deriv1<<<ceil_div((long)a.n * a.noc * a.w * a.h, 256), 256, 0, s>>>(a);
+  k_tv_deriv1<<<ceil_div((long)a.n * a.noc * a.sp, 256), 256, 0, s>>>(a);
 }
 void launch_tv_deriv2(const TvArgs &a, hipStream_t s) {
-  k_tv_deriv2<<<ceil_div((long)a.n * a.noc * a.w * a.h, 256), 256, 0, s>>>(a);
+  k_tv_deriv2<<<ceil_div((long)a.n * a.noc * a.sp, 256), 256, 0, s>>>(a);
+}
+void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
+  if (a.nop == 2)
+    k_tv_smooth<2><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
+  else
+    k_tv_smooth<1><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
 }
 void launch_tv_system(const TvArgs &a, hipStream_t s) {
-  dim3 grid(ceil_div(a.w, kTX), ceil_div(a.h, kTY), a.n);
   if (a.nop == 2)
-    k_tv_system<2><<<grid, kTX * kTY, 0, s>>>(a);
+    k_tv_system<2><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
   else
-    k_tv_system<1><<<grid, kTX * kTY, 0, s>>>(a);
+    k_tv_system<1><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
+}
+template <int S>
+static void sor_pipe(const TvArgs &a, hipStream_t s) {
+  const int threads = ((a.h + 63) / 64) * 64;
+  if (a.nop == 2)
+    k_tv_sor_pipe<S, 0><<<a.n, threads, 0, s>>>(a);
+  else
+    k_tv_sor_pipe<S, 2><<<a.n, threads, 0, s>>>(a);
 }
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
+  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2);
+  if (!tiny && a.h <= 1024 && a.solverit <= 4 && !a.sor_generic) {
+    switch (a.solverit) {
+      case 1: sor_pipe<1>(a, s); return;
+      case 2: sor_pipe<2>(a, s); return;
+      case 3: sor_pipe<3>(a, s); return;
+      case 4: sor_pipe<4>(a, s); return;
+    }
+  }
   if (a.nop == 1)
     k_tv_sor<2><<<a.n, 256, 0, s>>>(a);
-  else if (a.w < 2 || a.h < 2)
+  else if (tiny)
     k_tv_sor<1><<<a.n, 256, 0, s>>>(a);
   else
     k_tv_sor<0><<<a.n, 256, 0, s>>>(a);

@@ -7,6 +7,7 @@
 // verbosity timers or a host-buffer entry point asks for it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -55,6 +56,7 @@ struct ofdis_context {
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
   std::map<int, std::pair<double, long>> acc;
+  int opt_sor_generic = 0;
   std::mutex mu;
 };
 
@@ -181,8 +183,10 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
   P.off_pw = off;
   off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
   P.off_tv = off;
-  P.tv_plane = max_plane;
-  if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_plane * (10 + 9 * (size_t)P.noc));
+  size_t max_sp = 0;  // skewed TV plane (w + h - 1) * h
+  for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, (size_t)(g.w + g.h - 1) * g.h);
+  P.tv_plane = max_sp;
+  if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_sp * (13 + 9 * (size_t)P.noc));
   P.total = off;
   return P;
 }
@@ -190,7 +194,7 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
 int ensure_ws(ofdis_context *c, size_t bytes) {
   if (bytes <= c->ws_cap) return OFDIS_OK;
   if (c->ws) {
-    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipDeviceSynchronize());  // callers may have queued work on their own streams
     HIP_OK(hipFree(c->ws));
     c->ws = nullptr;
     c->ws_cap = 0;
@@ -296,7 +300,8 @@ int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream
 
     const int n_inner = p->tv_innerit * (sl + 1);  // refine_variational.cpp:36
     if (p->usetvref && n_inner > 0) {
-      const size_t pl = (size_t)n * g.w * g.h;
+      const long sp = (long)(g.w + g.h - 1) * g.h;
+      const size_t pl = (size_t)n * sp;
       float *t0 = (float *)(ws + P.off_tv);
       TvArgs tv{};
       tv.img_a = img;
@@ -312,7 +317,11 @@ int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream
       tv.b2 = t0 + 7 * pl;
       tv.sh = t0 + 8 * pl;
       tv.sv = t0 + 9 * pl;
-      float *cp = t0 + 10 * pl;
+      tv.s = t0 + 10 * pl;
+      tv.wxs = t0 + 11 * pl;
+      tv.wys = t0 + 12 * pl;
+      tv.sp = sp;
+      float *cp = t0 + 13 * pl;
       const size_t cpl = pl * noc;
       tv.t = cp;
       tv.dt = cp + cpl;
@@ -337,6 +346,7 @@ int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream
       tv.omega = p->tv_sor;
       tv.solverit = p->tv_solverit;
       tv.camlr = 0;
+      tv.sor_generic = c->opt_sor_generic;
       timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
       timed(c, 6, s, [&] {
         launch_tv_deriv1(tv, s);
@@ -344,7 +354,10 @@ int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream
       });
       for (int it = 0; it < n_inner; ++it) {
         tv.first_iter = it == 0;
-        timed(c, 7, s, [&] { launch_tv_system(tv, s); });
+        timed(c, 7, s, [&] {
+          launch_tv_smooth(tv, s);
+          launch_tv_system(tv, s);
+        });
         timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
       }
       timed(c, 9, s, [&] { launch_tv_final(tv, s); });
@@ -596,6 +609,16 @@ int ofdis_context_set_stage_capture(ofdis_context *c, float *const *dis_flow, fl
     if (tv_flow) c->cap_tv[i] = tv_flow[i];
   }
   return OFDIS_OK;
+}
+
+int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
+  if (!c || !key) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lock(c->mu);
+  if (std::strcmp(key, "sor_generic") == 0) {
+    c->opt_sor_generic = value != 0;
+    return OFDIS_OK;
+  }
+  return OFDIS_ERR_INVALID_ARGUMENT;
 }
 
 int ofdis_context_enable_kernel_timing(ofdis_context *c, int enable) {

@@ -204,6 +204,9 @@ class Context:
                 self._keep.append(a)
         check(lib().ofdis_context_set_stage_capture(self._h, d, t, nscales), "capture")
 
+    def set_option(self, key: str, value: int):
+        check(lib().ofdis_context_set_option(self._h, key.encode(), int(value)), f"option {key}")
+
     def enable_kernel_timing(self, on: bool = True):
         check(lib().ofdis_context_enable_kernel_timing(self._h, int(on)), "timing")
 

@@ -82,6 +82,20 @@ def test_pipeline_bitexact(oracle, od, ctx, w, h, noc, mode, op, over):
     assert_bitexact(got, ref, "full-resolution flow")
 
 
+@pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in CASES if c[0] <= 200])
+def test_generic_sor_bitexact(oracle, od, ctx, w, h, noc, mode, op, over):
+    """The generic global-memory SOR wavefront gives the same bits as the register-pipelined one."""
+    a, b = od.synth_pair(w, h, noc, 4, mode)
+    p, q = _params(od, oracle, w, noc, mode, op, over)
+    ref = oracle.run_u8(a, b, q)
+    ctx.set_option("sor_generic", 1)
+    try:
+        got = ctx.run_host(a, b, p)
+    finally:
+        ctx.set_option("sor_generic", 0)
+    assert_bitexact(got, ref, "generic SOR path")
+
+
 @pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2)])
 def test_pyramid_bitexact(oracle, od, ctx, w, h, noc, op):
     O = oracle
