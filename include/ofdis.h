@@ -128,8 +128,13 @@ int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int
  * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL). */
 int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, float *const *tv_flow, int nscales);
 
-/* Tuning / A-B switches: "sor_generic" (0/1) forces the generic global-memory SOR wavefront instead of
- * the register-pipelined one (both are exact-order; used by the parity tests). */
+/* Tuning / A-B switches:
+ *   "sor_generic" (0/1): force the generic global-memory SOR wavefront instead of the register-pipelined
+ *                        one (both are exact-order; used by the parity tests);
+ *   "streams" (1-16, default 4) and "chunk" (frames, default 32, 0 = whole batch): a batch is cut into
+ *                        chunks that run round-robin on that many HIP streams with separate workspaces,
+ *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels.
+ * Results never depend on these settings (frames are independent). */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);
 
 /* HIP-event timing of individual kernels on the launch stream (used by bench.py for the roofline). */

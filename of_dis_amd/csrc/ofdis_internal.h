@@ -75,10 +75,10 @@ struct TvArgs {
   float *flow;                 // planar row-major [n][nop][h][w]  (wx, wy)
   float *wxs, *wys;            // skewed copies of the flow at the start of the level [n][sp]
   float *du, *dv, *mask, *s;   // skewed [n][sp]
-  float *a11, *a12, *a22, *b1, *b2, *sh, *sv;
+  float *coef;                 // AoS per pixel: OF (a11,a12,a22,b1)(b2,sh,sv,-) = 8 floats; DE (a11,b1,sh,sv)
   float *t, *dt;               // skewed [n][noc][sp]
   float *Ix, *Iy, *Iz, *Ixx, *Ixy, *Iyy, *Ixz, *Iyz;  // skewed [n][noc][sp]
-  long sp;                     // skewed plane size (w + h - 1) * h
+  long sp;                     // skewed plane stride: (w + h - 1) * h pixels + 64 dump slots (SOR)
   int n, nop, noc, w, h, pad, W;
   float quarter_alpha, hdo3, hgo3, omega;
   int first_iter;              // uu = wx (memcpy) on the first inner iteration

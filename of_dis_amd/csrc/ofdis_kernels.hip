@@ -42,40 +42,49 @@ inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
 // ------------------------------------------------------------------------------------------------ pyramid
 
 __global__ __launch_bounds__(256) void k_pyr_base(PyrBaseArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = 2L * a.n * a.h * a.w;
-  if (idx >= total) return;
-  const int x = (int)(idx % a.w);
-  const long r = idx / a.w;
-  const int y = (int)(r % a.h);
-  const int f = (int)(r / a.h);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= a.w) return;
+  const long idx = ((long)f * a.h + y) * a.w + x;
   const long fs = (long)a.H0 * a.W0 * a.noc;
   const uint8_t *src = f < a.n ? a.img_a + (long)f * fs : a.img_b + (long)(f - a.n) * fs;
   const int B = 1 << a.log2s;
   // 2^l x 2^l box mean of the replicate-padded u8 image.  The sum is an integer < 2^24 and the scale
   // is a power of two, so this equals the reference's repeated ((a+b)+(c+d))*0.25 exactly (l <= 8).
   const float scale = 1.0f / (float)(1 << (2 * a.log2s));
+  const int x0 = x * B - a.padl;
+  // fast path: intensity image, block row fully inside and 16-byte aligned -> uint4 loads + v_sad_u8
+  if (a.noc == 1 && B >= 16 && x0 >= 0 && x0 + B <= a.W0 && ((((uintptr_t)src) + x0) & 15) == 0 && (a.W0 & 15) == 0) {
+    unsigned sum = 0;
+    for (int by = 0; by < B; ++by) {
+      const int yy = clampi(y * B + by - a.padt, 0, a.H0 - 1);
+      const uint4 *row = reinterpret_cast<const uint4 *>(src + (long)yy * a.W0 + x0);
+      for (int q = 0; q < B / 16; ++q) {
+        const uint4 v = row[q];
+        sum = __builtin_amdgcn_sad_u8(v.x, 0u, sum);
+        sum = __builtin_amdgcn_sad_u8(v.y, 0u, sum);
+        sum = __builtin_amdgcn_sad_u8(v.z, 0u, sum);
+        sum = __builtin_amdgcn_sad_u8(v.w, 0u, sum);
+      }
+    }
+    a.out[idx] = (float)sum * scale;
+    return;
+  }
   for (int c = 0; c < a.noc; ++c) {
     unsigned sum = 0;
     for (int by = 0; by < B; ++by) {
       const int yy = clampi(y * B + by - a.padt, 0, a.H0 - 1);
       const uint8_t *row = src + (long)yy * a.W0 * a.noc + c;
-      for (int bx = 0; bx < B; ++bx) sum += row[clampi(x * B + bx - a.padl, 0, a.W0 - 1) * a.noc];
+      for (int bx = 0; bx < B; ++bx) sum += row[clampi(x0 + bx, 0, a.W0 - 1) * a.noc];
     }
     a.out[idx * a.noc + c] = (float)sum * scale;
   }
 }
 
 __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)a.n2 * a.h * a.w * a.noc;
-  if (idx >= total) return;
-  const int c = (int)(idx % a.noc);
-  long r = idx / a.noc;
-  const int x = (int)(r % a.w);
-  r /= a.w;
-  const int y = (int)(r % a.h);
-  const int f = (int)(r / a.h);
+  const int xc = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (xc >= a.w * a.noc) return;
+  const int x = xc / a.noc, c = xc - x * a.noc;
+  const long idx = (((long)f * a.h + y) * a.w + x) * a.noc + c;
   const int sw = 2 * a.w;
   const float *s = a.src + (long)f * (2 * a.h) * sw * a.noc;
   const float p = s[((2 * y) * sw + 2 * x) * a.noc + c], q = s[((2 * y) * sw + 2 * x + 1) * a.noc + c];
@@ -92,13 +101,9 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 
 __global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
   const int W = a.w + 2 * a.pad, H = a.h + 2 * a.pad;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)a.n2 * H * W;
-  if (idx >= total) return;
-  const int X = (int)(idx % W);
-  const long r = idx / W;
-  const int Y = (int)(r % H);
-  const int f = (int)(r / H);
+  const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y, f = blockIdx.z;
+  if (X >= W) return;
+  const long idx = ((long)f * H + Y) * W + X;
   const int sx = X - a.pad, sy = Y - a.pad;
   const int noc = a.noc, w = a.w;
   const float *L = a.lvl + (long)f * a.h * a.w * noc;
@@ -416,13 +421,8 @@ __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : 
 
 __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
   const LevelGeom &g = a.g;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)a.n * g.w * g.h;
-  if (idx >= total) return;
-  const int x = (int)(idx % g.w);
-  const long r = idx / g.w;
-  const int y = (int)(r % g.h);
-  const int f = (int)(r / g.h);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= g.w) return;
   const int hp = a.p / 2;
   // patches whose footprint [pt - p/2, pt + p/2 - 1] covers x, visited in ascending patch id
   const int pxlo = max(0, -floordiv(-(x - hp + 1 - g.offw), a.steps));
@@ -478,12 +478,10 @@ __device__ __forceinline__ long skw(int x, int y, int h) { return (long)(x + y) 
 // image_warp (opticalflow_aux.c:31-75) + the mean / temporal images of get_derivatives (:88-99), plus the
 // skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
 __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= a.w) return;
   const long plane = (long)a.w * a.h;
-  if (idx >= (long)a.n * plane) return;
-  const int f = (int)(idx / plane);
-  const long o = idx % plane;
-  const int x = (int)(o % a.w), y = (int)(o / a.w);
+  const long o = (long)y * a.w + x;
   const long fk = (long)f * a.sp + skw(x, y, a.h);
   const float wx = a.flow[(long)f * a.nop * plane + o];
   const float wy = a.nop == 2 ? a.flow[(long)f * a.nop * plane + plane + o] : 0.0f;
@@ -531,16 +529,17 @@ __device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int
 }
 
 // decode a skewed-plane thread index; false for the padding triangles
-__device__ __forceinline__ bool skew_xy(long kk, int w, int h, int &x, int &y) {
-  y = (int)(kk % h);
-  x = (int)(kk / h) - y;
+__device__ __forceinline__ bool skew_xy(int kk, int w, int h, int &x, int &y) {
+  const int t = kk / h;
+  y = kk - t * h;
+  x = t - y;
   return x >= 0 && x < w;
 }
 
 __global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * a.noc * a.sp) return;
-  const long pl = idx / a.sp, kk = idx % a.sp;
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk >= a.sp) return;
+  const long pl = blockIdx.y, idx = pl * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const float *t = a.t + pl * a.sp, *dt = a.dt + pl * a.sp;
@@ -551,9 +550,9 @@ __global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * a.noc * a.sp) return;
-  const long pl = idx / a.sp, kk = idx % a.sp;
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk >= a.sp) return;
+  const long pl = blockIdx.y, idx = pl * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   a.Ixx[idx] = conv5h(a.Ix + pl * a.sp, x, y, a.w, a.h);
@@ -789,9 +788,9 @@ __device__ __forceinline__ float uu_at(const TvArgs &a, long fk) {
 // compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
 template <int NOP>
 __global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * a.sp) return;
-  const long f0 = (idx / a.sp) * a.sp, kk = idx % a.sp;
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk >= a.sp) return;
+  const long f0 = (long)blockIdx.y * a.sp, idx = f0 + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const int w = a.w, h = a.h;
@@ -818,9 +817,9 @@ __global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
 // (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
 template <int NOP>
 __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * a.sp) return;
-  const long fr = idx / a.sp, kk = idx % a.sp;
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk >= a.sp) return;
+  const long fr = blockIdx.y, idx = fr * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const int w = a.w, h = a.h;
@@ -853,14 +852,12 @@ __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
     if (x <= w - 2) B2 = B2 + shv * (WY[idx + h] - c0);
     if (y >= 1) B2 = B2 - (S[idx - h - 1] + sc) * (c0 - WY[idx - h - 1]);
     if (y <= h - 2) B2 = B2 + svv * (WY[idx + h + 1] - c0);
-    a.a12[idx] = A12;
-    a.a22[idx] = A22;
-    a.b2[idx] = B2;
+    float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
+    C[0] = make_float4(A11, A12, A22, B1);
+    C[1] = make_float4(B2, shv, svv, 0.0f);
+  } else {
+    reinterpret_cast<float4 *>(a.coef)[idx] = make_float4(A11, B1, shv, svv);
   }
-  a.a11[idx] = A11;
-  a.b1[idx] = B1;
-  a.sh[idx] = shv;
-  a.sv[idx] = svv;
 }
 
 // Generic exact-order SOR (any size / sweep count): one workgroup per frame, in-place skewed arrays in
@@ -874,8 +871,11 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
   const int f = blockIdx.x;
   const int w = a.w, h = a.h, S = a.solverit;
   const long fo = (long)f * a.sp;
-  float *du = a.du + fo, *dv = a.dv + fo, *a11 = a.a11 + fo, *a12 = a.a12 + fo, *a22 = a.a22 + fo;
-  const float *b1 = a.b1 + fo, *b2 = a.b2 + fo, *hh = a.sh + fo, *vv = a.sv + fo;
+  float *du = a.du + fo, *dv = a.dv + fo;
+  float4 *C = reinterpret_cast<float4 *>(a.coef) + fo * (MODE == 2 ? 1 : 2);
+  // AoS accessors: OF (a11, a12, a22, b1) (b2, sh, sv, -); DE (a11, b1, sh, sv)
+#define SH_(o) (MODE == 2 ? C[o].z : C[2 * (o) + 1].y)
+#define SV_(o) (MODE == 2 ? C[o].w : C[2 * (o) + 1].z)
   const float omega = a.omega;
   const int items = S * h;
   const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
@@ -887,38 +887,41 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
       if (x < 0 || x >= w) continue;
       const long o = skw(x, y, h);
       if (MODE == 0) {
-        const float hl = x > 0 ? hh[o - L] : 0.0f, hr = hh[o];
+        float4 &c0 = C[2 * o];
+        const float4 c1 = C[2 * o + 1];
+        const float b1 = c0.w, b2 = c1.x, hr = c1.y, vo = c1.z;
+        const float hl = x > 0 ? SH_(o - L) : 0.0f;
         const float ur = x < w - 1 ? du[o + L] : 0.0f, vr = x < w - 1 ? dv[o + L] : 0.0f;
         float s1, s2, dpsis;
         if (y == 0) {
-          dpsis = hl + (hr + vv[o]);
-          s1 = (b1[o] + hr * ur) + vv[o] * du[o + U];
-          s2 = (b2[o] + hr * vr) + vv[o] * dv[o + U];
+          dpsis = hl + (hr + vo);
+          s1 = (b1 + hr * ur) + vo * du[o + U];
+          s2 = (b2 + hr * vr) + vo * dv[o + U];
         } else if (y < h - 1) {
-          const float vt = vv[o - U];
-          dpsis = (hl + hr) + (vt + vv[o]);
-          s1 = ((hr * ur) + vt * du[o - U]) + (b1[o] + vv[o] * du[o + U]);
-          s2 = ((hr * vr) + vt * dv[o - U]) + (b2[o] + vv[o] * dv[o + U]);
+          const float vt = SV_(o - U);
+          dpsis = (hl + hr) + (vt + vo);
+          s1 = ((hr * ur) + vt * du[o - U]) + (b1 + vo * du[o + U]);
+          s2 = ((hr * vr) + vt * dv[o - U]) + (b2 + vo * dv[o + U]);
         } else {
-          const float vt = vv[o - U];
+          const float vt = SV_(o - U);
           dpsis = hl + (hr + vt);
-          s1 = (b1[o] + hr * ur) + vt * du[o - U];
-          s2 = (b2[o] + hr * vr) + vt * dv[o - U];
+          s1 = (b1 + hr * ur) + vt * du[o - U];
+          s2 = (b2 + hr * vr) + vt * dv[o - U];
         }
         float i11, i12, i22;
         if (s == 0) {
-          const float A11 = a22[o] + dpsis, A22 = a11[o] + dpsis, m12 = a12[o];
+          const float A11 = c0.z + dpsis, A22 = c0.x + dpsis, m12 = c0.y;
           const float det = A11 * A22 - m12 * m12;
           i11 = A11 / det;
           i22 = A22 / det;
           i12 = m12 / (0.0f - det);
-          a11[o] = i11;
-          a22[o] = i22;
-          a12[o] = i12;
+          c0.x = i11;
+          c0.y = i12;
+          c0.z = i22;
         } else {
-          i11 = a11[o];
-          i12 = a12[o];
-          i22 = a22[o];
+          i11 = c0.x;
+          i12 = c0.y;
+          i22 = c0.z;
         }
         float B1 = s1, B2 = s2;
         if (x > 0) {
@@ -929,27 +932,31 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
         du[o] = u0 + omega * (i11 * B1 + i12 * B2 - u0);
         dv[o] = v0 + omega * (i12 * B1 + i22 * B2 - v0);
       } else if (MODE == 1) {
+        const float4 c0 = C[2 * o], c1 = C[2 * o + 1];
         float su = 0.0f, sv = 0.0f, sd = 0.0f;
-        if (y > 0) { su -= vv[o - U] * du[o - U]; sv -= vv[o - U] * dv[o - U]; sd += vv[o - U]; }
-        if (x > 0) { su -= hh[o - L] * du[o - L]; sv -= hh[o - L] * dv[o - L]; sd += hh[o - L]; }
-        if (y < h - 1) { su -= vv[o] * du[o + U]; sv -= vv[o] * dv[o + U]; sd += vv[o]; }
-        if (x < w - 1) { su -= hh[o] * du[o + L]; sv -= hh[o] * dv[o + L]; sd += hh[o]; }
-        const float A11 = a11[o] + sd, A12 = a12[o], A22 = a22[o] + sd;
-        const float B1 = b1[o] - su, B2 = b2[o] - sv;
+        if (y > 0) { const float q = SV_(o - U); su -= q * du[o - U]; sv -= q * dv[o - U]; sd += q; }
+        if (x > 0) { const float q = SH_(o - L); su -= q * du[o - L]; sv -= q * dv[o - L]; sd += q; }
+        if (y < h - 1) { su -= c1.z * du[o + U]; sv -= c1.z * dv[o + U]; sd += c1.z; }
+        if (x < w - 1) { su -= c1.y * du[o + L]; sv -= c1.y * dv[o + L]; sd += c1.y; }
+        const float A11 = c0.x + sd, A12 = c0.y, A22 = c0.z + sd;
+        const float B1 = c0.w - su, B2 = c1.x - sv;
         du[o] = (1.0f - omega) * du[o] + omega / A11 * (B1 - A12 * dv[o]);
         dv[o] = (1.0f - omega) * dv[o] + omega / A22 * (B2 - A12 * du[o]);
       } else {
+        const float4 c0 = C[o];
         float su = 0.0f, sd = 0.0f;
-        if (y > 0) { su -= vv[o - U] * du[o - U]; sd += vv[o - U]; }
-        if (x > 0) { su -= hh[o - L] * du[o - L]; sd += hh[o - L]; }
-        if (y < h - 1) { su -= vv[o] * du[o + U]; sd += vv[o]; }
-        if (x < w - 1) { su -= hh[o] * du[o + L]; sd += hh[o]; }
-        const float A11 = a11[o] + sd, B1 = b1[o] - su;
+        if (y > 0) { const float q = SV_(o - U); su -= q * du[o - U]; sd += q; }
+        if (x > 0) { const float q = SH_(o - L); su -= q * du[o - L]; sd += q; }
+        if (y < h - 1) { su -= c0.w * du[o + U]; sd += c0.w; }
+        if (x < w - 1) { su -= c0.z * du[o + L]; sd += c0.z; }
+        const float A11 = c0.x + sd, B1 = c0.y - su;
         du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
       }
     }
     __syncthreads();
   }
+#undef SH_
+#undef SV_
 }
 
 __device__ __forceinline__ float dpp_from_prev_lane(float v) {  // lane i <- lane i-1 (wave_shr:1)
@@ -960,71 +967,89 @@ __device__ __forceinline__ float dpp_from_next_lane(float v) {  // lane i <- lan
 }
 
 // Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later (register ring).
+// Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later.
 struct SorPix {
   float i11, i12, i22, b1, b2, hl, hr, vv, vt;
 };
 
 // Register-pipelined exact-order SOR: thread = row y (h <= 1024), one workgroup per frame.  At step t the
-// thread runs sweep s on pixel x_s = t - y - 2 s for every s < S.  Left/right/own values come from its
-// own registers (the results of steps t-1 / t-2), top/bottom values from the neighbouring lanes by DPP
-// (and through LDS across wave boundaries), coefficients from the skewed arrays (one coalesced load per
-// array per step), so a wavefront step costs a few hundred cycles instead of a round trip to L2.
+// thread runs sweep s on pixel x_s = t - y - 2 s for every s < S.  Left/right/own values come from its own
+// registers (results of steps t-1 / t-2), top/bottom values from the neighbouring lanes by DPP (through LDS
+// across wave boundaries), coefficients from the skewed array-of-structs (two 16-byte loads per step,
+// issued two steps ahead).  The step loop is unrolled by U = lcm(2, 2(S-1)) so that the load buffers, the
+// per-step history and the sweep ring are all indexed by compile-time phase: no register copies.
 // Same arithmetic, same order as k_tv_sor -> bit-identical results.  MODE 0: OF block SOR, 2: DE point SOR.
 template <int S, int MODE>
-__global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
-  constexpr int D = S > 1 ? 2 * (S - 1) : 1;  // ring depth
-  constexpr int NV = 2 * S + 1;                 // values exchanged per wave boundary
-  __shared__ float xtop[2][16][NV];             // published by each wave's lane 63: cu[*], cv[*], sv
-  __shared__ float xbot[2][16][NV];             // published by each wave's lane 0: cu[*], cv[*]
-  const int f = blockIdx.x, w = a.w, h = a.h;
-  const int y = threadIdx.x, lane = y & 63, wv = y >> 6, nw = (int)(blockDim.x >> 6);
-  const long fo = (long)f * a.sp;
-  float *du = a.du + fo, *dv = a.dv + fo;
-  const float *A11p = a.a11 + fo, *A12p = a.a12 + fo, *A22p = a.a22 + fo, *B1p = a.b1 + fo, *B2p = a.b2 + fo;
-  const float *SH = a.sh + fo, *SV = a.sv + fo;
-  const float omega = a.omega;
-  const bool has_top = y > 0, has_bot = y < h - 1;
-  float cu[S], cv[S], pu[S], pv[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) cu[s] = cv[s] = pu[s] = pv[s] = 0.0f;
-  SorPix ring[D];
-  float own_u = 0.0f, own_v = 0.0f;  // du/dv initial value at (y, x0): the "right" load of the previous step
-  if (y == 0 && w > 0) {  // row 0 starts at step 0: its first own value has no previous-step load
-    own_u = du[0];
-    if (MODE == 0) own_v = dv[0];
-  }
-  float hprev = 0.0f, svprev = 0.0f;
-  const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
-  // prefetched loads for the current step
-  float n11 = 0, n12 = 0, n22 = 0, nb1 = 0, nb2 = 0, nsh = 0, nsv = 0, nru = 0, nrv = 0, nbu = 0, nbv = 0;
-  auto load = [&](int t) {
-    const int x0 = t - y;
-    const long o = (long)t * h + y;  // skewed index of (x0, y)
-    const bool in = y < h && x0 >= 0 && x0 < w;
-    if (in) {
-      n11 = A11p[o]; nb1 = B1p[o]; nsh = SH[o]; nsv = SV[o];
-      if (MODE == 0) { n12 = A12p[o]; n22 = A22p[o]; nb2 = B2p[o]; }
-      if (has_bot) { nbu = du[o + h + 1]; if (MODE == 0) nbv = dv[o + h + 1]; }
-    }
-    if (y < h && x0 + 1 >= 0 && x0 + 1 < w) { nru = du[o + h]; if (MODE == 0) nrv = dv[o + h]; }
+struct SorPipe {
+  static constexpr int D = S > 1 ? 2 * (S - 1) : 1;          // sweep ring depth
+  static constexpr int U = S > 1 ? D : 2;  // unroll = lcm(2, D); D = 2(S-1) is even
+  static constexpr int NV = 2 * S + 1;
+  struct Ld {
+    float4 c0, c1;   // AoS coefficients: OF (a11, a12, a22, b1), (b2, sh, sv, -); DE (a11, b1, sh, sv)
+    float ru, rv, bu, bv;
   };
-  load(0);
-  for (int t = 0; t < T; ++t) {
-    const int par = t & 1;
-    const float c11 = n11, c12 = n12, c22 = n22, cb1 = nb1, cb2 = nb2, csh = nsh, csv = nsv;
-    const float cru = nru, crv = nrv, cbu = nbu, cbv = nbv;
-    if (t + 1 < T) load(t + 1);
+  // state
+  float hu[2][S], hv[2][S];   // sweep results of the last step of each parity
+  float own_u[2], own_v[2];   // "right" initial values loaded at a step of each parity
+  float hsh[2], hsv[2];       // sh / sv loaded at a step of each parity
+  SorPix ring[D];
+  Ld L[2];
+  // constants
+  const float4 *C;
+  float *du, *dv;
+  float (*xtop)[16][NV], (*xbot)[16][NV];
+  int w, h, y, lane, wv, nw;
+  long dump;
+  float omega;
+  bool has_top, has_bot;
+
+  __device__ __forceinline__ void load(int t, Ld &B) {
+    const int x0 = t - y;
+    const bool in = y < h && x0 >= 0 && x0 < w;
+    const long o = in ? (long)t * h + y : dump;
+    if (MODE == 0) {
+      B.c0 = C[2 * o];
+      B.c1 = C[2 * o + 1];
+    } else {
+      B.c0 = C[o];
+    }
+    const long ob = in && has_bot ? o + h + 1 : dump;
+    B.bu = du[ob];
+    if (MODE == 0) B.bv = dv[ob];
+    const long orr = y < h && x0 + 1 >= 0 && x0 + 1 < w ? (long)t * h + h + y : dump;
+    B.ru = du[orr];
+    if (MODE == 0) B.rv = dv[orr];
+  }
+
+  template <int PH>
+  __device__ __forceinline__ void step(const int t) {
+    constexpr int q = PH & 1, qp = q ^ 1;
+    Ld &B = L[q];
+    // consume this step's prefetched values, then reuse the buffer for step t + 2
+    float c11, c12 = 0, c22 = 0, cb1, cb2 = 0, csh, csv;
+    if (MODE == 0) {
+      c11 = B.c0.x; c12 = B.c0.y; c22 = B.c0.z; cb1 = B.c0.w; cb2 = B.c1.x; csh = B.c1.y; csv = B.c1.z;
+    } else {
+      c11 = B.c0.x; cb1 = B.c0.y; csh = B.c0.z; csv = B.c0.w;
+    }
+    const float cru = B.ru, crv = B.rv, cbu = B.bu, cbv = B.bv;
+    load(t + 2, B);
     // neighbour values from the previous step
     float tu[S], tv[S], bu[S], bv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      tu[s] = dpp_from_prev_lane(cu[s]);
-      tv[s] = MODE == 0 ? dpp_from_prev_lane(cv[s]) : 0.0f;
-      bu[s] = dpp_from_next_lane(cu[s]);
-      bv[s] = MODE == 0 ? dpp_from_next_lane(cv[s]) : 0.0f;
+      tu[s] = dpp_from_prev_lane(hu[qp][s]);
+      bu[s] = dpp_from_next_lane(hu[qp][s]);
+      if (MODE == 0) {
+        tv[s] = dpp_from_prev_lane(hv[qp][s]);
+        bv[s] = dpp_from_next_lane(hv[qp][s]);
+      } else {
+        tv[s] = bv[s] = 0.0f;
+      }
     }
-    float svt = dpp_from_prev_lane(svprev);
-    if (t > 0) {
+    float svt = dpp_from_prev_lane(hsv[qp]);
+    if (nw > 1 && t > 0) {
+      const int par = t & 1;
       if (lane == 0 && wv > 0) {
 #pragma unroll
         for (int s = 0; s < S; ++s) { tu[s] = xtop[par ^ 1][wv - 1][s]; tv[s] = xtop[par ^ 1][wv - 1][S + s]; }
@@ -1037,9 +1062,11 @@ __global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
     }
     float nu[S], nvv[S];
     const int x0 = t - y;
-    // ---- sweep 0 on pixel x0 (computes and stores the 2x2 inverse, solver.c:122-128)
+    const float own_u0 = own_u[qp], own_v0 = own_v[qp];
+    // ---- sweep 0 on pixel x0 (computes the 2x2 inverse, solver.c:122-128).  Its data goes to the ring slot
+    // of age 0 only after sweeps 1..S-1 have read theirs: the oldest one (age D) lives in that same slot.
     SorPix d;
-    d.b1 = cb1; d.b2 = cb2; d.hr = csh; d.hl = x0 > 0 ? hprev : 0.0f; d.vv = csv; d.vt = has_top ? svt : 0.0f;
+    d.b1 = cb1; d.b2 = cb2; d.hr = csh; d.hl = x0 > 0 ? hsh[qp] : 0.0f; d.vv = csv; d.vt = has_top ? svt : 0.0f;
     {
       const float ur = x0 < w - 1 ? cru : 0.0f, vr = x0 < w - 1 ? crv : 0.0f;
       if (MODE == 0) {
@@ -1064,31 +1091,31 @@ __global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
         d.i12 = c12 / (0.0f - det);
         float B1 = s1, B2 = s2;
         if (x0 > 0) {
-          B1 = d.hl * cu[0] + s1;
-          B2 = d.hl * cv[0] + s2;
+          B1 = d.hl * hu[qp][0] + s1;
+          B2 = d.hl * hv[qp][0] + s2;
         }
-        nu[0] = own_u + omega * (d.i11 * B1 + d.i12 * B2 - own_u);
-        nvv[0] = own_v + omega * (d.i12 * B1 + d.i22 * B2 - own_v);
+        nu[0] = own_u0 + omega * (d.i11 * B1 + d.i12 * B2 - own_u0);
+        nvv[0] = own_v0 + omega * (d.i12 * B1 + d.i22 * B2 - own_v0);
       } else {
         d.i11 = c11;
         float su = 0.0f, sd = 0.0f;
         if (has_top) { su -= d.vt * tu[0]; sd += d.vt; }
-        if (x0 > 0) { su -= d.hl * cu[0]; sd += d.hl; }
+        if (x0 > 0) { su -= d.hl * hu[qp][0]; sd += d.hl; }
         if (has_bot) { su -= d.vv * cbu; sd += d.vv; }
         if (x0 < w - 1) { su -= d.hr * ur; sd += d.hr; }
-        const float A = c11 + sd, B = d.b1 - su;
-        nu[0] = (1.0f - omega) * own_u + omega * (B / A);
+        const float A = c11 + sd, Bv = d.b1 - su;
+        nu[0] = (1.0f - omega) * own_u0 + omega * (Bv / A);
         nvv[0] = 0.0f;
       }
     }
-    // ---- sweeps 1..S-1 on pixel x0 - 2 s, with the data sweep 0 saw 2 s steps ago
+    // ---- sweeps 1..S-1 on pixel x0 - 2 s with the data sweep 0 saw 2 s steps ago
 #pragma unroll
     for (int s = 1; s < S; ++s) {
-      const SorPix &e = ring[2 * s - 1];
+      const SorPix &e = ring[(PH + 2 * D - 2 * s) % D];
       const int xs = x0 - 2 * s;
-      const float ou = pu[s - 1], ov = pv[s - 1];             // own value after sweep s-1
-      const float ur = xs < w - 1 ? cu[s - 1] : 0.0f;         // right neighbour after sweep s-1
-      const float vr = xs < w - 1 ? cv[s - 1] : 0.0f;
+      const float ou = hu[q][s - 1], ov = hv[q][s - 1];          // own value after sweep s-1 (step t-2)
+      const float ur = xs < w - 1 ? hu[qp][s - 1] : 0.0f;        // right neighbour after sweep s-1
+      const float vr = xs < w - 1 ? hv[qp][s - 1] : 0.0f;
       if (MODE == 0) {
         float s1, s2;
         if (!has_top) {
@@ -1103,67 +1130,109 @@ __global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
         }
         float B1 = s1, B2 = s2;
         if (xs > 0) {
-          B1 = e.hl * cu[s] + s1;
-          B2 = e.hl * cv[s] + s2;
+          B1 = e.hl * hu[qp][s] + s1;
+          B2 = e.hl * hv[qp][s] + s2;
         }
         nu[s] = ou + omega * (e.i11 * B1 + e.i12 * B2 - ou);
         nvv[s] = ov + omega * (e.i12 * B1 + e.i22 * B2 - ov);
       } else {
         float su = 0.0f, sd = 0.0f;
         if (has_top) { su -= e.vt * tu[s]; sd += e.vt; }
-        if (xs > 0) { su -= e.hl * cu[s]; sd += e.hl; }
+        if (xs > 0) { su -= e.hl * hu[qp][s]; sd += e.hl; }
         if (has_bot) { su -= e.vv * bu[s - 1]; sd += e.vv; }
         if (xs < w - 1) { su -= e.hr * ur; sd += e.hr; }
-        const float A = e.i11 + sd, B = e.b1 - su;
-        nu[s] = (1.0f - omega) * ou + omega * (B / A);
+        const float A = e.i11 + sd, Bv = e.b1 - su;
+        nu[s] = (1.0f - omega) * ou + omega * (Bv / A);
         nvv[s] = 0.0f;
       }
     }
-    // ---- the last sweep's result is final
+    if (S > 1) ring[PH % D] = d;
+    // ---- the last sweep's result is final (unconditional store: inactive lanes hit the dump slots)
     {
       const int xl = x0 - 2 * (S - 1);
-      if (y < h && xl >= 0 && xl < w) {
-        const long o = (long)(t - 2 * (S - 1)) * h + y;
-        du[o] = nu[S - 1];
-        if (MODE == 0) dv[o] = nvv[S - 1];
-      }
+      const long o = y < h && xl >= 0 && xl < w ? (long)(t - 2 * (S - 1)) * h + y : dump;
+      du[o] = nu[S - 1];
+      if (MODE == 0) dv[o] = nvv[S - 1];
     }
-    // ---- rotate registers
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      pu[s] = cu[s]; pv[s] = cv[s];
-      cu[s] = nu[s]; cv[s] = nvv[s];
+      hu[q][s] = nu[s];
+      hv[q][s] = nvv[s];
     }
-    if (S > 1) {
-#pragma unroll
-      for (int j = D - 1; j > 0; --j) ring[j] = ring[j - 1];
-      ring[0] = d;
-    }
-    own_u = cru; own_v = crv;
-    hprev = csh; svprev = csv;
+    own_u[q] = cru;
+    own_v[q] = crv;
+    hsh[q] = csh;
+    hsv[q] = csv;
     // ---- publish wave-boundary values, one barrier per step
     if (nw > 1) {
+      const int par = t & 1;
       if (lane == 63) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) { xtop[par][wv][s] = cu[s]; xtop[par][wv][S + s] = cv[s]; }
-        xtop[par][wv][2 * S] = svprev;
+        for (int s = 0; s < S; ++s) { xtop[par][wv][s] = nu[s]; xtop[par][wv][S + s] = nvv[s]; }
+        xtop[par][wv][2 * S] = csv;
       }
       if (lane == 0) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) { xbot[par][wv][s] = cu[s]; xbot[par][wv][S + s] = cv[s]; }
+        for (int s = 0; s < S; ++s) { xbot[par][wv][s] = nu[s]; xbot[par][wv][S + s] = nvv[s]; }
       }
       __syncthreads();
     }
   }
+
+  template <int PH>
+  __device__ __forceinline__ void steps(const int t) {
+    step<PH>(t + PH);
+    if constexpr (PH + 1 < U) steps<PH + 1>(t);
+  }
+};
+
+template <int S, int MODE>
+__global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
+  using P = SorPipe<S, MODE>;
+  __shared__ float xtop[2][16][P::NV];  // published by each wave's lane 63: results of the step, sv
+  __shared__ float xbot[2][16][P::NV];  // published by each wave's lane 0
+  P st;
+  const int f = blockIdx.x;
+  st.w = a.w;
+  st.h = a.h;
+  st.y = threadIdx.x;
+  st.lane = st.y & 63;
+  st.wv = st.y >> 6;
+  st.nw = (int)(blockDim.x >> 6);
+  const long fo = (long)f * a.sp;
+  st.du = a.du + fo;
+  st.dv = a.dv + fo;
+  st.C = reinterpret_cast<const float4 *>(a.coef) + fo * (MODE == 0 ? 2 : 1);
+  st.xtop = xtop;
+  st.xbot = xbot;
+  st.omega = a.omega;
+  st.has_top = st.y > 0;
+  st.has_bot = st.y < a.h - 1;
+  st.dump = (long)(a.w + a.h - 1) * a.h + st.lane;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) st.hu[q][s] = st.hv[q][s] = 0.0f;
+    st.own_u[q] = st.own_v[q] = st.hsh[q] = st.hsv[q] = 0.0f;
+  }
+  if (st.y == 0 && a.w > 0) {  // row 0 starts at step 0: its first own value has no previous-step load
+    st.own_u[1] = st.du[0];
+    if (MODE == 0) st.own_v[1] = st.dv[0];
+  }
+  const int T = (a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1;
+  // steps t >= T are past the right border for every lane and sweep (dump-slot traffic only)
+  const int TU = (T + P::U - 1) / P::U * P::U;
+  st.load(0, st.L[0]);
+  st.load(1, st.L[1]);
+  for (int t = 0; t < TU; t += P::U) st.template steps<0>(t);
 }
 
 __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= a.w) return;
   const long plane = (long)a.w * a.h;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.n * plane) return;
-  const int f = (int)(idx / plane);
-  const long o = idx % plane;
-  const long fk = (long)f * a.sp + skw((int)(o % a.w), (int)(o / a.w), a.h);
+  const long o = (long)y * a.w + x;
+  const long fk = (long)f * a.sp + skw(x, y, a.h);
   float *WX = a.flow + (long)f * a.nop * plane;
   if (a.nop == 2) {
     WX[o] = a.wxs[fk] + a.du[fk];
@@ -1177,17 +1246,114 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
 // ------------------------------------------------------------------------------------------------ output
 
 // flow *= 2^l ; cv::resize(INTER_LINEAR) generic float path (HResizeLinear + VResizeLinear) ; crop.
+// Horizontal source position / weight of output column dx (resizeGeneric_: fx, sx, xmax clamping).
+struct XTap {
+  int sx;
+  float fx;
+  bool lin;
+};
+__device__ __forceinline__ XTap xtap(int dx, double scale, int wl) {
+  XTap r;
+  float fx = (float)((dx + 0.5) * scale - 0.5);
+  int sx = (int)floorf(fx);
+  fx -= (float)sx;
+  if (sx < 0) { fx = 0; sx = 0; }
+  r.lin = true;
+  if (sx + 1 >= wl) {
+    r.lin = false;
+    if (sx >= wl - 1) { fx = 0; sx = wl - 1; }
+  }
+  r.sx = sx;
+  r.fx = fx;
+  return r;
+}
+
+__device__ __forceinline__ float up_px(const float *P, long r0, long r1, const XTap &xt, float fct, float b0, float b1) {
+  float h0, h1;
+  {
+    const float *S = P + r0;
+    const float s0 = S[xt.sx] * fct;
+    h0 = xt.lin ? s0 * (1.f - xt.fx) + (S[xt.sx + 1] * fct) * xt.fx : s0;
+  }
+  {
+    const float *S = P + r1;
+    const float s0 = S[xt.sx] * fct;
+    h1 = xt.lin ? s0 * (1.f - xt.fx) + (S[xt.sx + 1] * fct) * xt.fx : s0;
+  }
+  return h0 * b0 + h1 * b1;
+}
+
+// Upsample for 2^l >= 2, nop = 2: one block = 1024 output columns of one output row, 4 pixels
+// (two 16-byte stores) per thread.  The two source rows it needs are staged in LDS already multiplied by
+// 2^l.  The OpenCV tap positions fx = (dx + .5) / 2^l - .5 are dyadic rationals, so computing them as
+// (2 dx + 1 - 2^l) * 2^-(l+1) in fp32 is exact and equals resizeGeneric_'s double -> float value.
+constexpr int kUpCols = 1024;
+__global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
+  __shared__ float src[2][2][kUpCols / 2 + 8];  // [row][comp][col]; 2^l >= 2 -> <= 513 source columns
+  const int y = blockIdx.y, f = blockIdx.z;
+  const int dx0 = blockIdx.x * kUpCols + a.offx;  // first output column of the block (uncropped coordinates)
+  const int fct_i = 1 << a.log2s;
+  const float fct = (float)fct_i, half_inv = 1.0f / (float)(2 * fct_i);
+  const long plane = (long)a.wl * a.hl;
+  const float *F = a.flow + (long)f * 2 * plane;
+  // rows (resizeGeneric_Invoker: clip(sy, 0, hl), clip(sy + 1, 0, hl); weights not clamped)
+  const int dy = y + a.offy;
+  float fy = (float)(2 * dy + 1 - fct_i) * half_inv;
+  const int sy = (int)floorf(fy);
+  fy -= (float)sy;
+  const int r0 = sy >= 0 ? (sy < a.hl ? sy : a.hl - 1) : 0;
+  const int r1 = sy + 1 >= 0 ? (sy + 1 < a.hl ? sy + 1 : a.hl - 1) : 0;
+  const float b0 = 1.f - fy, b1 = fy;
+  // source column window of this block
+  const int c_lo = max(0, (int)floorf((float)(2 * dx0 + 1 - fct_i) * half_inv));
+  const int ncol = kUpCols / fct_i + 2;
+  for (int k = threadIdx.x; k < 2 * 2 * ncol; k += blockDim.x) {
+    const int col = k % ncol, rc = k / ncol;  // rc = row * 2 + comp
+    const int r = rc >> 1, comp = rc & 1;
+    const int sc = min(c_lo + col, a.wl - 1);
+    src[r][comp][col] = F[comp * plane + (long)(r ? r1 : r0) * a.wl + sc] * fct;
+  }
+  __syncthreads();
+  const int x = blockIdx.x * kUpCols + threadIdx.x * 4;  // output column (cropped)
+  if (x >= a.W0) return;
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int dx = x + i + a.offx;
+    float fx = (float)(2 * dx + 1 - fct_i) * half_inv;
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    bool lin = true;
+    if (sx + 1 >= a.wl) {
+      lin = false;
+      if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
+    }
+    const int c = sx - c_lo;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float s00 = src[0][k][c], s10 = src[1][k][c];
+      const float h0 = lin ? s00 * (1.f - fx) + src[0][k][c + 1] * fx : s00;
+      const float h1 = lin ? s10 * (1.f - fx) + src[1][k][c + 1] * fx : s10;
+      v[i * 2 + k] = h0 * b0 + h1 * b1;
+    }
+  }
+  float *out = a.out + (((long)f * a.H0 + y) * a.W0 + x) * 2;
+  if (x + 4 <= a.W0) {
+    reinterpret_cast<float4 *>(out)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4 *>(out)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    for (int i = 0; i < 2 * (a.W0 - x); ++i) out[i] = v[i];
+  }
+}
+
+// Generic path (any nop, 2^l = 1, unaligned output): one output pixel per thread.
 __global__ __launch_bounds__(256) void k_upsample(UpArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)a.n * a.W0 * a.H0;
-  if (idx >= total) return;
-  const int x = (int)(idx % a.W0);
-  const long r = idx / a.W0;
-  const int y = (int)(r % a.H0);
-  const int f = (int)(r / a.H0);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= a.W0) return;
   const long plane = (long)a.wl * a.hl;
   const float *F = a.flow + (long)f * a.nop * plane;
-  float *out = a.out + idx * a.nop;
+  float *out = a.out + (((long)f * a.H0 + y) * a.W0 + x) * a.nop;
   if (a.log2s == 0) {
     const long o = (long)(y + a.offy) * a.wl + (x + a.offx);
     out[0] = F[o];
@@ -1196,37 +1362,15 @@ __global__ __launch_bounds__(256) void k_upsample(UpArgs a) {
   }
   const float fct = (float)(1 << a.log2s);
   const double scale = 1.0 / (double)(1 << a.log2s);
-  const int dx = x + a.offx, dy = y + a.offy;
-  float fx = (float)((dx + 0.5) * scale - 0.5);
-  int sx = (int)floorf(fx);
-  fx -= (float)sx;
-  if (sx < 0) { fx = 0; sx = 0; }
-  bool lin = true;
-  if (sx + 1 >= a.wl) {
-    lin = false;
-    if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
-  }
+  const int dy = y + a.offy;
   float fy = (float)((dy + 0.5) * scale - 0.5);
   const int sy = (int)floorf(fy);
   fy -= (float)sy;
-  const int r0 = sy >= 0 ? (sy < a.hl ? sy : a.hl - 1) : 0;
-  const int r1 = sy + 1 >= 0 ? (sy + 1 < a.hl ? sy + 1 : a.hl - 1) : 0;
+  const long r0 = (long)(sy >= 0 ? (sy < a.hl ? sy : a.hl - 1) : 0) * a.wl;
+  const long r1 = (long)(sy + 1 >= 0 ? (sy + 1 < a.hl ? sy + 1 : a.hl - 1) : 0) * a.wl;
   const float b0 = 1.f - fy, b1 = fy;
-  for (int k = 0; k < a.nop; ++k) {
-    const float *P = F + k * plane;
-    float h0, h1;
-    {
-      const float *S = P + (long)r0 * a.wl;
-      const float s0 = S[sx] * fct;
-      h0 = lin ? s0 * (1.f - fx) + (S[sx + 1] * fct) * fx : s0;
-    }
-    {
-      const float *S = P + (long)r1 * a.wl;
-      const float s0 = S[sx] * fct;
-      h1 = lin ? s0 * (1.f - fx) + (S[sx + 1] * fct) * fx : s0;
-    }
-    out[k] = h0 * b0 + h1 * b1;
-  }
+  const XTap xt = xtap(x + a.offx, scale, a.wl);
+  for (int k = 0; k < a.nop; ++k) out[k] = up_px(F + k * plane, r0, r1, xt, fct, b0, b1);
 }
 
 }  // namespace
@@ -1234,16 +1378,13 @@ __global__ __launch_bounds__(256) void k_upsample(UpArgs a) {
 // ------------------------------------------------------------------------------------------------ launchers
 
 void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s) {
-  const long total = 2L * a.n * a.h * a.w;
-  k_pyr_base<<<ceil_div(total, 256), 256, 0, s>>>(a);
+  k_pyr_base<<<dim3(ceil_div(a.w, 256), a.h, 2 * a.n), 256, 0, s>>>(a);
 }
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {
-  const long total = (long)a.n2 * a.h * a.w * a.noc;
-  k_pyr_down<<<ceil_div(total, 256), 256, 0, s>>>(a);
+  k_pyr_down<<<dim3(ceil_div((long)a.w * a.noc, 256), a.h, a.n2), 256, 0, s>>>(a);
 }
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s) {
-  const long total = (long)a.n2 * (a.h + 2 * a.pad) * (a.w + 2 * a.pad);
-  k_pyr_pad_grad<<<ceil_div(total, 256), 256, 0, s>>>(a);
+  k_pyr_pad_grad<<<dim3(ceil_div(a.w + 2 * a.pad, 256), a.h + 2 * a.pad, a.n2), 256, 0, s>>>(a);
 }
 void launch_patch(const PatchArgs &a, hipStream_t s) {
   const long waves = (long)a.n * a.g.npatch;
@@ -1255,29 +1396,28 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
     k_patch<1><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
 }
 void launch_aggregate(const AggArgs &a, hipStream_t s) {
-  const long total = (long)a.n * a.g.w * a.g.h;
-  k_aggregate<<<ceil_div(total, 256), 256, 0, s>>>(a);
+  k_aggregate<<<dim3(ceil_div(a.g.w, 256), a.g.h, a.n), 256, 0, s>>>(a);
 }
 void launch_tv_prep(const TvArgs &a, hipStream_t s) {
-  k_tv_prep<<<ceil_div((long)a.n * a.w * a.h, 256), 256, 0, s>>>(a);
+  k_tv_prep<<<dim3(ceil_div(a.w, 256), a.h, a.n), 256, 0, s>>>(a);
 }
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
-  k_tv_deriv1<<<ceil_div((long)a.n * a.noc * a.sp, 256), 256, 0, s>>>(a);
+  k_tv_deriv1<<<dim3(ceil_div(a.sp, 256), a.n * a.noc), 256, 0, s>>>(a);
 }
 void launch_tv_deriv2(const TvArgs &a, hipStream_t s) {
-  k_tv_deriv2<<<ceil_div((long)a.n * a.noc * a.sp, 256), 256, 0, s>>>(a);
+  k_tv_deriv2<<<dim3(ceil_div(a.sp, 256), a.n * a.noc), 256, 0, s>>>(a);
 }
 void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
   if (a.nop == 2)
-    k_tv_smooth<2><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
+    k_tv_smooth<2><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
   else
-    k_tv_smooth<1><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
+    k_tv_smooth<1><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
 }
 void launch_tv_system(const TvArgs &a, hipStream_t s) {
   if (a.nop == 2)
-    k_tv_system<2><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
+    k_tv_system<2><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
   else
-    k_tv_system<1><<<ceil_div((long)a.n * a.sp, 256), 256, 0, s>>>(a);
+    k_tv_system<1><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
 }
 template <int S>
 static void sor_pipe(const TvArgs &a, hipStream_t s) {
@@ -1306,11 +1446,13 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
     k_tv_sor<0><<<a.n, 256, 0, s>>>(a);
 }
 void launch_tv_final(const TvArgs &a, hipStream_t s) {
-  k_tv_final<<<ceil_div((long)a.n * a.w * a.h, 256), 256, 0, s>>>(a);
+  k_tv_final<<<dim3(ceil_div(a.w, 256), a.h, a.n), 256, 0, s>>>(a);
 }
 void launch_upsample(const UpArgs &a, hipStream_t s) {
-  const long total = (long)a.n * a.W0 * a.H0;
-  k_upsample<<<ceil_div(total, 256), 256, 0, s>>>(a);
+  if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
+    k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), a.H0, a.n), 256, 0, s>>>(a);
+  else
+    k_upsample<<<dim3(ceil_div(a.W0, 256), a.H0, a.n), 256, 0, s>>>(a);
 }
 
 }  // namespace ofdis

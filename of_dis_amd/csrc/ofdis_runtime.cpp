@@ -57,6 +57,17 @@ struct ofdis_context {
   std::vector<hipEvent_t> pool;
   std::map<int, std::pair<double, long>> acc;
   int opt_sor_generic = 0;
+  // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
+  // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
+  int opt_streams = 4, opt_chunk = 32;
+  struct Lane {
+    hipStream_t s = nullptr;
+    char *ws = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+  };
+  std::vector<Lane> lanes;
+  hipEvent_t entry = nullptr;
   std::mutex mu;
 };
 
@@ -184,9 +195,9 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
   off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
   P.off_tv = off;
   size_t max_sp = 0;  // skewed TV plane (w + h - 1) * h
-  for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, (size_t)(g.w + g.h - 1) * g.h);
+  for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, ((size_t)(g.w + g.h - 1) * g.h + 64 + 3) / 4 * 4);
   P.tv_plane = max_sp;
-  if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_sp * (13 + 9 * (size_t)P.noc));
+  if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_sp * (14 + 9 * (size_t)P.noc));
   P.total = off;
   return P;
 }
@@ -223,12 +234,11 @@ struct StageTimes {
 
 // The coarse-to-fine loop (oflow.cpp:182-330) over device pyramids already in the workspace.
 // init: optional coarse initial flow (device, interleaved, (w_f/2)*(h_f/2)*nop per frame).
-int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream_t s, const float *init,
+int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, hipStream_t s, const float *init,
                std::vector<StageTimes> *times) {
   const int nop = P.nop, noc = P.noc, n = P.n;
   const int novals = noc * p->p_samp_s * p->p_samp_s;
   const int steps = steps_of(p);
-  char *ws = c->ws;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   if (times)
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
@@ -300,7 +310,7 @@ int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream
 
     const int n_inner = p->tv_innerit * (sl + 1);  // refine_variational.cpp:36
     if (p->usetvref && n_inner > 0) {
-      const long sp = (long)(g.w + g.h - 1) * g.h;
+      const long sp = ((long)(g.w + g.h - 1) * g.h + 64 + 3) / 4 * 4;  // + SOR dump slots; 16-B multiple
       const size_t pl = (size_t)n * sp;
       float *t0 = (float *)(ws + P.off_tv);
       TvArgs tv{};
@@ -310,18 +320,12 @@ int run_levels(ofdis_context *c, const Plan &P, const ofdis_params *p, hipStream
       tv.du = t0;
       tv.dv = t0 + pl;
       tv.mask = t0 + 2 * pl;
-      tv.a11 = t0 + 3 * pl;
-      tv.a12 = t0 + 4 * pl;
-      tv.a22 = t0 + 5 * pl;
-      tv.b1 = t0 + 6 * pl;
-      tv.b2 = t0 + 7 * pl;
-      tv.sh = t0 + 8 * pl;
-      tv.sv = t0 + 9 * pl;
-      tv.s = t0 + 10 * pl;
-      tv.wxs = t0 + 11 * pl;
-      tv.wys = t0 + 12 * pl;
+      tv.coef = t0 + 3 * pl;  // 8 planes' worth (float4 x 2 per pixel), 16-byte aligned: sp % 4 == 0 ensured
+      tv.s = t0 + 11 * pl;
+      tv.wxs = t0 + 12 * pl;
+      tv.wys = t0 + 13 * pl;
       tv.sp = sp;
-      float *cp = t0 + 13 * pl;
+      float *cp = t0 + 14 * pl;
       const size_t cpl = pl * noc;
       tv.t = cp;
       tv.dt = cp + cpl;
@@ -410,8 +414,7 @@ int check_device(int device) {
 }
 
 // Pyramid of the batch (run_dense.cpp:299-312,327-328,131-179) into the workspace.
-int run_pyramid(ofdis_context *c, const Plan &P, const uint8_t *a, const uint8_t *b, hipStream_t s) {
-  char *ws = c->ws;
+int run_pyramid(ofdis_context *c, char *ws, const Plan &P, const uint8_t *a, const uint8_t *b, hipStream_t s) {
   const int n2 = 2 * P.n;
   {
     PyrBaseArgs pb{};
@@ -495,9 +498,64 @@ void ofdis_context_destroy(ofdis_context *c) {
   drain_timing(c);
   for (auto e : c->pool) hipEventDestroy(e);
   if (c->ws) hipFree(c->ws);
+  for (auto &L : c->lanes) {
+    if (L.s) hipStreamSynchronize(L.s);
+    if (L.ws) hipFree(L.ws);
+    if (L.done) hipEventDestroy(L.done);
+    if (L.s) hipStreamDestroy(L.s);
+  }
+  if (c->entry) hipEventDestroy(c->entry);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
+
+namespace {
+
+// One chunk of frames through the whole pipeline on stream s with workspace ws.
+int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
+              const uint8_t *img_b, float *flow_out, hipStream_t s) {
+  int rc = run_pyramid(c, ws, P, img_a, img_b, s);
+  if (rc) return rc;
+  rc = run_levels(c, ws, P, p, s, nullptr, nullptr);
+  if (rc) return rc;
+  UpArgs up{};
+  up.flow = (const float *)(ws + P.off_flow[0]);
+  up.out = flow_out;
+  up.n = P.n;
+  up.nop = P.nop;
+  up.wl = P.lv[0].w;
+  up.hl = P.lv[0].h;
+  up.log2s = p->sc_l;
+  up.W0 = P.W0;
+  up.H0 = P.H0;
+  up.offx = P.padl;
+  up.offy = P.padt;
+  timed(c, 10, s, [&] { launch_upsample(up, s); });
+  return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+}
+
+int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
+  if ((int)c->lanes.size() < k) c->lanes.resize(k);
+  if (!c->entry) HIP_OK(hipEventCreateWithFlags(&c->entry, hipEventDisableTiming));
+  for (int i = 0; i < k; ++i) {
+    auto &L = c->lanes[i];
+    if (!L.s) HIP_OK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+    if (!L.done) HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+    if (L.cap < bytes) {
+      if (L.ws) {
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipFree(L.ws));
+        L.ws = nullptr;
+        L.cap = 0;
+      }
+      HIP_OK(hipMalloc(&L.ws, bytes));
+      L.cap = bytes;
+    }
+  }
+  return OFDIS_OK;
+}
+
+}  // namespace
 
 int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width, int height,
                        const ofdis_params *p, float *flow_out, void *stream) {
@@ -510,26 +568,33 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
   Plan P = batch_plan(p, n, width, height);
   rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
   if (rc) return rc;
-  rc = ensure_ws(c, P.total);
+  const bool capturing = !c->cap_dis.empty() || !c->cap_tv.empty();
+  const int chunk = c->opt_chunk > 0 ? c->opt_chunk : n;
+  const int nchunks = (n + chunk - 1) / chunk;
+  if (c->opt_streams <= 1 || nchunks <= 1 || capturing) {
+    rc = ensure_ws(c, P.total);
+    if (rc) return rc;
+    return run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, s);
+  }
+  const int k = std::min(c->opt_streams, nchunks);
+  Plan PC = batch_plan(p, chunk, width, height);
+  rc = ensure_lanes(c, k, PC.total);
   if (rc) return rc;
-  rc = run_pyramid(c, P, img_a, img_b, s);
-  if (rc) return rc;
-  rc = run_levels(c, P, p, s, nullptr, nullptr);
-  if (rc) return rc;
-  UpArgs up{};
-  up.flow = (const float *)(c->ws + P.off_flow[0]);
-  up.out = flow_out;
-  up.n = n;
-  up.nop = P.nop;
-  up.wl = P.lv[0].w;
-  up.hl = P.lv[0].h;
-  up.log2s = p->sc_l;
-  up.W0 = width;
-  up.H0 = height;
-  up.offx = P.padl;
-  up.offy = P.padt;
-  timed(c, 10, s, [&] { launch_upsample(up, s); });
-  return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+  HIP_OK(hipEventRecord(c->entry, s));
+  for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
+  const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * P.nop;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int f0 = ch * chunk, m = std::min(chunk, n - f0);
+    auto &L = c->lanes[ch % k];
+    Plan PM = m == chunk ? PC : batch_plan(p, m, width, height);
+    rc = run_chunk(c, L.ws, PM, p, img_a + f0 * in_frame, img_b + f0 * in_frame, flow_out + f0 * out_frame, L.s);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < k; ++i) {
+    HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
+    HIP_OK(hipStreamWaitEvent(s, c->lanes[i].done, 0));
+  }
+  return OFDIS_OK;
 }
 
 int ofdis_run_batch_u8_host(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
@@ -584,7 +649,7 @@ int ofdis_pyramid_u8_host(ofdis_context *c, const uint8_t *img, int width, int h
   uint8_t *d = nullptr;
   HIP_OK(hipMalloc(&d, in));
   HIP_OK(hipMemcpy(d, img, in, hipMemcpyHostToDevice));
-  rc = run_pyramid(c, P, d, d, c->stream);
+  rc = run_pyramid(c, c->ws, P, d, d, c->stream);
   if (rc == OFDIS_OK) {
     HIP_OK(hipStreamSynchronize(c->stream));
     for (int s = p->sc_l; s <= p->sc_f; ++s) {
@@ -616,6 +681,14 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   std::lock_guard<std::mutex> lock(c->mu);
   if (std::strcmp(key, "sor_generic") == 0) {
     c->opt_sor_generic = value != 0;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "streams") == 0 && value >= 1 && value <= 16) {
+    c->opt_streams = value;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "chunk") == 0 && value >= 0) {
+    c->opt_chunk = value;
     return OFDIS_OK;
   }
   return OFDIS_ERR_INVALID_ARGUMENT;
@@ -713,7 +786,7 @@ int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx,
     if (nb) HIP_OK(hipMemcpyAsync(dinit, initflow, nb, hipMemcpyHostToDevice, s));
   }
   std::vector<StageTimes> times;
-  rc = run_levels(c, P, p, s, dinit, p->verbosity > 1 ? &times : nullptr);
+  rc = run_levels(c, c->ws, P, p, s, dinit, p->verbosity > 1 ? &times : nullptr);
   if (rc == OFDIS_OK) {
     const LevelGeom &g = P.lv[0];
     const size_t plane = (size_t)g.w * g.h;

@@ -144,12 +144,19 @@ def test_batch_equals_singles(od, ctx):
     a = torch.from_numpy(np.stack([x[0] for x in pairs])).cuda()
     b = torch.from_numpy(np.stack([x[1] for x in pairs])).cuda()
     p = od.oppoint(2, w, 1, 1)
-    out = ctx.run(a, b, p)
-    torch.cuda.synchronize()
-    out = out.cpu().numpy()
+    outs = []
+    for streams, chunk in ((1, 0), (3, 2), (4, 1)):  # whole batch on one stream; chunks over streams
+        ctx.set_option("streams", streams)
+        ctx.set_option("chunk", chunk)
+        o = ctx.run(a, b, p)
+        torch.cuda.synchronize()
+        outs.append(o.cpu().numpy())
+    ctx.set_option("streams", 4)
+    ctx.set_option("chunk", 32)
     for f in range(n):
         single = ctx.run_host(pairs[f][0], pairs[f][1], p)
-        assert_bitexact(out[f], single, f"batch frame {f}")
+        for k, out in enumerate(outs):
+            assert_bitexact(out[f], single, f"batch frame {f} (config {k})")
 
 
 def test_full_1080p_bitexact(oracle, od, ctx):
