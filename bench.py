@@ -28,14 +28,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="frame pairs per GPU per step")
+    ap.add_argument("--batch", type=int, default=256, help="frame pairs per GPU per step")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--oppoint", type=int, default=2)
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--streams", type=int, default=4, help="HIP streams the batch's chunks round-robin over")
-    ap.add_argument("--chunk", type=int, default=32, help="frames per chunk (0 = whole batch in one chunk)")
+    ap.add_argument("--streams", type=int, default=1, help="HIP streams the batch's chunks round-robin over")
+    ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = whole batch in one chunk)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     return ap.parse_args()
 

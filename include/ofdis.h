@@ -131,7 +131,7 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
 /* Tuning / A-B switches:
  *   "sor_generic" (0/1): force the generic global-memory SOR wavefront instead of the register-pipelined
  *                        one (both are exact-order; used by the parity tests);
- *   "streams" (1-16, default 4) and "chunk" (frames, default 32, 0 = whole batch): a batch is cut into
+ *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into
  *                        chunks that run round-robin on that many HIP streams with separate workspaces,
  *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels.
  * Results never depend on these settings (frames are independent). */

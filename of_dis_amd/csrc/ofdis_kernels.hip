@@ -134,13 +134,21 @@ __global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
 // ------------------------------------------------------------------------------------------------ DIS patches
 
 constexpr int kPatchWaves = 4;
-constexpr int kJmax = 7;  // values per lane: novals <= 448 (p = 12, RGB: 432)
 
-// Eigen's SSE redux order (two 4-lane packet accumulators over packet pairs, res0 + res1, odd trailing
-// packet, predux (l0 + l2) + (l1 + l3)).  The R arrays were stored to lds[r * rs + v]; lane (r = lane/8,
-// slot = lane%8) walks its slot's chain v = slot, slot + 8, ... in order, then the 8 lanes of a group
-// combine exactly like the reference's packet tree.  Result r is returned to every lane.
-template <int R>
+template <int N>
+__device__ __forceinline__ float row_shl(float v) {  // lane i <- lane i+N within its 16-lane row (else 0)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x100 + N, 0xF, 0xF, false));
+}
+
+// Eigen's SSE redux order for a dynamic vector (redux_impl, LinearVectorizedTraversal): two 4-lane packet
+// accumulators over packet pairs, res0 + res1, odd trailing packet, predux (l0 + l2) + (l1 + l3).  Value v
+// of a slot chain (slot = v % 8) is accumulated in v order.  R arrays are reduced at once: lanes
+// (r = lane / 8, s = lane % 8) walk chain s of array r, then the 8 lanes of a group combine by DPP exactly
+// like the packet tree.  Returns the R totals as wave-uniform values.
+//
+// JM == 1 (n <= 64, one value per lane): the arrays were stored TRANSPOSED (v -> (v % 8) * 8 + v / 8), so a
+// chain is 8 contiguous floats: two ds_read_b128 per lane.  JM > 1: stored as lds[r * rs + v].
+template <int R, int JM>
 __device__ __forceinline__ void eigen_reduce(const float *lds, int rs, int n, int lane, float (&out)[R]) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -150,68 +158,91 @@ __device__ __forceinline__ void eigen_reduce(const float *lds, int rs, int n, in
   const bool odd = ((n >> 2) & 1) != 0;
   float acc = 0.0f, first = 0.0f, tail = 0.0f;
   if (r < R) {
-    const float *x = lds + r * rs;
-    first = x[s];
-    acc = first;
-    for (int c = 1; c < pairs; ++c) acc = acc + x[s + 8 * c];
-    tail = x[pairs * 8 + s];
-  }
-  const float other = __shfl_down(acc, 4, 64);
-  float rl = pairs > 0 ? acc + other : first;
-  if (odd && pairs > 0) rl = rl + tail;
-  const float t = rl + __shfl_down(rl, 2, 64);
-  const float tot = t + __shfl_down(t, 1, 64);
+    if (JM == 1) {
+      const float4 A = *reinterpret_cast<const float4 *>(lds + r * 64 + s * 8);
+      const float4 B = *reinterpret_cast<const float4 *>(lds + r * 64 + s * 8 + 4);
+      const float e[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+      first = e[0];
+      acc = first;
 #pragma unroll
-  for (int k = 0; k < R; ++k) out[k] = __shfl(tot, k * 8, 64);
+      for (int c = 1; c < 8; ++c)
+        if (c < pairs) acc = acc + e[c];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c == pairs) tail = e[c];
+    } else {
+      const float *x = lds + r * rs;
+      first = x[s];
+      acc = first;
+      for (int c = 1; c < pairs; ++c) acc = acc + x[s + 8 * c];
+      tail = x[pairs * 8 + s];
+    }
+  }
+  float rl = pairs > 0 ? acc + row_shl<4>(acc) : first;
+  if (odd && pairs > 0) rl = rl + tail;
+  const float t = rl + row_shl<2>(rl);
+  const float tot = t + row_shl<1>(t);
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    out[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), k * 8));
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void lds_store(float *lds, int n, int lane, const float (&v)[kJmax], int J) {
-#pragma unroll
-  for (int j = 0; j < kJmax; ++j)
-    if (j < J) {
-      const int e = lane + 64 * j;
-      if (e < n) lds[e] = v[j];
-    }
-}
-
-// Eigen LLT<2x2>::solve: unblocked llt_inplace (stops at a non-positive pivot, leaving raw entries)
-// followed by the unrolled lower and upper triangular solves.
-__device__ __forceinline__ void llt2_solve(float H00, float H01, float H11, float b0, float b1, float &x0,
-                                           float &x1) {
-  float L00 = H00, L10 = H01, L11 = H11;
-  if (!(H00 <= 0.0f)) {
-    L00 = sqrtf(H00);
-    L10 = H01 / L00;
-    const float t = H11 - L10 * L10;
-    if (!(t <= 0.0f)) L11 = sqrtf(t);
+template <int JM>
+__device__ __forceinline__ void lds_store(float *lds, int n, int lane, const float (&v)[JM]) {
+  if (JM == 1) {
+    lds[(lane & 7) * 8 + (lane >> 3)] = lane < n ? v[0] : 0.0f;
+    return;
   }
-  const float y0 = b0 / L00;
-  const float y1 = (b1 - L10 * y0) / L11;
-  x1 = y1 / L11;
-  x0 = (y0 - L10 * x1) / L00;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int e = lane + 64 * j;
+    if (e < n) lds[e] = v[j];
+  }
 }
 
-__device__ __forceinline__ float llt1_solve(float H, float b) {
-  float L = H;
-  if (!(H <= 0.0f)) L = sqrtf(H);
+// Eigen LLT<2x2> (unblocked llt_inplace: a non-positive pivot stops the factorisation and leaves the raw
+// entries) -- the factor depends only on the Hessian, so it is computed once per patch.
+struct Llt2 {
+  float L00, L10, L11;
+};
+__device__ __forceinline__ Llt2 llt2_factor(float H00, float H01, float H11) {
+  Llt2 f{H00, H01, H11};
+  if (!(H00 <= 0.0f)) {
+    f.L00 = sqrtf(H00);
+    f.L10 = H01 / f.L00;
+    const float t = H11 - f.L10 * f.L10;
+    if (!(t <= 0.0f)) f.L11 = sqrtf(t);
+  }
+  return f;
+}
+// LLT::solve: unrolled lower then upper triangular substitution.
+__device__ __forceinline__ void llt2_solve(const Llt2 &f, float b0, float b1, float &x0, float &x1) {
+  const float y0 = b0 / f.L00;
+  const float y1 = (b1 - f.L10 * y0) / f.L11;
+  x1 = y1 / f.L11;
+  x0 = (y0 - f.L10 * x1) / f.L00;
+}
+__device__ __forceinline__ float llt1_factor(float H) { return !(H <= 0.0f) ? sqrtf(H) : H; }
+__device__ __forceinline__ float llt1_solve(float L, float b) {
   const float y = b / L;
   return y / L;
 }
 
+template <int JM>
 struct PatchCtx {
   const float *B;
-  int W, noc, p, pad, novals, J, lane, rs, costfct, patnorm, nop;
+  int W, noc, p, pad, novals, lane, rs, costfct, patnorm;
   float *lds;
-  int offs[kJmax];
+  int offs[JM];
 };
 
 // getPatchStaticBil (patch.cpp:345-413) + mean normalisation + LossComputeErrorImage (patch.cpp:221-273).
-// Leaves pdiff/pweight per lane and returns Eigen sums of |pweight|, dx*pdiff, dy*pdiff.
-template <int NOP>
-__device__ __forceinline__ void patch_eval(const PatchCtx &c, float mx, float my, const float (&tmp)[kJmax],
-                                           const float (&gx)[kJmax], const float (&gy)[kJmax],
-                                           float (&pd)[kJmax], float (&pw)[kJmax], float (&red)[NOP + 1]) {
+// Leaves pdiff / pweight per lane and returns the Eigen sums of |pweight|, dx * pdiff (, dy * pdiff).
+template <int NOP, int JM>
+__device__ __forceinline__ void patch_eval(const PatchCtx<JM> &c, float mx, float my, const float (&tmp)[JM],
+                                           const float (&gx)[JM], const float (&gy)[JM], float (&pd)[JM],
+                                           float (&pw)[JM], float (&red)[NOP + 1]) {
   const int pos0 = (int)ceilf(mx + 0.00001f) + c.pad;
   const int pos1 = (int)ceilf(my + 0.00001f) + c.pad;
   const int pos2 = (int)floorf(mx), pos3 = (int)floorf(my);
@@ -220,86 +251,87 @@ __device__ __forceinline__ void patch_eval(const PatchCtx &c, float mx, float my
   const long base = ((long)(pos1 - c.p / 2) * c.W + (pos0 - c.p / 2)) * c.noc;
   const long rowstep = (long)c.W * c.noc;
 #pragma unroll
-  for (int j = 0; j < kJmax; ++j)
-    if (j < c.J) {
-      if (c.lane + 64 * j < c.novals) {
-        const float *q = c.B + base + c.offs[j];
-        const float A = q[0], Bv = q[-c.noc], C = q[-rowstep], D = q[-rowstep - c.noc];
-        pd[j] = w0 * A + w1 * Bv + w2 * C + w3 * D;
-      } else {
-        pd[j] = 0.0f;
-      }
+  for (int j = 0; j < JM; ++j) {
+    if (c.lane + 64 * j < c.novals) {
+      const float *q = c.B + base + c.offs[j];
+      const float A = q[0], Bv = q[-c.noc], C = q[-rowstep], D = q[-rowstep - c.noc];
+      pd[j] = w0 * A + w1 * Bv + w2 * C + w3 * D;
+    } else {
+      pd[j] = 0.0f;
     }
+  }
   if (c.patnorm > 0) {
-    lds_store(c.lds, c.novals, c.lane, pd, c.J);
+    lds_store<JM>(c.lds, c.novals, c.lane, pd);
     float s[1];
-    eigen_reduce<1>(c.lds, c.rs, c.novals, c.lane, s);
+    eigen_reduce<1, JM>(c.lds, c.rs, c.novals, c.lane, s);
     const float mean = s[0] / (float)c.novals;
 #pragma unroll
-    for (int j = 0; j < kJmax; ++j)
-      if (j < c.J) pd[j] = pd[j] - mean;
+    for (int j = 0; j < JM; ++j) pd[j] = pd[j] - mean;
   }
-  float ab[kJmax], px[kJmax], py[kJmax];
+  float ab[JM], px[JM], py[JM];
 #pragma unroll
-  for (int j = 0; j < kJmax; ++j)
-    if (j < c.J) {
-      const float d = pd[j] - tmp[j];
-      float w;
-      if (c.costfct == 0) {
-        pd[j] = d;
-        w = fabsf(d);
-      } else if (c.costfct == 1) {
-        w = sqrtf(fabsf(d));
-        pd[j] = copysignf(w, d);
-      } else {
-        w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
-        pd[j] = copysignf(w, d);
-      }
-      pw[j] = w;
-      ab[j] = fabsf(w);
-      px[j] = gx[j] * pd[j];
-      py[j] = gy[j] * pd[j];
+  for (int j = 0; j < JM; ++j) {
+    const float d = pd[j] - tmp[j];
+    float w;
+    if (c.costfct == 0) {
+      pd[j] = d;
+      w = fabsf(d);
+    } else if (c.costfct == 1) {
+      w = sqrtf(fabsf(d));
+      pd[j] = copysignf(w, d);
+    } else {
+      w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+      pd[j] = copysignf(w, d);
     }
-  lds_store(c.lds, c.novals, c.lane, ab, c.J);
-  lds_store(c.lds + c.rs, c.novals, c.lane, px, c.J);
-  if (NOP == 2) lds_store(c.lds + 2 * c.rs, c.novals, c.lane, py, c.J);
-  eigen_reduce<NOP + 1>(c.lds, c.rs, c.novals, c.lane, red);
+    pw[j] = w;
+    ab[j] = fabsf(w);
+    px[j] = gx[j] * pd[j];
+    py[j] = gy[j] * pd[j];
+  }
+  const int stride = JM == 1 ? 64 : c.rs;
+  lds_store<JM>(c.lds, c.novals, c.lane, ab);
+  lds_store<JM>(c.lds + stride, c.novals, c.lane, px);
+  if (NOP == 2) lds_store<JM>(c.lds + 2 * stride, c.novals, c.lane, py);
+  eigen_reduce<NOP + 1, JM>(c.lds, c.rs, c.novals, c.lane, red);
 }
 
-template <int NOP>
+// One wave64 per patch: InitializePatch + SetTargetImage + OptimizeIter(p_init, true)
+// (patch.cpp:55-210, patchgrid.cpp:98-141,195-211).  JM = values per lane (ceil(p*p*noc / 64)).
+template <int NOP, int JM>
 __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_all[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const LevelGeom &g = a.g;
   const long gp = (long)blockIdx.x * kPatchWaves + wid;
-  if (gp >= (long)a.n * g.npatch) return;  // whole wave exits; kernel uses no block barrier
+  if (gp >= (long)a.n * g.npatch) return;  // whole wave exits; the kernel has no block barrier
   const int f = (int)(gp / g.npatch), ip = (int)(gp % g.npatch);
   const int pxi = ip / g.noph, pyi = ip % g.noph;
   const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
   const long fs = (long)g.W * g.H * a.noc;
 
-  PatchCtx c;
+  PatchCtx<JM> c;
   c.B = a.img_b + f * fs;
   c.W = g.W; c.noc = a.noc; c.p = a.p; c.pad = g.pad; c.novals = a.novals;
-  c.J = (a.novals + 63) >> 6; c.lane = lane; c.costfct = a.costfct; c.patnorm = a.patnorm; c.nop = NOP;
+  c.lane = lane; c.costfct = a.costfct; c.patnorm = a.patnorm;
   c.rs = ((a.novals + 31) / 32) * 32 + 8;
-  c.lds = lds_all + wid * 3 * c.rs;
+  c.lds = lds_all + wid * 3 * (JM == 1 ? 64 : c.rs);
 #pragma unroll
-  for (int j = 0; j < kJmax; ++j) {
+  for (int j = 0; j < JM; ++j) {
     const int e = lane + 64 * j;
     const int ch = e % a.noc, q = e / a.noc;
     c.offs[j] = ((q / a.p) * g.W + (q % a.p)) * a.noc + ch;
   }
+  const int stride = JM == 1 ? 64 : c.rs;
 
   // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
-  float tmp[kJmax], gx[kJmax], gy[kJmax], pd[kJmax], pw[kJmax];
+  float tmp[JM], gx[JM], gy[JM], pd[JM], pw[JM];
   {
     const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
     const long base = ((long)(py - a.p / 2) * g.W + (px - a.p / 2)) * a.noc;
     const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
 #pragma unroll
-    for (int j = 0; j < kJmax; ++j) {
-      const bool ok = j < c.J && lane + 64 * j < a.novals;
+    for (int j = 0; j < JM; ++j) {
+      const bool ok = lane + 64 * j < a.novals;
       tmp[j] = ok ? A[c.offs[j]] : 0.0f;
       gx[j] = ok ? DX[c.offs[j]] : 0.0f;
       gy[j] = ok ? DY[c.offs[j]] : 0.0f;
@@ -308,42 +340,43 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
     }
   }
   if (a.patnorm > 0) {
-    lds_store(c.lds, a.novals, lane, tmp, c.J);
+    lds_store<JM>(c.lds, a.novals, lane, tmp);
     float s[1];
-    eigen_reduce<1>(c.lds, c.rs, a.novals, lane, s);
+    eigen_reduce<1, JM>(c.lds, c.rs, a.novals, lane, s);
     const float mean = s[0] / (float)a.novals;
 #pragma unroll
-    for (int j = 0; j < kJmax; ++j)
-      if (j < c.J) tmp[j] = tmp[j] - mean;
+    for (int j = 0; j < JM; ++j) tmp[j] = tmp[j] - mean;
   }
   // ---- ComputeHessian (patch.cpp:69-86)
   float H00, H01 = 0.0f, H11 = 0.0f;
   {
-    float q0[kJmax], q1[kJmax], q2[kJmax];
+    float q0[JM], q1[JM], q2[JM];
 #pragma unroll
-    for (int j = 0; j < kJmax; ++j) {
+    for (int j = 0; j < JM; ++j) {
       q0[j] = gx[j] * gx[j];
       q1[j] = gx[j] * gy[j];
       q2[j] = gy[j] * gy[j];
     }
-    lds_store(c.lds, a.novals, lane, q0, c.J);
+    lds_store<JM>(c.lds, a.novals, lane, q0);
     if (NOP == 2) {
-      lds_store(c.lds + c.rs, a.novals, lane, q1, c.J);
-      lds_store(c.lds + 2 * c.rs, a.novals, lane, q2, c.J);
-      float h[3];
-      eigen_reduce<3>(c.lds, c.rs, a.novals, lane, h);
-      H00 = h[0]; H01 = h[1]; H11 = h[2];
+      lds_store<JM>(c.lds + stride, a.novals, lane, q1);
+      lds_store<JM>(c.lds + 2 * stride, a.novals, lane, q2);
+      float hh[3];
+      eigen_reduce<3, JM>(c.lds, c.rs, a.novals, lane, hh);
+      H00 = hh[0]; H01 = hh[1]; H11 = hh[2];
       if (H00 * H11 - H01 * H01 == 0.0f) {
         H00 = (float)((double)H00 + 1e-10);
         H11 = (float)((double)H11 + 1e-10);
       }
     } else {
-      float h[1];
-      eigen_reduce<1>(c.lds, c.rs, a.novals, lane, h);
-      H00 = h[0];
+      float hh[1];
+      eigen_reduce<1, JM>(c.lds, c.rs, a.novals, lane, hh);
+      H00 = hh[0];
       if (H00 == 0.0f) H00 = (float)((double)H00 + 1e-10);
     }
   }
+  const Llt2 fac = llt2_factor(H00, H01, H11);
+  const float fac1 = llt1_factor(H00);
   // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
   float pin0 = 0.0f, pin1 = 0.0f;
   if (a.prev) {
@@ -363,7 +396,7 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
   auto err = [&]() {  // OptimizeComputeErrImg (patch.cpp:275-295)
     float red[NOP + 1];
-    patch_eval<NOP>(c, pt0, pt1, tmp, gx, gy, pd, pw, red);
+    patch_eval<NOP, JM>(c, pt0, pt1, tmp, gx, gy, pd, pw, red);
     sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
     if (cnt == 1) sq_init = sq;
     mares_old = mares;
@@ -378,7 +411,7 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   if (oob(pt0, pt1)) {
     converged = true;
 #pragma unroll
-    for (int j = 0; j < kJmax; ++j) pw[j] = 0.0f;  // never written upstream; defined as 0
+    for (int j = 0; j < JM; ++j) pw[j] = 0.0f;  // never written upstream; defined as 0
   } else {
     mares = 1e5f;
     err();
@@ -387,11 +420,11 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   while (!converged) {
     ++cnt;
     if (NOP == 2) {
-      llt2_solve(H00, H01, H11, b0, b1, d0, d1);
+      llt2_solve(fac, b0, b1, d0, d1);
       p0 = p0 - d0;
       p1 = p1 - d1;
     } else {
-      d0 = llt1_solve(H00, b0);
+      d0 = llt1_solve(fac1, b0);
       p0 = p0 - d0;
       p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
     }
@@ -411,8 +444,8 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   if (lane < NOP) a.p_iter[gp * NOP + lane] = lane == 0 ? p0 : p1;
   float *pwo = a.pweight + gp * a.novals;
 #pragma unroll
-  for (int j = 0; j < kJmax; ++j)
-    if (j < c.J && lane + 64 * j < a.novals) pwo[lane + 64 * j] = pw[j];
+  for (int j = 0; j < JM; ++j)
+    if (lane + 64 * j < a.novals) pwo[lane + 64 * j] = pw[j];
 }
 
 // ------------------------------------------------------------------------------------------------ aggregation
@@ -1386,14 +1419,24 @@ void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s) {
   k_pyr_pad_grad<<<dim3(ceil_div(a.w + 2 * a.pad, 256), a.h + 2 * a.pad, a.n2), 256, 0, s>>>(a);
 }
-void launch_patch(const PatchArgs &a, hipStream_t s) {
+template <int JM>
+static void patch_jm(const PatchArgs &a, hipStream_t s) {
   const long waves = (long)a.n * a.g.npatch;
-  const int rs = ((a.novals + 31) / 32) * 32 + 8;
+  const int rs = JM == 1 ? 64 : ((a.novals + 31) / 32) * 32 + 8;
   const size_t lds = sizeof(float) * 3 * rs * kPatchWaves;
   if (a.nop == 2)
-    k_patch<2><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
+    k_patch<2, JM><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
   else
-    k_patch<1><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
+    k_patch<1, JM><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
+}
+void launch_patch(const PatchArgs &a, hipStream_t s) {
+  const int J = (a.novals + 63) / 64;
+  if (J <= 1)
+    patch_jm<1>(a, s);
+  else if (J <= 3)
+    patch_jm<3>(a, s);
+  else
+    patch_jm<7>(a, s);
 }
 void launch_aggregate(const AggArgs &a, hipStream_t s) {
   k_aggregate<<<dim3(ceil_div(a.g.w, 256), a.g.h, a.n), 256, 0, s>>>(a);

@@ -59,7 +59,7 @@ struct ofdis_context {
   int opt_sor_generic = 0;
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
-  int opt_streams = 4, opt_chunk = 32;
+  int opt_streams = 1, opt_chunk = 0;
   struct Lane {
     hipStream_t s = nullptr;
     char *ws = nullptr;

@@ -151,8 +151,8 @@ def test_batch_equals_singles(od, ctx):
         o = ctx.run(a, b, p)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
-    ctx.set_option("streams", 4)
-    ctx.set_option("chunk", 32)
+    ctx.set_option("streams", 1)
+    ctx.set_option("chunk", 0)
     for f in range(n):
         single = ctx.run_host(pairs[f][0], pairs[f][1], p)
         for k, out in enumerate(outs):
