@@ -727,6 +727,8 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
   const int novals = noc * p->p_samp_s * p->p_samp_s;
   double b = 0.0;
   const std::string k(kernel);
+  if (("," + std::string(ofdis_kernel_names()) + ",").find("," + k + ",") == std::string::npos)
+    return OFDIS_ERR_INVALID_ARGUMENT;
   for (const LevelGeom &g : P.lv) {
     const double px = (double)g.w * g.h;
     const int n_inner = p->usetvref ? p->tv_innerit * (g.level + 1) : 0;
@@ -736,6 +738,12 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
                                                                    (double)(p->max_iter + 1) + 4.0 * (nop + novals));
     if (k == "aggregate") b += px * 4.0 * nop + (double)g.npatch * 4.0 * (nop + novals);
     if (k == "pyr_pad_grad") b += 2.0 * (px * 4.0 * noc + 3.0 * g.W * g.H * 4.0 * noc);
+    if (k == "pyr_down" && g.level > p->sc_l) b += 2.0 * noc * 4.0 * (4.0 * px + px);
+    if (p->usetvref) {
+      if (k == "tv_prep") b += px * 4.0 * (4 * noc + 1 + 3 * nop);
+      if (k == "tv_deriv") b += px * 4.0 * noc * (2 + 4 + 2 + 3);
+      if (k == "tv_final") b += px * 4.0 * 3 * nop;
+    }
   }
   if (k == "pyr_base") b = 2.0 * width * height * noc + 2.0 * 4.0 * P.lv[0].w * P.lv[0].h * noc;
   if (k == "upsample") b = (double)width * height * nop * 4.0;

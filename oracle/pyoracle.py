@@ -247,3 +247,53 @@ def ref_conv(L, order: int):
     else:
         half = (C.c_float * 2)(0.0, -0.5)
     return L.convolution_new(order, half, 0)
+
+
+def ref_refine_level(noc, mode, im1, im2, flow, level, p):
+    """refine_variational.cpp:152-342 glue, driven through the reference FDF functions."""
+    h, w = im1.shape[-2:]
+    R = ref(noc)
+    n_inner = p["tv_innerit"] * (level + 1)
+    f32 = np.float32
+    qa = f32(0.25) * f32(p["tv_alpha"])
+    hgo3 = f32(p["tv_gamma"]) * f32(0.5) / f32(3.0)
+    hdo3 = f32(p["tv_delta"]) * f32(0.5) / f32(3.0)
+    img = lambda c=1: RefImage(w, h, c)
+    rim1, rim2 = img(noc), img(noc)
+    rim1.set(im1); rim2.set(im2)
+    wx, wy = img(), img()
+    wx.set(flow[..., 0])
+    if mode == 1:
+        wy.set(flow[..., 1])
+    else:
+        wy.buf[:] = 0  # image_erase(wy_dummy)
+    du, dv, mask, sh, sv, uu, vv = (img() for _ in range(7))
+    a11, a12, a22, b1, b2 = (img() for _ in range(5))
+    wim2 = img(noc)
+    I = [img(noc) for _ in range(8)]
+    R.image_warp(wim2.ptr, mask.ptr, rim2.ptr, wx.ptr, wy.ptr)
+    R.get_derivatives(rim1.ptr, wim2.ptr, ref_conv(R, 2), *[x.ptr for x in I])
+    du.buf[:] = 0; dv.buf[:] = 0
+    uu.buf[:] = wx.buf; vv.buf[:] = wy.buf
+    dflow = ref_conv(R, 1)
+    for _ in range(n_inner):
+        R.compute_smoothness(sh.ptr, sv.ptr, uu.ptr, vv.ptr if mode == 1 else wy.ptr, dflow, C.c_float(qa))
+        if mode == 1:
+            R.compute_data(a11.ptr, a12.ptr, a22.ptr, b1.ptr, b2.ptr, mask.ptr, wx.ptr, wy.ptr, du.ptr, dv.ptr,
+                           uu.ptr, vv.ptr, *[x.ptr for x in I], C.c_float(hdo3), C.c_float(0), C.c_float(hgo3))
+            R.sub_laplacian(b1.ptr, wx.ptr, sh.ptr, sv.ptr)
+            R.sub_laplacian(b2.ptr, wy.ptr, sh.ptr, sv.ptr)
+            R.sor_coupled(du.ptr, dv.ptr, a11.ptr, a12.ptr, a22.ptr, b1.ptr, b2.ptr, sh.ptr, sv.ptr,
+                          p["tv_solverit"], C.c_float(p["tv_sor"]))
+            uu.buf[:] = wx.buf + du.buf
+            vv.buf[:] = wy.buf + dv.buf
+        else:
+            R.compute_data_DE(a11.ptr, b1.ptr, mask.ptr, wx.ptr, du.ptr, uu.ptr, *[x.ptr for x in I],
+                              C.c_float(hdo3), C.c_float(0), C.c_float(hgo3))
+            R.sub_laplacian(b1.ptr, wx.ptr, sh.ptr, sv.ptr)
+            R.sor_coupled_slow_but_readable_DE(du.ptr, a11.ptr, b1.ptr, sh.ptr, sv.ptr, p["tv_solverit"],
+                                               C.c_float(p["tv_sor"]))
+            s = wx.buf + du.buf
+            uu.buf[:] = np.where(s < 0, s, np.float32(0))  # _mm_min_ps(s, 0)
+    out = np.stack([uu.get()] + ([vv.get()] if mode == 1 else []), axis=-1)
+    return out

@@ -1,0 +1,70 @@
+"""Frame sharding on CPU: world_size-2 gloo process groups stand in for RCCL ranks.
+
+The data path has no collective; these tests cover the control collectives bench.py uses (barrier,
+max of elapsed time, sum of counters) and that the shards tile the batch exactly once.
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from of_dis_amd.distributed import shard_range
+
+
+@pytest.mark.parametrize("n,world", [(256, 8), (10, 3), (3, 4), (0, 2), (1, 1)])
+def test_shards_tile_the_batch(n, world):
+    seen = []
+    sizes = []
+    for r in range(world):
+        a, b = shard_range(n, r, world)
+        assert 0 <= a <= b <= n
+        seen.extend(range(a, b))
+        sizes.append(b - a)
+    assert seen == list(range(n))
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_range_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        shard_range(8, 2, 2)
+    with pytest.raises(ValueError):
+        shard_range(8, 0, 0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from of_dis_amd.distributed import max_over_ranks, shard_range, sum_over_ranks
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b = shard_range(64, rank, world)
+        dist.barrier()
+        t = max_over_ranks(0.5 + rank)           # per-rank "elapsed"
+        tot = sum_over_ranks([b - a, 1.0])        # frames processed, ranks
+        q.put((rank, a, b, t, tot))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_control_collectives():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 32), (32, 64)]
+    assert all(r[3] == 1.5 for r in res)          # max over ranks
+    assert all(r[4] == [64.0, 2.0] for r in res)  # whole-job frames
