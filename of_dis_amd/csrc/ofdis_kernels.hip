@@ -885,6 +885,25 @@ __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
     if (x <= w - 2) B2 = B2 + shv * (WY[idx + h] - c0);
     if (y >= 1) B2 = B2 - (S[idx - h - 1] + sc) * (c0 - WY[idx - h - 1]);
     if (y <= h - 2) B2 = B2 + svv * (WY[idx + h + 1] - c0);
+    // sor_coupled's first sweep replaces a11/a12/a22 by the inverse of [[a11+d, a12], [a12, a22+d]] with
+    // d = the sum of the four diffusivities (solver.c:122-128, border forms :131-190).  It depends on the
+    // system only, so it is computed here, fully parallel, with the same expressions; every SOR sweep then
+    // reads the inverse.  (w < 2 or h < 2 run the point-SOR fallback on the raw matrix, solver.c:34-78.)
+    if (w >= 2 && h >= 2) {
+      const float hl = x > 0 ? S[idx - h] + sc : 0.0f;            // h[x-1]
+      float dpsis;
+      if (y == 0) {
+        dpsis = hl + (shv + svv);
+      } else {
+        const float vt = S[idx - h - 1] + sc;                       // v[y-1]
+        dpsis = y < h - 1 ? (hl + shv) + (vt + svv) : hl + (shv + vt);
+      }
+      const float M11 = A22 + dpsis, M22 = A11 + dpsis;
+      const float det = M11 * M22 - A12 * A12;
+      A11 = M11 / det;
+      A22 = M22 / det;
+      A12 = A12 / (0.0f - det);
+    }
     float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
     C[0] = make_float4(A11, A12, A22, B1);
     C[1] = make_float4(B2, shv, svv, 0.0f);
@@ -920,42 +939,25 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
       if (x < 0 || x >= w) continue;
       const long o = skw(x, y, h);
       if (MODE == 0) {
-        float4 &c0 = C[2 * o];
+        const float4 c0 = C[2 * o];
         const float4 c1 = C[2 * o + 1];
         const float b1 = c0.w, b2 = c1.x, hr = c1.y, vo = c1.z;
         const float hl = x > 0 ? SH_(o - L) : 0.0f;
         const float ur = x < w - 1 ? du[o + L] : 0.0f, vr = x < w - 1 ? dv[o + L] : 0.0f;
-        float s1, s2, dpsis;
+        float s1, s2;
         if (y == 0) {
-          dpsis = hl + (hr + vo);
           s1 = (b1 + hr * ur) + vo * du[o + U];
           s2 = (b2 + hr * vr) + vo * dv[o + U];
         } else if (y < h - 1) {
           const float vt = SV_(o - U);
-          dpsis = (hl + hr) + (vt + vo);
           s1 = ((hr * ur) + vt * du[o - U]) + (b1 + vo * du[o + U]);
           s2 = ((hr * vr) + vt * dv[o - U]) + (b2 + vo * dv[o + U]);
         } else {
           const float vt = SV_(o - U);
-          dpsis = hl + (hr + vt);
           s1 = (b1 + hr * ur) + vt * du[o - U];
           s2 = (b2 + hr * vr) + vt * dv[o - U];
         }
-        float i11, i12, i22;
-        if (s == 0) {
-          const float A11 = c0.z + dpsis, A22 = c0.x + dpsis, m12 = c0.y;
-          const float det = A11 * A22 - m12 * m12;
-          i11 = A11 / det;
-          i22 = A22 / det;
-          i12 = m12 / (0.0f - det);
-          c0.x = i11;
-          c0.y = i12;
-          c0.z = i22;
-        } else {
-          i11 = c0.x;
-          i12 = c0.y;
-          i22 = c0.z;
-        }
+        const float i11 = c0.x, i12 = c0.y, i22 = c0.z;  // inverse precomputed by k_tv_system
         float B1 = s1, B2 = s2;
         if (x > 0) {
           B1 = hl * du[o - L] + s1;
@@ -992,31 +994,47 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
 #undef SV_
 }
 
-__device__ __forceinline__ float dpp_from_prev_lane(float v) {  // lane i <- lane i-1 (wave_shr:1)
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+// Lane i <- lane i-1 (wave_shr:1) / lane i+1 (wave_shl:1).  bound_ctrl: the lane without a source reads 0
+// (its value is never used: border selects / cross-wave LDS values replace it), so no "old" register.
+__device__ __forceinline__ float dpp_from_prev_lane(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
 }
-__device__ __forceinline__ float dpp_from_next_lane(float v) {  // lane i <- lane i+1 (wave_shl:1)
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
+__device__ __forceinline__ float dpp_from_next_lane(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
 }
 
 // Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later (register ring).
-// Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later.
 struct SorPix {
   float i11, i12, i22, b1, b2, hl, hr, vv, vt;
 };
 
+// The three border variants of solver.c's block-SOR right-hand side as ONE branch-free expression tree.
+// The reference evaluates (first row / last row / interior, solver.c:131-190 and :241-300)
+//   top:      s = (b + X) + Z
+//   bottom:   s = (b + X) + Y
+//   interior: s = (X + Y) + (b + Z)
+// with X = hr*u_right, Y = vt*u_top, Z = vv*u_bottom.  Selecting operands (and -0.0f, the exact additive
+// identity of IEEE round-to-nearest: -0 + x == x bit-for-bit, x = +-0 included) reproduces every variant
+// exactly, so a wave never splits into per-lane branches.
+__device__ __forceinline__ float sor_rhs(bool border, bool notop, float b, float X, float Y, float Z) {
+  const float l = X + (border ? b : Y);
+  const float r = (border ? -0.0f : b) + (border ? (notop ? Z : Y) : Z);
+  return l + r;
+}
 // Register-pipelined exact-order SOR: thread = row y (h <= 1024), one workgroup per frame.  At step t the
 // thread runs sweep s on pixel x_s = t - y - 2 s for every s < S.  Left/right/own values come from its own
 // registers (results of steps t-1 / t-2), top/bottom values from the neighbouring lanes by DPP (through LDS
 // across wave boundaries), coefficients from the skewed array-of-structs (two 16-byte loads per step,
 // issued two steps ahead).  The step loop is unrolled by U = lcm(2, 2(S-1)) so that the load buffers, the
-// per-step history and the sweep ring are all indexed by compile-time phase: no register copies.
+// per-step history and the sweep ring are all indexed by compile-time phase: no register copies.  Every
+// per-lane condition (borders, inactive lanes) is a select, never a branch: one instruction stream per wave.
 // Same arithmetic, same order as k_tv_sor -> bit-identical results.  MODE 0: OF block SOR, 2: DE point SOR.
 template <int S, int MODE>
 struct SorPipe {
   static constexpr int D = S > 1 ? 2 * (S - 1) : 1;          // sweep ring depth
   static constexpr int U = S > 1 ? D : 2;  // unroll = lcm(2, D); D = 2(S-1) is even
   static constexpr int NV = 2 * S + 1;
+  static constexpr int NV4 = (NV + 3) / 4;                   // float4s per published record
   struct Ld {
     float4 c0, c1;   // AoS coefficients: OF (a11, a12, a22, b1), (b2, sh, sv, -); DE (a11, b1, sh, sv)
     float ru, rv, bu, bv;
@@ -1030,26 +1048,27 @@ struct SorPipe {
   // constants
   const float4 *C;
   float *du, *dv;
-  float (*xtop)[16][NV], (*xbot)[16][NV];
+  float4 (*xtop)[16][NV4], (*xbot)[16][NV4];
   int w, h, y, lane, wv, nw;
-  long dump;
+  unsigned dump;
   float omega;
-  bool has_top, has_bot;
+  bool has_top, has_bot, border, notop, get_top, get_bot;
 
   __device__ __forceinline__ void load(int t, Ld &B) {
     const int x0 = t - y;
     const bool in = y < h && x0 >= 0 && x0 < w;
-    const long o = in ? (long)t * h + y : dump;
+    const unsigned here = (unsigned)(t * h + y);
+    const unsigned o = in ? here : dump;
     if (MODE == 0) {
       B.c0 = C[2 * o];
       B.c1 = C[2 * o + 1];
     } else {
       B.c0 = C[o];
     }
-    const long ob = in && has_bot ? o + h + 1 : dump;
+    const unsigned ob = in && has_bot ? here + h + 1 : dump;
     B.bu = du[ob];
     if (MODE == 0) B.bv = dv[ob];
-    const long orr = y < h && x0 + 1 >= 0 && x0 + 1 < w ? (long)t * h + h + y : dump;
+    const unsigned orr = y < h && x0 + 1 >= 0 && x0 + 1 < w ? here + h : dump;
     B.ru = du[orr];
     if (MODE == 0) B.rv = dv[orr];
   }
@@ -1081,61 +1100,51 @@ struct SorPipe {
       }
     }
     float svt = dpp_from_prev_lane(hsv[qp]);
-    if (nw > 1 && t > 0) {
-      const int par = t & 1;
-      if (lane == 0 && wv > 0) {
+    if (nw > 1 && t > 0) {  // wave-boundary lanes take the neighbouring wave's values (uniform LDS reads)
+      const int par = (t & 1) ^ 1;
+      float xt[4 * NV4], xb[4 * NV4];
 #pragma unroll
-        for (int s = 0; s < S; ++s) { tu[s] = xtop[par ^ 1][wv - 1][s]; tv[s] = xtop[par ^ 1][wv - 1][S + s]; }
-        svt = xtop[par ^ 1][wv - 1][2 * S];
+      for (int k = 0; k < NV4; ++k) {
+        const float4 a4 = xtop[par][wv > 0 ? wv - 1 : 0][k], b4 = xbot[par][wv < nw - 1 ? wv + 1 : wv][k];
+        xt[4 * k] = a4.x; xt[4 * k + 1] = a4.y; xt[4 * k + 2] = a4.z; xt[4 * k + 3] = a4.w;
+        xb[4 * k] = b4.x; xb[4 * k + 1] = b4.y; xb[4 * k + 2] = b4.z; xb[4 * k + 3] = b4.w;
       }
-      if (lane == 63 && wv < nw - 1) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) { bu[s] = xbot[par ^ 1][wv + 1][s]; bv[s] = xbot[par ^ 1][wv + 1][S + s]; }
+      for (int s = 0; s < S; ++s) {
+        tu[s] = get_top ? xt[s] : tu[s];
+        bu[s] = get_bot ? xb[s] : bu[s];
+        if (MODE == 0) {
+          tv[s] = get_top ? xt[S + s] : tv[s];
+          bv[s] = get_bot ? xb[S + s] : bv[s];
+        }
       }
+      svt = get_top ? xt[2 * S] : svt;
     }
     float nu[S], nvv[S];
     const int x0 = t - y;
     const float own_u0 = own_u[qp], own_v0 = own_v[qp];
-    // ---- sweep 0 on pixel x0 (computes the 2x2 inverse, solver.c:122-128).  Its data goes to the ring slot
-    // of age 0 only after sweeps 1..S-1 have read theirs: the oldest one (age D) lives in that same slot.
+    // ---- sweep 0 on pixel x0.  Its data goes to the ring slot of age 0 only after sweeps 1..S-1 have read theirs: the oldest one (age D) lives in that same slot.
     SorPix d;
     d.b1 = cb1; d.b2 = cb2; d.hr = csh; d.hl = x0 > 0 ? hsh[qp] : 0.0f; d.vv = csv; d.vt = has_top ? svt : 0.0f;
     {
       const float ur = x0 < w - 1 ? cru : 0.0f, vr = x0 < w - 1 ? crv : 0.0f;
       if (MODE == 0) {
-        float s1, s2, dpsis;
-        if (!has_top) {
-          dpsis = d.hl + (d.hr + d.vv);
-          s1 = (d.b1 + d.hr * ur) + d.vv * cbu;
-          s2 = (d.b2 + d.hr * vr) + d.vv * cbv;
-        } else if (has_bot) {
-          dpsis = (d.hl + d.hr) + (d.vt + d.vv);
-          s1 = ((d.hr * ur) + d.vt * tu[0]) + (d.b1 + d.vv * cbu);
-          s2 = ((d.hr * vr) + d.vt * tv[0]) + (d.b2 + d.vv * cbv);
-        } else {
-          dpsis = d.hl + (d.hr + d.vt);
-          s1 = (d.b1 + d.hr * ur) + d.vt * tu[0];
-          s2 = (d.b2 + d.hr * vr) + d.vt * tv[0];
-        }
-        const float A11 = c22 + dpsis, A22 = c11 + dpsis;
-        const float det = A11 * A22 - c12 * c12;
-        d.i11 = A11 / det;
-        d.i22 = A22 / det;
-        d.i12 = c12 / (0.0f - det);
-        float B1 = s1, B2 = s2;
-        if (x0 > 0) {
-          B1 = d.hl * hu[qp][0] + s1;
-          B2 = d.hl * hv[qp][0] + s2;
-        }
+        const float s1 = sor_rhs(border, notop, d.b1, d.hr * ur, d.vt * tu[0], d.vv * cbu);
+        const float s2 = sor_rhs(border, notop, d.b2, d.hr * vr, d.vt * tv[0], d.vv * cbv);
+        d.i11 = c11;  // inverse precomputed by k_tv_system (solver.c:122-128)
+        d.i12 = c12;
+        d.i22 = c22;
+        const float B1 = x0 > 0 ? d.hl * hu[qp][0] + s1 : s1;
+        const float B2 = x0 > 0 ? d.hl * hv[qp][0] + s2 : s2;
         nu[0] = own_u0 + omega * (d.i11 * B1 + d.i12 * B2 - own_u0);
         nvv[0] = own_v0 + omega * (d.i12 * B1 + d.i22 * B2 - own_v0);
       } else {
         d.i11 = c11;
         float su = 0.0f, sd = 0.0f;
-        if (has_top) { su -= d.vt * tu[0]; sd += d.vt; }
-        if (x0 > 0) { su -= d.hl * hu[qp][0]; sd += d.hl; }
-        if (has_bot) { su -= d.vv * cbu; sd += d.vv; }
-        if (x0 < w - 1) { su -= d.hr * ur; sd += d.hr; }
+        su = has_top ? su - d.vt * tu[0] : su;      sd = has_top ? sd + d.vt : sd;
+        su = x0 > 0 ? su - d.hl * hu[qp][0] : su;   sd = x0 > 0 ? sd + d.hl : sd;
+        su = has_bot ? su - d.vv * cbu : su;        sd = has_bot ? sd + d.vv : sd;
+        su = x0 < w - 1 ? su - d.hr * ur : su;      sd = x0 < w - 1 ? sd + d.hr : sd;
         const float A = c11 + sd, Bv = d.b1 - su;
         nu[0] = (1.0f - omega) * own_u0 + omega * (Bv / A);
         nvv[0] = 0.0f;
@@ -1150,30 +1159,18 @@ struct SorPipe {
       const float ur = xs < w - 1 ? hu[qp][s - 1] : 0.0f;        // right neighbour after sweep s-1
       const float vr = xs < w - 1 ? hv[qp][s - 1] : 0.0f;
       if (MODE == 0) {
-        float s1, s2;
-        if (!has_top) {
-          s1 = (e.b1 + e.hr * ur) + e.vv * bu[s - 1];
-          s2 = (e.b2 + e.hr * vr) + e.vv * bv[s - 1];
-        } else if (has_bot) {
-          s1 = ((e.hr * ur) + e.vt * tu[s]) + (e.b1 + e.vv * bu[s - 1]);
-          s2 = ((e.hr * vr) + e.vt * tv[s]) + (e.b2 + e.vv * bv[s - 1]);
-        } else {
-          s1 = (e.b1 + e.hr * ur) + e.vt * tu[s];
-          s2 = (e.b2 + e.hr * vr) + e.vt * tv[s];
-        }
-        float B1 = s1, B2 = s2;
-        if (xs > 0) {
-          B1 = e.hl * hu[qp][s] + s1;
-          B2 = e.hl * hv[qp][s] + s2;
-        }
+        const float s1 = sor_rhs(border, notop, e.b1, e.hr * ur, e.vt * tu[s], e.vv * bu[s - 1]);
+        const float s2 = sor_rhs(border, notop, e.b2, e.hr * vr, e.vt * tv[s], e.vv * bv[s - 1]);
+        const float B1 = xs > 0 ? e.hl * hu[qp][s] + s1 : s1;
+        const float B2 = xs > 0 ? e.hl * hv[qp][s] + s2 : s2;
         nu[s] = ou + omega * (e.i11 * B1 + e.i12 * B2 - ou);
         nvv[s] = ov + omega * (e.i12 * B1 + e.i22 * B2 - ov);
       } else {
         float su = 0.0f, sd = 0.0f;
-        if (has_top) { su -= e.vt * tu[s]; sd += e.vt; }
-        if (xs > 0) { su -= e.hl * hu[qp][s]; sd += e.hl; }
-        if (has_bot) { su -= e.vv * bu[s - 1]; sd += e.vv; }
-        if (xs < w - 1) { su -= e.hr * ur; sd += e.hr; }
+        su = has_top ? su - e.vt * tu[s] : su;          sd = has_top ? sd + e.vt : sd;
+        su = xs > 0 ? su - e.hl * hu[qp][s] : su;       sd = xs > 0 ? sd + e.hl : sd;
+        su = has_bot ? su - e.vv * bu[s - 1] : su;      sd = has_bot ? sd + e.vv : sd;
+        su = xs < w - 1 ? su - e.hr * ur : su;          sd = xs < w - 1 ? sd + e.hr : sd;
         const float A = e.i11 + sd, Bv = e.b1 - su;
         nu[s] = (1.0f - omega) * ou + omega * (Bv / A);
         nvv[s] = 0.0f;
@@ -1183,7 +1180,7 @@ struct SorPipe {
     // ---- the last sweep's result is final (unconditional store: inactive lanes hit the dump slots)
     {
       const int xl = x0 - 2 * (S - 1);
-      const long o = y < h && xl >= 0 && xl < w ? (long)(t - 2 * (S - 1)) * h + y : dump;
+      const unsigned o = y < h && xl >= 0 && xl < w ? (unsigned)((t - 2 * (S - 1)) * h + y) : dump;
       du[o] = nu[S - 1];
       if (MODE == 0) dv[o] = nvv[S - 1];
     }
@@ -1199,14 +1196,19 @@ struct SorPipe {
     // ---- publish wave-boundary values, one barrier per step
     if (nw > 1) {
       const int par = t & 1;
+      float rec[4 * NV4];
+#pragma unroll
+      for (int s = 0; s < S; ++s) { rec[s] = nu[s]; rec[S + s] = nvv[s]; }
+      rec[2 * S] = csv;
+#pragma unroll
+      for (int k = 2 * S + 1; k < 4 * NV4; ++k) rec[k] = 0.0f;
       if (lane == 63) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) { xtop[par][wv][s] = nu[s]; xtop[par][wv][S + s] = nvv[s]; }
-        xtop[par][wv][2 * S] = csv;
+        for (int k = 0; k < NV4; ++k) xtop[par][wv][k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
       }
       if (lane == 0) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) { xbot[par][wv][s] = nu[s]; xbot[par][wv][S + s] = nvv[s]; }
+        for (int k = 0; k < NV4; ++k) xbot[par][wv][k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
       }
       __syncthreads();
     }
@@ -1219,11 +1221,13 @@ struct SorPipe {
   }
 };
 
-template <int S, int MODE>
-__global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
+// MAXT = launch bound: 256 (one wave per SIMD, up to 512 registers) for h <= 256, 512 for h <= 512 (the
+// S <= 4 rings fit without spilling in both), 1024 for taller levels.
+template <int S, int MODE, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tv_sor_pipe(TvArgs a) {
   using P = SorPipe<S, MODE>;
-  __shared__ float xtop[2][16][P::NV];  // published by each wave's lane 63: results of the step, sv
-  __shared__ float xbot[2][16][P::NV];  // published by each wave's lane 0
+  __shared__ float4 xtop[2][16][P::NV4];  // published by each wave's lane 63: results of the step, sv
+  __shared__ float4 xbot[2][16][P::NV4];  // published by each wave's lane 0
   P st;
   const int f = blockIdx.x;
   st.w = a.w;
@@ -1241,7 +1245,11 @@ __global__ __launch_bounds__(1024) void k_tv_sor_pipe(TvArgs a) {
   st.omega = a.omega;
   st.has_top = st.y > 0;
   st.has_bot = st.y < a.h - 1;
-  st.dump = (long)(a.w + a.h - 1) * a.h + st.lane;
+  st.notop = !st.has_top;
+  st.border = !st.has_top || !st.has_bot;
+  st.get_top = st.lane == 0 && st.wv > 0;
+  st.get_bot = st.lane == 63 && st.wv < st.nw - 1;
+  st.dump = (unsigned)((a.w + a.h - 1) * a.h + st.lane);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -1465,10 +1473,22 @@ void launch_tv_system(const TvArgs &a, hipStream_t s) {
 template <int S>
 static void sor_pipe(const TvArgs &a, hipStream_t s) {
   const int threads = ((a.h + 63) / 64) * 64;
-  if (a.nop == 2)
-    k_tv_sor_pipe<S, 0><<<a.n, threads, 0, s>>>(a);
-  else
-    k_tv_sor_pipe<S, 2><<<a.n, threads, 0, s>>>(a);
+  if (threads <= 256) {
+    if (a.nop == 2)
+      k_tv_sor_pipe<S, 0, 256><<<a.n, threads, 0, s>>>(a);
+    else
+      k_tv_sor_pipe<S, 2, 256><<<a.n, threads, 0, s>>>(a);
+  } else if (threads <= 512) {
+    if (a.nop == 2)
+      k_tv_sor_pipe<S, 0, 512><<<a.n, threads, 0, s>>>(a);
+    else
+      k_tv_sor_pipe<S, 2, 512><<<a.n, threads, 0, s>>>(a);
+  } else {
+    if (a.nop == 2)
+      k_tv_sor_pipe<S, 0, 1024><<<a.n, threads, 0, s>>>(a);
+    else
+      k_tv_sor_pipe<S, 2, 1024><<<a.n, threads, 0, s>>>(a);
+  }
 }
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
