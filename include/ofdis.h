@@ -131,6 +131,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
 /* Tuning / A-B switches:
  *   "sor_generic" (0/1): force the generic global-memory SOR wavefront instead of the register-pipelined
  *                        one (both are exact-order; used by the parity tests);
+ *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline instead of the default
+ *                        sweep-per-wave SOR (same bits; A/B and parity tests);
  *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into
  *                        chunks that run round-robin on that many HIP streams with separate workspaces,
  *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels.

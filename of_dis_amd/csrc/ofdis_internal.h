@@ -85,6 +85,7 @@ struct TvArgs {
   int solverit;
   int camlr;
   int sor_generic;             // force the generic global-memory SOR wavefront (A/B testing)
+  int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
 };
 
 struct UpArgs {

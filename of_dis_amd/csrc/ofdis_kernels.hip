@@ -1268,6 +1268,164 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_pipe(TvArgs a) {
   for (int t = 0; t < TU; t += P::U) st.template steps<0>(t);
 }
 
+// Sweep-per-wave exact-order SOR.  Same wavefront as SorPipe (pixel (x, y) of sweep s at step
+// t = x + y + 2 s), but the S sweeps run on S different waves of the workgroup: wave (g, s) owns rows
+// 64 g .. 64 g + 63 of sweep s.  Per step every wave computes ONE pixel per lane and publishes
+// (u, v, sv) in an LDS ring of depth 3 (steps t, t-1, t-2); the wave of sweep s+1 reads its own / right /
+// bottom "old" values there, every wave reads its top neighbour there (lane y-1 of any row group), and its
+// left neighbour is its own result of step t-1.  Sweep 0 reads the old values from global memory (the
+// values of the previous SOR call, never yet overwritten: the last sweep writes pixel (x, y) at step
+// x + y + 2 (S-1) > every read of it).  One barrier per step.  Splitting the sweeps over waves shortens
+// the per-step critical path S-fold and fills S times more SIMDs.  Arithmetic and order as SorPipe:
+// bit-identical.  MODE 0: OF block SOR (2x2 inverse precomputed), 2: DE point SOR.
+template <int S, int MODE, bool FIRST, bool LAST>
+struct SorWave {
+  struct Ld {
+    float4 c0, c1;
+    float ou, ov, ru, rv, bu, bv;
+  };
+  Ld L[2];
+  float pu, pv, phr;           // own results / sh of step t-1 (left neighbour of step t)
+  const float4 *C;
+  float *du, *dv;
+  float4 *ring_s;              // [3][NR] this sweep's results
+  const float4 *ring_p;        // [3][NR] previous sweep's results (s >= 1)
+  int w, h, y, s, NR;
+  unsigned dump;
+  float omega;
+  bool has_top, has_bot, border, notop;
+
+  __device__ __forceinline__ void load(int t, Ld &B) {
+    const int x = t - y - 2 * s;
+    const bool in = y < h && x >= 0 && x < w;
+    const unsigned here = (unsigned)((x + y) * h + y);
+    const unsigned o = in ? here : dump;
+    if (MODE == 0) {
+      B.c0 = C[2 * o];
+      B.c1 = C[2 * o + 1];
+    } else {
+      B.c0 = C[o];
+    }
+    if (FIRST) {
+      B.ou = du[o];
+      const unsigned orr = in && x + 1 < w ? here + h : dump;
+      B.ru = du[orr];
+      const unsigned ob = in && has_bot ? here + h + 1 : dump;
+      B.bu = du[ob];
+      if (MODE == 0) {
+        B.ov = dv[o];
+        B.rv = dv[orr];
+        B.bv = dv[ob];
+      }
+    }
+  }
+
+  template <int Q>
+  __device__ __forceinline__ void step(const int t) {
+    Ld &B = L[Q];
+    float i11, i12 = 0, i22 = 0, b1, b2 = 0, hr, vv;
+    if (MODE == 0) {
+      i11 = B.c0.x; i12 = B.c0.y; i22 = B.c0.z; b1 = B.c0.w; b2 = B.c1.x; hr = B.c1.y; vv = B.c1.z;
+    } else {
+      i11 = B.c0.x; b1 = B.c0.y; hr = B.c0.z; vv = B.c0.w;
+    }
+    float ou, ov = 0, ru, rv = 0, bu, bv = 0;
+    const int m1 = (t + 2) % 3, m2 = (t + 1) % 3, m0 = t % 3;  // ring slots of steps t-1, t-2, t
+    if (FIRST) {
+      ou = B.ou; ru = B.ru; bu = B.bu;
+      if (MODE == 0) { ov = B.ov; rv = B.rv; bv = B.bv; }
+    } else {
+      const float4 o4 = ring_p[m2 * NR + y + 1], r4 = ring_p[m1 * NR + y + 1], b4 = ring_p[m1 * NR + y + 2];
+      ou = o4.x; ov = o4.y; ru = r4.x; rv = r4.y; bu = b4.x; bv = b4.y;
+    }
+    load(t + 2, B);
+    const float4 t4 = ring_s[m1 * NR + y];   // lane y-1 (any row group) at step t-1
+    const int x = t - y - 2 * s;
+    const float hl = x > 0 ? phr : 0.0f;
+    const float vt = has_top ? t4.z : 0.0f;
+    const float ur = x < w - 1 ? ru : 0.0f;
+    float nu, nv = 0.0f;
+    if (MODE == 0) {
+      const float vr = x < w - 1 ? rv : 0.0f;
+      const float s1 = sor_rhs(border, notop, b1, hr * ur, vt * t4.x, vv * bu);
+      const float s2 = sor_rhs(border, notop, b2, hr * vr, vt * t4.y, vv * bv);
+      const float B1 = x > 0 ? hl * pu + s1 : s1;
+      const float B2 = x > 0 ? hl * pv + s2 : s2;
+      nu = ou + omega * (i11 * B1 + i12 * B2 - ou);
+      nv = ov + omega * (i12 * B1 + i22 * B2 - ov);
+    } else {
+      float su = 0.0f, sd = 0.0f;
+      su = has_top ? su - vt * t4.x : su;     sd = has_top ? sd + vt : sd;
+      su = x > 0 ? su - hl * pu : su;         sd = x > 0 ? sd + hl : sd;
+      su = has_bot ? su - vv * bu : su;       sd = has_bot ? sd + vv : sd;
+      su = x < w - 1 ? su - hr * ur : su;     sd = x < w - 1 ? sd + hr : sd;
+      const float A = i11 + sd, Bv = b1 - su;
+      nu = (1.0f - omega) * ou + omega * (Bv / A);
+    }
+    ring_s[m0 * NR + y + 1] = make_float4(nu, nv, vv, 0.0f);
+    if (LAST) {
+      const unsigned o = y < h && x >= 0 && x < w ? (unsigned)((x + y) * h + y) : dump;
+      du[o] = nu;
+      if (MODE == 0) dv[o] = nv;
+    }
+    pu = nu;
+    pv = nv;
+    phr = hr;
+    __syncthreads();
+  }
+
+  __device__ __forceinline__ void run(int T) {
+    pu = pv = phr = 0.0f;
+    load(0, L[0]);
+    load(1, L[1]);
+    for (int t = 0; t < T; t += 2) {
+      step<0>(t);
+      step<1>(t + 1);
+    }
+  }
+};
+
+template <int S, int MODE>
+__global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
+  extern __shared__ float4 ring[];  // [S][3][NR]
+  const int G = (a.h + 63) >> 6;
+  const int NR = G * 64 + 2;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = wid / S, s = wid - g * S;
+  const int y = g * 64 + lane;
+  // clear the rings: pads and not-yet-written slots are read only by lanes whose selects discard the
+  // values, but they are kept finite and deterministic anyway
+  for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) ring[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const long fo = (long)blockIdx.x * a.sp;
+  const int T2 = (((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1) + 1) & ~1;  // step count, even
+  auto setup = [&](auto &st) {
+    st.C = reinterpret_cast<const float4 *>(a.coef) + fo * (MODE == 0 ? 2 : 1);
+    st.du = a.du + fo;
+    st.dv = a.dv + fo;
+    st.ring_s = ring + s * 3 * NR;
+    st.ring_p = ring + (s > 0 ? s - 1 : 0) * 3 * NR;
+    st.w = a.w; st.h = a.h; st.y = y; st.s = s; st.NR = NR;
+    st.dump = (unsigned)((a.w + a.h - 1) * a.h + lane);
+    st.omega = a.omega;
+    st.has_top = y > 0;
+    st.has_bot = y < a.h - 1;
+    st.notop = !st.has_top;
+    st.border = !st.has_top || !st.has_bot;
+    st.run(T2);
+  };
+  if (s == 0) {
+    SorWave<S, MODE, true, S == 1> st;
+    setup(st);
+  } else if (s == S - 1) {
+    SorWave<S, MODE, false, true> st;
+    setup(st);
+  } else {
+    SorWave<S, MODE, false, false> st;
+    setup(st);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
   if (x >= a.w) return;
@@ -1490,9 +1648,26 @@ static void sor_pipe(const TvArgs &a, hipStream_t s) {
       k_tv_sor_pipe<S, 2, 1024><<<a.n, threads, 0, s>>>(a);
   }
 }
+template <int S>
+static void sor_waves(const TvArgs &a, hipStream_t s) {
+  const int G = (a.h + 63) / 64;
+  const size_t lds = sizeof(float4) * S * 3 * (G * 64 + 2);
+  if (a.nop == 2)
+    k_tv_sor_waves<S, 0><<<a.n, 64 * G * S, lds, s>>>(a);
+  else
+    k_tv_sor_waves<S, 2><<<a.n, 64 * G * S, lds, s>>>(a);
+}
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
   const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2);
+  const int G = (a.h + 63) / 64;
+  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && G * a.solverit <= 16) {
+    switch (a.solverit) {
+      case 2: sor_waves<2>(a, s); return;
+      case 3: sor_waves<3>(a, s); return;
+      case 4: sor_waves<4>(a, s); return;
+    }
+  }
   if (!tiny && a.h <= 1024 && a.solverit <= 4 && !a.sor_generic) {
     switch (a.solverit) {
       case 1: sor_pipe<1>(a, s); return;

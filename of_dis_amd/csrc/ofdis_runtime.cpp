@@ -57,6 +57,7 @@ struct ofdis_context {
   std::vector<hipEvent_t> pool;
   std::map<int, std::pair<double, long>> acc;
   int opt_sor_generic = 0;
+  int opt_sor_pipe = 0;  // 1: force the single-wave-per-row-group register pipeline (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
   int opt_streams = 1, opt_chunk = 0;
@@ -351,6 +352,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.solverit = p->tv_solverit;
       tv.camlr = 0;
       tv.sor_generic = c->opt_sor_generic;
+      tv.sor_variant = c->opt_sor_pipe;
       timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
       timed(c, 6, s, [&] {
         launch_tv_deriv1(tv, s);
@@ -681,6 +683,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   std::lock_guard<std::mutex> lock(c->mu);
   if (std::strcmp(key, "sor_generic") == 0) {
     c->opt_sor_generic = value != 0;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "sor_pipe") == 0) {
+    c->opt_sor_pipe = value != 0;
     return OFDIS_OK;
   }
   if (std::strcmp(key, "streams") == 0 && value >= 1 && value <= 16) {

@@ -51,6 +51,8 @@ CASES = [
     (160, 120, 1, 1, 2, {"patnorm": 0, "tv_innerit": 2, "tv_solverit": 4, "tv_sor": 1.3}),
     (240, 120, 1, 2, 4, {"max_iter": 16, "min_iter": 16}),    # depth from stereo, op4
     (240, 120, 3, 2, 2, {}),                                  # RGB depth
+    (400, 300, 1, 1, 2, {"sc_l": 0, "sc_f": 2}),              # 300 rows: 5 row groups x 3 sweep waves
+    (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows: register pipeline, 1024 threads
 ]
 
 
@@ -82,18 +84,20 @@ def test_pipeline_bitexact(oracle, od, ctx, w, h, noc, mode, op, over):
     assert_bitexact(got, ref, "full-resolution flow")
 
 
-@pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in CASES if c[0] <= 200])
-def test_generic_sor_bitexact(oracle, od, ctx, w, h, noc, mode, op, over):
-    """The generic global-memory SOR wavefront gives the same bits as the register-pipelined one."""
+@pytest.mark.parametrize("variant", ["sor_generic", "sor_pipe"])
+@pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in CASES if c[0] <= 200 or c[1] > 256])
+def test_sor_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op, over):
+    """The generic global-memory SOR wavefront and the one-wave register pipeline give the same bits as
+    the default sweep-per-wave kernel (and as the oracle)."""
     a, b = od.synth_pair(w, h, noc, 4, mode)
     p, q = _params(od, oracle, w, noc, mode, op, over)
     ref = oracle.run_u8(a, b, q)
-    ctx.set_option("sor_generic", 1)
+    ctx.set_option(variant, 1)
     try:
         got = ctx.run_host(a, b, p)
     finally:
-        ctx.set_option("sor_generic", 0)
-    assert_bitexact(got, ref, "generic SOR path")
+        ctx.set_option(variant, 0)
+    assert_bitexact(got, ref, f"{variant} SOR path")
 
 
 @pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2)])
