@@ -1482,67 +1482,101 @@ __device__ __forceinline__ float up_px(const float *P, long r0, long r1, const X
   return h0 * b0 + h1 * b1;
 }
 
-// Upsample for 2^l >= 2, nop = 2: one block = 1024 output columns of one output row, 4 pixels
-// (two 16-byte stores) per thread.  The two source rows it needs are staged in LDS already multiplied by
-// 2^l.  The OpenCV tap positions fx = (dx + .5) / 2^l - .5 are dyadic rationals, so computing them as
-// (2 dx + 1 - 2^l) * 2^-(l+1) in fp32 is exact and equals resizeGeneric_'s double -> float value.
+// Upsample for 2^l >= 2, nop = 2: one block = 1024 output columns x kUpRows output rows, 4 columns (two
+// 16-byte stores per row) per thread.  The source rows the block needs are staged in LDS once,
+// already multiplied by 2^l.  The OpenCV tap positions fx = (dx + .5) / 2^l - .5 are dyadic rationals, so
+// computing them as (2 dx + 1 - 2^l) * 2^-(l+1) in fp32 is exact and equals resizeGeneric_'s double ->
+// float value.  Horizontal taps are per source row (HResizeLinear), the vertical blend per output row
+// (VResizeLinear), exactly as in OpenCV's generic float path.
 constexpr int kUpCols = 1024;
+constexpr int kUpRows = 8;
+constexpr int kUpSrcRows = kUpRows / 2 + 3;  // source rows a block can touch (2^l >= 2)
+typedef float v4f __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
-  __shared__ float src[2][2][kUpCols / 2 + 8];  // [row][comp][col]; 2^l >= 2 -> <= 513 source columns
-  const int y = blockIdx.y, f = blockIdx.z;
+  __shared__ float src[kUpSrcRows][2][kUpCols / 2 + 8];  // [row][comp][col]
+  const int y0 = blockIdx.y * kUpRows, f = blockIdx.z;
   const int dx0 = blockIdx.x * kUpCols + a.offx;  // first output column of the block (uncropped coordinates)
   const int fct_i = 1 << a.log2s;
   const float fct = (float)fct_i, half_inv = 1.0f / (float)(2 * fct_i);
   const long plane = (long)a.wl * a.hl;
   const float *F = a.flow + (long)f * 2 * plane;
-  // rows (resizeGeneric_Invoker: clip(sy, 0, hl), clip(sy + 1, 0, hl); weights not clamped)
-  const int dy = y + a.offy;
-  float fy = (float)(2 * dy + 1 - fct_i) * half_inv;
-  const int sy = (int)floorf(fy);
-  fy -= (float)sy;
-  const int r0 = sy >= 0 ? (sy < a.hl ? sy : a.hl - 1) : 0;
-  const int r1 = sy + 1 >= 0 ? (sy + 1 < a.hl ? sy + 1 : a.hl - 1) : 0;
-  const float b0 = 1.f - fy, b1 = fy;
+  auto src_row = [&](int dy, float &fy) {  // resizeGeneric_Invoker rows: sy, fy (weights not clamped)
+    fy = (float)(2 * dy + 1 - fct_i) * half_inv;
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    return sy;
+  };
+  auto clip_row = [&](int r) { return r >= 0 ? (r < a.hl ? r : a.hl - 1) : 0; };
+  const int yl = min(y0 + kUpRows, a.H0) - 1;
+  float dummy;
+  const int r_first = clip_row(src_row(y0 + a.offy, dummy));
+  const int r_last = clip_row(src_row(yl + a.offy, dummy) + 1);
+  const int nr = r_last - r_first + 1;
   // source column window of this block
   const int c_lo = max(0, (int)floorf((float)(2 * dx0 + 1 - fct_i) * half_inv));
   const int ncol = kUpCols / fct_i + 2;
-  for (int k = threadIdx.x; k < 2 * 2 * ncol; k += blockDim.x) {
+  for (int k = threadIdx.x; k < nr * 2 * ncol; k += blockDim.x) {
     const int col = k % ncol, rc = k / ncol;  // rc = row * 2 + comp
     const int r = rc >> 1, comp = rc & 1;
     const int sc = min(c_lo + col, a.wl - 1);
-    src[r][comp][col] = F[comp * plane + (long)(r ? r1 : r0) * a.wl + sc] * fct;
+    src[r][comp][col] = F[comp * plane + (long)(r_first + r) * a.wl + sc] * fct;
   }
   __syncthreads();
-  const int x = blockIdx.x * kUpCols + threadIdx.x * 4;  // output column (cropped)
-  if (x >= a.W0) return;
-  float v[8];
+  // lane i of wave wv owns output columns xb + {2i, 2i+1} and xb + 128 + {2i, 2i+1} (xb = block + 256 wv):
+  // each 16-byte store instruction of a wave then covers 1 KiB contiguously (full cache lines).
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int xb = blockIdx.x * kUpCols + wv * 256 + 2 * lane;
+  int xs[2] = {xb, xb + 128};
+  int cc[4];
+  float fxs[4];
+  bool lin[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int dx = x + i + a.offx;
+    const int dx = xs[i >> 1] + (i & 1) + a.offx;
     float fx = (float)(2 * dx + 1 - fct_i) * half_inv;
     int sx = (int)floorf(fx);
     fx -= (float)sx;
     if (sx < 0) { fx = 0; sx = 0; }
-    bool lin = true;
+    bool l = true;
     if (sx + 1 >= a.wl) {
-      lin = false;
+      l = false;
       if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
     }
-    const int c = sx - c_lo;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const float s00 = src[0][k][c], s10 = src[1][k][c];
-      const float h0 = lin ? s00 * (1.f - fx) + src[0][k][c + 1] * fx : s00;
-      const float h1 = lin ? s10 * (1.f - fx) + src[1][k][c + 1] * fx : s10;
-      v[i * 2 + k] = h0 * b0 + h1 * b1;
-    }
+    cc[i] = min(max(sx - c_lo, 0), kUpCols / 2 + 6);  // columns past W0 are computed, never stored
+    fxs[i] = fx;
+    lin[i] = l;
   }
-  float *out = a.out + (((long)f * a.H0 + y) * a.W0 + x) * 2;
-  if (x + 4 <= a.W0) {
-    reinterpret_cast<float4 *>(out)[0] = make_float4(v[0], v[1], v[2], v[3]);
-    reinterpret_cast<float4 *>(out)[1] = make_float4(v[4], v[5], v[6], v[7]);
-  } else {
-    for (int i = 0; i < 2 * (a.W0 - x); ++i) out[i] = v[i];
+#pragma unroll
+  for (int i = 0; i < kUpRows; ++i) {
+    const int y = y0 + i;
+    if (y >= a.H0) break;
+    float fy;
+    const int sy = src_row(y + a.offy, fy);
+    const int j0 = clip_row(sy) - r_first, j1 = clip_row(sy + 1) - r_first;
+    const float b0 = 1.f - fy, b1 = fy;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = cc[q];
+        const float s00 = src[j0][k][c], s10 = src[j1][k][c];
+        const float h0 = lin[q] ? s00 * (1.f - fxs[q]) + src[j0][k][c + 1] * fxs[q] : s00;
+        const float h1 = lin[q] ? s10 * (1.f - fxs[q]) + src[j1][k][c + 1] * fxs[q] : s10;
+        v[q * 2 + k] = h0 * b0 + h1 * b1;
+      }
+    }
+    float *row = a.out + ((long)f * a.H0 + y) * a.W0 * 2;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int x = xs[hh];
+      if (x + 2 <= a.W0) {
+        *reinterpret_cast<v4f *>(row + 2 * x) = v4f{v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]};
+      } else if (x < a.W0) {
+        row[2 * x] = v[4 * hh];
+        row[2 * x + 1] = v[4 * hh + 1];
+      }
+    }
   }
 }
 
@@ -1688,7 +1722,7 @@ void launch_tv_final(const TvArgs &a, hipStream_t s) {
 }
 void launch_upsample(const UpArgs &a, hipStream_t s) {
   if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
-    k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), a.H0, a.n), 256, 0, s>>>(a);
+    k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
   else
     k_upsample<<<dim3(ceil_div(a.W0, 256), a.H0, a.n), 256, 0, s>>>(a);
 }
