@@ -452,10 +452,8 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
-__global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
+__device__ __forceinline__ void aggregate_px(const AggArgs &a, int x, int y, int f) {
   const LevelGeom &g = a.g;
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-  if (x >= g.w) return;
   const int hp = a.p / 2;
   // patches whose footprint [pt - p/2, pt + p/2 - 1] covers x, visited in ascending patch id
   const int pxlo = max(0, -floordiv(-(x - hp + 1 - g.offw), a.steps));
@@ -504,15 +502,23 @@ __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
   if (a.nop == 2) fl[plane] = f1;
 }
 
+// 64 x 16 pixel tiles: the patch weights of one patch row are then read by one workgroup (one XCD's L2).
+__global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63), f = blockIdx.z;
+  if (x >= a.g.w) return;
+  for (int r = threadIdx.x >> 6; r < 16; r += 4) {
+    const int y = blockIdx.y * 16 + r;
+    if (y < a.g.h) aggregate_px(a, x, y, f);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ variational
 
 __device__ __forceinline__ long skw(int x, int y, int h) { return (long)(x + y) * h + y; }
 
 // image_warp (opticalflow_aux.c:31-75) + the mean / temporal images of get_derivatives (:88-99), plus the
 // skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
-__global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-  if (x >= a.w) return;
+__device__ __forceinline__ void tv_prep_px(const TvArgs &a, int x, int y, int f) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
   const long fk = (long)f * a.sp + skw(x, y, a.h);
@@ -541,6 +547,19 @@ __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
   if (a.nop == 2) {
     a.wys[fk] = wy;
     a.dv[fk] = 0.0f;
+  }
+}
+
+// Row-major <-> skewed conversions run on 64 x 16 pixel tiles: every 64-byte line of the skewed planes
+// (16 pixels of one anti-diagonal) and of the row-major planes is then touched by ONE workgroup, so partial
+// lines merge in that XCD's L2 instead of being written / fetched once per XCD.
+constexpr int kTileW = 64, kTileH = 16;
+__global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
+  const int x = blockIdx.x * kTileW + (threadIdx.x & 63), f = blockIdx.z;
+  if (x >= a.w) return;
+  for (int r = threadIdx.x >> 6; r < kTileH; r += 4) {
+    const int y = blockIdx.y * kTileH + r;
+    if (y < a.h) tv_prep_px(a, x, y, f);
   }
 }
 
@@ -1426,9 +1445,7 @@ __global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-  if (x >= a.w) return;
+__device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
   const long fk = (long)f * a.sp + skw(x, y, a.h);
@@ -1439,6 +1456,15 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
   } else {
     const float s = a.wxs[fk] + a.du[fk];
     WX[o] = a.camlr == 0 ? ssemin(s, 0.0f) : ssemax(s, 0.0f);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
+  const int x = blockIdx.x * kTileW + (threadIdx.x & 63), f = blockIdx.z;
+  if (x >= a.w) return;
+  for (int r = threadIdx.x >> 6; r < kTileH; r += 4) {
+    const int y = blockIdx.y * kTileH + r;
+    if (y < a.h) tv_final_px(a, x, y, f);
   }
 }
 
@@ -1639,10 +1665,10 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
     patch_jm<7>(a, s);
 }
 void launch_aggregate(const AggArgs &a, hipStream_t s) {
-  k_aggregate<<<dim3(ceil_div(a.g.w, 256), a.g.h, a.n), 256, 0, s>>>(a);
+  k_aggregate<<<dim3(ceil_div(a.g.w, 64), ceil_div(a.g.h, 16), a.n), 256, 0, s>>>(a);
 }
 void launch_tv_prep(const TvArgs &a, hipStream_t s) {
-  k_tv_prep<<<dim3(ceil_div(a.w, 256), a.h, a.n), 256, 0, s>>>(a);
+  k_tv_prep<<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, kTileH), a.n), 256, 0, s>>>(a);
 }
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
   k_tv_deriv1<<<dim3(ceil_div(a.sp, 256), a.n * a.noc), 256, 0, s>>>(a);
@@ -1718,7 +1744,7 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
     k_tv_sor<0><<<a.n, 256, 0, s>>>(a);
 }
 void launch_tv_final(const TvArgs &a, hipStream_t s) {
-  k_tv_final<<<dim3(ceil_div(a.w, 256), a.h, a.n), 256, 0, s>>>(a);
+  k_tv_final<<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, kTileH), a.n), 256, 0, s>>>(a);
 }
 void launch_upsample(const UpArgs &a, hipStream_t s) {
   if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)

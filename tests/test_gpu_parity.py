@@ -170,3 +170,22 @@ def test_full_1080p_bitexact(oracle, od, ctx):
     got = ctx.run_host(a, b, p)
     ref = oracle.run_u8(a, b, oracle.oppoint(2, 1920, 1, 1))
     assert_bitexact(got, ref, "1080p op2")
+
+
+def test_oflow_hpp_dropin_program(oracle, od, tmp_path):
+    """A C++ program written against include/ofdis_oflow.hpp (reference signature of OFC::OFClass) gives
+    the oracle's flow bit-for-bit."""
+    import subprocess
+    from test_host_abi import build_dropin
+    w, h = 256, 128
+    a, b = od.synth_pair(w, h, 1, 9, 1)
+    for name, im in (("a.pgm", a), ("b.pgm", b)):
+        (tmp_path / name).write_bytes(f"P5\n{w} {h}\n255\n".encode() + im.tobytes())
+    exe = build_dropin(tmp_path)
+    out = tmp_path / "o.flo"
+    r = subprocess.run([exe, str(tmp_path / "a.pgm"), str(tmp_path / "b.pgm"), str(out)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    q = oracle.oppoint(2, w, 1, 1)
+    want = oracle.oflow(oracle.build_pyramid(a, q, 8), oracle.build_pyramid(b, q, 8), w, h, q, 8)
+    assert_bitexact(od.read_flo(str(out)), want, "OFC::OFClass drop-in program")

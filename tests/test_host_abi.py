@@ -206,3 +206,18 @@ def test_cli_usage_and_no_gpu(tmp_path):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert not (tmp_path / "o.flo").exists()
+
+
+def build_dropin(tmp_path):
+    """Compile tests/cpp/dropin_ofclass.cpp against include/ofdis_oflow.hpp + libofdis.so."""
+    exe = str(tmp_path / "dropin_ofclass")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-std=c++14", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "dropin_ofclass.cpp"), "-L", libdir, "-lofdis",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True, capture_output=True, timeout=300)
+    return exe
+
+
+def test_oflow_hpp_dropin_compiles(tmp_path):
+    """The reference-signature OFC::OFClass wrapper compiles and links as plain C++ (no HIP headers)."""
+    assert os.access(build_dropin(tmp_path), os.X_OK)
