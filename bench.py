@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the batch's chunks round-robin over")
     ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = whole batch in one chunk)")
+    ap.add_argument("--tv-fused", type=int, default=-1, help="1/0: force the fused TV level kernel on/off")
     ap.add_argument("--no-kernel-timing", action="store_true")
     return ap.parse_args()
 
@@ -87,6 +88,8 @@ def main():
     ctx = od.Context(dev.index)
     ctx.set_option("streams", args.streams)
     ctx.set_option("chunk", args.chunk)
+    if args.tv_fused >= 0:
+        ctx.set_option("tv_fused", args.tv_fused)
 
     # synthetic inputs, resident in HBM before timing: distinct pairs per rank, tiled over the batch
     first = odd.shard_range(B * world, rank, world)[0]
@@ -181,7 +184,7 @@ def main():
             "frames_per_sec": round(frames / elapsed, 2),
             "config": {"workload": f"run_OF_INT {W}x{H} gray op-point {args.oppoint}, {B} pairs/GPU/step",
                        "width": W, "height": H, "oppoint": args.oppoint, "batch_per_gpu": B,
-                       "streams": args.streams, "chunk": args.chunk,
+                       "streams": args.streams, "chunk": args.chunk, "tv_fused": args.tv_fused,
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity, "kernels": kernels,
         }

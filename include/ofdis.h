@@ -133,6 +133,10 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        one (both are exact-order; used by the parity tests);
  *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline instead of the default
  *                        sweep-per-wave SOR (same bits; A/B and parity tests);
+ *   "tv_fused" (0/1, default 0): run each refinement level as one launch per frame (k_tv_level) when the
+ *                        level fits one workgroup, instead of one launch per phase (same bits; slower
+ *                        today: one workgroup per frame leaves the data-parallel phases latency-bound);
+ *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (same bits; A/B);
  *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into
  *                        chunks that run round-robin on that many HIP streams with separate workspaces,
  *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels.

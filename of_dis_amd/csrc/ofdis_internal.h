@@ -55,6 +55,7 @@ struct PatchArgs {
   int costfct, patnorm, max_iter, min_iter;
   float dp_thresh_sq, dr_thresh, res_thresh, outlierthresh;
   int camlr;
+  int wave_per_patch;                         // 1: force the one-wave-per-patch kernel (A/B testing)
   LevelGeom g;
 };
 
@@ -106,6 +107,9 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
+// Whole refinement level in one launch per frame (k_tv_level); only when tv_level_fusable(a).
+bool tv_level_fusable(const TvArgs &a);
+void launch_tv_level(const TvArgs &a, int n_inner, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);
 
 }  // namespace ofdis

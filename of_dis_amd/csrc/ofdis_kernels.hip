@@ -448,6 +448,217 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
     if (lane + 64 * j < a.novals) pwo[lane + 64 * j] = pw[j];
 }
 
+// ---------------------------------------------------------------- DIS patches, eight lanes per patch
+// Eight lanes per patch, eight patches per wave.  Lane s of a patch holds the values v = s + 8k (k < PAIRS)
+// and, when p*p*noc is an odd number of 4-float packets, the tail value 8*PAIRS + (s & 3) (duplicated in
+// lanes s and s^4).  Eigen's SSE reduction (two 4-lane packet accumulators, res0 + res1, odd packet,
+// (l0 + l2) + (l1 + l3)) is then: the lane's own chain sum in registers, and a butterfly over lanes
+// s^4, s^2, s^1 (DPP, within the 8-lane group) whose pairings are exactly the packet tree's -- additions
+// commute bit-exactly, so every lane ends with the reference's total.  No LDS, and the per-patch scalar
+// work (the 2x2 solve, the stopping tests) runs lane-parallel for eight patches at once.
+__device__ __forceinline__ float grp_xor4(float v) {  // lane s <- lane s^4 (row_half_mirror, then quad xor 3)
+  const int m = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true);
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float grp_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float grp_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+}
+template <int PAIRS, int ODD>
+__device__ __forceinline__ float grp_eigen_sum(const float (&x)[PAIRS + ODD]) {
+  float r;
+  if (PAIRS > 0) {
+    float acc = x[0];
+#pragma unroll
+    for (int k = 1; k < PAIRS; ++k) acc = acc + x[k];
+    r = acc + grp_xor4(acc);             // res0 + res1
+    if (ODD) r = r + x[PAIRS];           // odd trailing packet
+  } else {
+    r = x[0];                            // a single packet
+  }
+  r = r + grp_xor2(r);                   // l0 + l2, l1 + l3
+  return r + grp_xor1(r);                // (l0 + l2) + (l1 + l3)
+}
+
+template <int NOP, int PAIRS, int ODD>
+__global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
+  constexpr int V = PAIRS + ODD;
+  const LevelGeom &g = a.g;
+  const int s8 = threadIdx.x & 7;
+  const long gp = (long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const bool live = gp < (long)a.n * g.npatch;
+  const long gq = live ? gp : 0;
+  const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
+  const int pxi = ip / g.noph, pyi = ip % g.noph;
+  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+  const long fs = (long)g.W * g.H * a.noc;
+  const int noc = a.noc, P = a.p, W = g.W;
+  const float inv_n = 1.0f / (float)a.novals;
+  const bool pow2 = (a.novals & (a.novals - 1)) == 0;  // x / n == x * (1/n) exactly for n = 2^k
+  auto div_n = [&](float x) { return pow2 ? x * inv_n : x / (float)a.novals; };
+  int offs[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int v = k < PAIRS ? s8 + 8 * k : 8 * PAIRS + (s8 & 3);
+    const int ch = v % noc, q = v / noc;
+    offs[k] = ((q / P) * W + (q % P)) * noc + ch;
+  }
+  // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
+  float tmp[V], gx[V], gy[V], pw[V];
+  {
+    const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
+    const long base = ((long)(py - P / 2) * W + (px - P / 2)) * noc;
+    const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      tmp[k] = A[offs[k]];
+      gx[k] = DX[offs[k]];
+      gy[k] = DY[offs[k]];
+      pw[k] = 0.0f;
+    }
+  }
+  if (a.patnorm > 0) {
+    const float mean = div_n(grp_eigen_sum<PAIRS, ODD>(tmp));
+#pragma unroll
+    for (int k = 0; k < V; ++k) tmp[k] = tmp[k] - mean;
+  }
+  // ---- ComputeHessian (patch.cpp:69-86)
+  float H00, H01 = 0.0f, H11 = 0.0f;
+  {
+    float q0[V], q1[V], q2[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      q0[k] = gx[k] * gx[k];
+      q1[k] = gx[k] * gy[k];
+      q2[k] = gy[k] * gy[k];
+    }
+    H00 = grp_eigen_sum<PAIRS, ODD>(q0);
+    if (NOP == 2) {
+      H01 = grp_eigen_sum<PAIRS, ODD>(q1);
+      H11 = grp_eigen_sum<PAIRS, ODD>(q2);
+      if (H00 * H11 - H01 * H01 == 0.0f) {
+        H00 = (float)((double)H00 + 1e-10);
+        H11 = (float)((double)H11 + 1e-10);
+      }
+    } else if (H00 == 0.0f) {
+      H00 = (float)((double)H00 + 1e-10);
+    }
+  }
+  const Llt2 fac = llt2_factor(H00, H01, H11);
+  const float fac1 = llt1_factor(H00);
+  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
+  float pin0 = 0.0f, pin1 = 0.0f;
+  if (a.prev) {
+    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
+    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
+    pin0 = pv[0] * 2;
+    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  const float *Bimg = a.img_b + f * fs;
+  const long rowstep = (long)W * noc;
+  // ---- OptimizeStart (patch.cpp:117-154)
+  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
+  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
+  const float st0 = pt0, st1 = pt1;
+  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
+  int cnt = 0;
+  bool converged = !live;
+  float b0 = 0.0f, b1 = 0.0f;
+  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  auto err = [&]() {  // getPatchStaticBil + LossComputeErrorImage + OptimizeComputeErrImg (patch.cpp:221-413)
+    const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
+    const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
+    const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
+    const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
+    const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+    const float *Q = Bimg + ((long)(pos1 - P / 2) * W + (pos0 - P / 2)) * noc;
+    float pd[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float *q = Q + offs[k];
+      const float A = q[0], Bv = q[-noc], C = q[-rowstep], D = q[-rowstep - noc];
+      pd[k] = w0 * A + w1 * Bv + w2 * C + w3 * D;
+    }
+    if (a.patnorm > 0) {
+      const float mean = div_n(grp_eigen_sum<PAIRS, ODD>(pd));
+#pragma unroll
+      for (int k = 0; k < V; ++k) pd[k] = pd[k] - mean;
+    }
+    float ab[V], ex[V], ey[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float d = pd[k] - tmp[k];
+      float w, e;
+      if (a.costfct == 0) {
+        e = d;
+        w = fabsf(d);
+      } else if (a.costfct == 1) {
+        w = sqrtf(fabsf(d));
+        e = copysignf(w, d);
+      } else {
+        w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        e = copysignf(w, d);
+      }
+      pw[k] = w;
+      ab[k] = fabsf(w);
+      ex[k] = gx[k] * e;
+      ey[k] = gy[k] * e;
+    }
+    const float r0 = grp_eigen_sum<PAIRS, ODD>(ab);
+    b0 = grp_eigen_sum<PAIRS, ODD>(ex);
+    if (NOP == 2) b1 = grp_eigen_sum<PAIRS, ODD>(ey);
+    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+    if (cnt == 1) sq_init = sq;
+    mares_old = mares;
+    mares = div_n(r0);
+    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+    if (!keep) converged = true;
+  };
+  if (!converged) {
+    if (oob(pt0, pt1)) {
+      converged = true;  // pweight stays 0: never written upstream, defined as 0
+    } else {
+      mares = 1e5f;
+      err();
+    }
+  }
+  // ---- OptimizeIter loop (patch.cpp:156-210)
+  while (!converged) {
+    ++cnt;
+    if (NOP == 2) {
+      llt2_solve(fac, b0, b1, d0, d1);
+      p0 = p0 - d0;
+      p1 = p1 - d1;
+    } else {
+      d0 = llt1_solve(fac1, b0);
+      p0 = p0 - d0;
+      p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+    }
+    pt0 = ptr0 + p0;
+    if (NOP == 2) pt1 = ptr1 + p1;
+    const float ex = st0 - pt0, ey = st1 - pt1;
+    if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+      p0 = pin0;
+      p1 = pin1;
+      pt0 = ptr0 + p0;
+      if (NOP == 2) pt1 = ptr1 + p1;
+      converged = true;
+    }
+    err();
+  }
+  // ---- outputs
+  if (!live) return;
+  if (s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
+  float *pwo = a.pweight + gp * a.novals;
+#pragma unroll
+  for (int k = 0; k < PAIRS; ++k) pwo[s8 + 8 * k] = pw[k];
+  if (ODD && s8 < 4) pwo[8 * PAIRS + s8] = pw[PAIRS];
+}
+
 // ------------------------------------------------------------------------------------------------ aggregation
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -588,10 +799,8 @@ __device__ __forceinline__ bool skew_xy(int kk, int w, int h, int &x, int &y) {
   return x >= 0 && x < w;
 }
 
-__global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk >= a.sp) return;
-  const long pl = blockIdx.y, idx = pl * a.sp + kk;
+__device__ __forceinline__ void tv_deriv1_px(const TvArgs &a, long pl, int kk) {
+  const long idx = pl * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const float *t = a.t + pl * a.sp, *dt = a.dt + pl * a.sp;
@@ -601,15 +810,22 @@ __global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
   a.Iyz[idx] = conv5v(dt, x, y, a.w, a.h);
 }
 
-__global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk >= a.sp) return;
-  const long pl = blockIdx.y, idx = pl * a.sp + kk;
+__device__ __forceinline__ void tv_deriv2_px(const TvArgs &a, long pl, int kk) {
+  const long idx = pl * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   a.Ixx[idx] = conv5h(a.Ix + pl * a.sp, x, y, a.w, a.h);
   a.Ixy[idx] = conv5v(a.Ix + pl * a.sp, x, y, a.w, a.h);
   a.Iyy[idx] = conv5v(a.Iy + pl * a.sp, x, y, a.w, a.h);
+}
+
+__global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_deriv1_px(a, blockIdx.y, kk);
+}
+__global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_deriv2_px(a, blockIdx.y, kk);
 }
 
 #define DNORM (0.1f * 0.1f)
@@ -830,30 +1046,28 @@ __device__ __forceinline__ void data_de(int noc, long plane, float u, float m, c
 
 // uu / vv of the current inner iteration (refine_variational.cpp:189-190,209-222,305-320)
 template <int NOP>
-__device__ __forceinline__ float uu_at(const TvArgs &a, long fk) {
+__device__ __forceinline__ float uu_at(const TvArgs &a, long fk, bool first) {
   const float wx = a.wxs[fk];
-  if (a.first_iter) return wx;
+  if (first) return wx;
   if (NOP == 2) return wx + a.du[fk];
   return a.camlr == 0 ? ssemin(wx + a.du[fk], 0.0f) : ssemax(wx + a.du[fk], 0.0f);
 }
 
 // compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
 template <int NOP>
-__global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk >= a.sp) return;
-  const long f0 = (long)blockIdx.y * a.sp, idx = f0 + kk;
+__device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, bool first) {
+  const long f0 = fr * a.sp, idx = f0 + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const int w = a.w, h = a.h;
   const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h);
   const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h);
-  const float uc = uu_at<NOP>(a, idx);
-  const float ux = kK3[0] * uu_at<NOP>(a, kl) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kr));
-  const float uy = kK3[0] * uu_at<NOP>(a, ku) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kd));
+  const float uc = uu_at<NOP>(a, idx, first);
+  const float ux = kK3[0] * uu_at<NOP>(a, kl, first) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kr, first));
+  const float uy = kK3[0] * uu_at<NOP>(a, ku, first) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kd, first));
   float vx, vy;
   if (NOP == 2) {
-    auto vv = [&](long k) { return a.first_iter ? a.wys[k] : a.wys[k] + a.dv[k]; };
+    auto vv = [&](long k) { return first ? a.wys[k] : a.wys[k] + a.dv[k]; };
     const float vc = vv(idx);
     vx = kK3[0] * vv(kl) + (kK3[1] * vc + kK3[2] * vv(kr));
     vy = kK3[0] * vv(ku) + (kK3[1] * vc + kK3[2] * vv(kd));
@@ -868,10 +1082,8 @@ __global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
 // One TV inner iteration's system (refine_variational.cpp:195-199): diffusivities from s
 // (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
 template <int NOP>
-__global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk >= a.sp) return;
-  const long fr = blockIdx.y, idx = fr * a.sp + kk;
+__device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
+  const long idx = fr * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const int w = a.w, h = a.h;
@@ -929,6 +1141,17 @@ __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
   } else {
     reinterpret_cast<float4 *>(a.coef)[idx] = make_float4(A11, B1, shv, svv);
   }
+}
+
+template <int NOP>
+__global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_smooth_px<NOP>(a, blockIdx.y, kk, a.first_iter != 0);
+}
+template <int NOP>
+__global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_system_px<NOP>(a, blockIdx.y, kk);
 }
 
 // Generic exact-order SOR (any size / sweep count): one workgroup per frame, in-place skewed arrays in
@@ -1404,9 +1627,9 @@ struct SorWave {
   }
 };
 
+// One frame's SOR call by the whole workgroup (64 * ceil(h/64) * S threads); ring: S * 3 * NR float4 of LDS.
 template <int S, int MODE>
-__global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
-  extern __shared__ float4 ring[];  // [S][3][NR]
+__device__ __forceinline__ void sor_waves_frame(const TvArgs &a, int frame, float4 *ring) {
   const int G = (a.h + 63) >> 6;
   const int NR = G * 64 + 2;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1416,7 +1639,7 @@ __global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
   // values, but they are kept finite and deterministic anyway
   for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) ring[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  const long fo = (long)blockIdx.x * a.sp;
+  const long fo = (long)frame * a.sp;
   const int T2 = (((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1) + 1) & ~1;  // step count, even
   auto setup = [&](auto &st) {
     st.C = reinterpret_cast<const float4 *>(a.coef) + fo * (MODE == 0 ? 2 : 1);
@@ -1445,6 +1668,12 @@ __global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
   }
 }
 
+template <int S, int MODE>
+__global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
+  extern __shared__ float4 ring[];  // [S][3][NR]
+  sor_waves_frame<S, MODE>(a, blockIdx.x, ring);
+}
+
 __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
@@ -1466,6 +1695,37 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
     const int y = blockIdx.y * kTileH + r;
     if (y < a.h) tv_final_px(a, x, y, f);
   }
+}
+
+// One whole refinement level per frame in ONE launch (refine_variational.cpp:152-342): warp + derivatives,
+// then tv_innerit * (level + 1) x [smoothness, system, exact-order SOR], then the flow update.  The
+// workgroup is the sweep-per-wave SOR's (64 * ceil(h/64) * S threads); the data-parallel phases loop over
+// the frame's skewed planes with all its threads, phases are separated by workgroup barriers, and the
+// frame's planes stay in the XCD's L2 / the Infinity Cache between phases.  Same per-pixel functions as
+// the one-phase-per-launch path: bit-identical.
+template <int S, int MODE, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tv_level(TvArgs a, int n_inner) {
+  extern __shared__ float4 ring[];
+  constexpr int NOP = MODE == 0 ? 2 : 1;
+  const int f = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int w = a.w, h = a.h, sp = (int)a.sp;
+  for (int p = tid; p < w * h; p += nt) tv_prep_px(a, p % w, p / w, f);
+  __syncthreads();
+  for (int c = 0; c < a.noc; ++c)
+    for (int kk = tid; kk < sp; kk += nt) tv_deriv1_px(a, (long)f * a.noc + c, kk);
+  __syncthreads();
+  for (int c = 0; c < a.noc; ++c)
+    for (int kk = tid; kk < sp; kk += nt) tv_deriv2_px(a, (long)f * a.noc + c, kk);
+  __syncthreads();
+  for (int it = 0; it < n_inner; ++it) {
+    for (int kk = tid; kk < sp; kk += nt) tv_smooth_px<NOP>(a, f, kk, it == 0);
+    __syncthreads();
+    for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP>(a, f, kk);
+    __syncthreads();
+    sor_waves_frame<S, MODE>(a, f, ring);
+    __syncthreads();
+  }
+  for (int p = tid; p < w * h; p += nt) tv_final_px(a, p % w, p / w, f);
 }
 
 // ------------------------------------------------------------------------------------------------ output
@@ -1655,7 +1915,26 @@ static void patch_jm(const PatchArgs &a, hipStream_t s) {
   else
     k_patch<1, JM><<<ceil_div(waves, kPatchWaves), 64 * kPatchWaves, lds, s>>>(a);
 }
+template <int PAIRS, int ODD>
+static void patch8(const PatchArgs &a, hipStream_t s) {
+  const long patches = (long)a.n * a.g.npatch;
+  if (a.nop == 2)
+    k_patch8<2, PAIRS, ODD><<<ceil_div(patches, 32), 256, 0, s>>>(a);
+  else
+    k_patch8<1, PAIRS, ODD><<<ceil_div(patches, 32), 256, 0, s>>>(a);
+}
 void launch_patch(const PatchArgs &a, hipStream_t s) {
+  if (!a.wave_per_patch) {
+    switch (a.novals) {  // eight lanes per patch for the common shapes
+      case 64: patch8<8, 0>(a, s); return;    // p 8, gray
+      case 144: patch8<18, 0>(a, s); return;  // p 12, gray
+      case 192: patch8<24, 0>(a, s); return;  // p 8, RGB
+      case 36: patch8<4, 1>(a, s); return;    // p 6, gray
+      case 100: patch8<12, 1>(a, s); return;  // p 10, gray
+      case 16: patch8<2, 0>(a, s); return;    // p 4, gray
+      case 4: patch8<0, 1>(a, s); return;     // p 2, gray
+    }
+  }
   const int J = (a.novals + 63) / 64;
   if (J <= 1)
     patch_jm<1>(a, s);
@@ -1742,6 +2021,34 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
     k_tv_sor<1><<<a.n, 256, 0, s>>>(a);
   else
     k_tv_sor<0><<<a.n, 256, 0, s>>>(a);
+}
+template <int S, int MODE>
+static void tv_level_s(const TvArgs &a, int n_inner, hipStream_t s) {
+  const int G = (a.h + 63) / 64;
+  const int threads = 64 * G * S;
+  const size_t lds = sizeof(float4) * S * 3 * (G * 64 + 2);
+  if (threads <= 256)
+    k_tv_level<S, MODE, 256><<<a.n, threads, lds, s>>>(a, n_inner);
+  else if (threads <= 512)
+    k_tv_level<S, MODE, 512><<<a.n, threads, lds, s>>>(a, n_inner);
+  else
+    k_tv_level<S, MODE, 1024><<<a.n, threads, lds, s>>>(a, n_inner);
+}
+bool tv_level_fusable(const TvArgs &a) {
+  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2);
+  const int G = (a.h + 63) / 64;
+  return !tiny && !a.sor_generic && a.sor_variant == 0 && a.solverit >= 2 && a.solverit <= 4 &&
+         G * a.solverit <= 16;
+}
+void launch_tv_level(const TvArgs &a, int n_inner, hipStream_t s) {
+  switch (a.solverit * 2 + (a.nop == 2 ? 0 : 1)) {
+    case 4: tv_level_s<2, 0>(a, n_inner, s); return;
+    case 5: tv_level_s<2, 2>(a, n_inner, s); return;
+    case 6: tv_level_s<3, 0>(a, n_inner, s); return;
+    case 7: tv_level_s<3, 2>(a, n_inner, s); return;
+    case 8: tv_level_s<4, 0>(a, n_inner, s); return;
+    case 9: tv_level_s<4, 2>(a, n_inner, s); return;
+  }
 }
 void launch_tv_final(const TvArgs &a, hipStream_t s) {
   k_tv_final<<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, kTileH), a.n), 256, 0, s>>>(a);

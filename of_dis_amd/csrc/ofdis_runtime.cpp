@@ -24,8 +24,8 @@ using namespace ofdis;
 
 namespace {
 
-const char *const kKernelNames[] = {"pyr_base", "pyr_down",  "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample"};
+const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_level"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -58,6 +58,8 @@ struct ofdis_context {
   std::map<int, std::pair<double, long>> acc;
   int opt_sor_generic = 0;
   int opt_sor_pipe = 0;  // 1: force the single-wave-per-row-group register pipeline (A/B)
+  int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
+  int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
   int opt_streams = 1, opt_chunk = 0;
@@ -289,6 +291,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.res_thresh = p->res_thresh;
     pa.outlierthresh = (float)p->p_samp_s / 2;
     pa.camlr = 0;
+    pa.wave_per_patch = c->opt_wave_per_patch;
     pa.g = g;
     timed(c, 3, s, [&] { launch_patch(pa, s); });
 
@@ -353,20 +356,24 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.camlr = 0;
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
-      timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
-      timed(c, 6, s, [&] {
-        launch_tv_deriv1(tv, s);
-        launch_tv_deriv2(tv, s);
-      });
-      for (int it = 0; it < n_inner; ++it) {
-        tv.first_iter = it == 0;
-        timed(c, 7, s, [&] {
-          launch_tv_smooth(tv, s);
-          launch_tv_system(tv, s);
+      if (c->opt_tv_fused && tv_level_fusable(tv)) {
+        timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
+      } else {
+        timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
+        timed(c, 6, s, [&] {
+          launch_tv_deriv1(tv, s);
+          launch_tv_deriv2(tv, s);
         });
-        timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
+        for (int it = 0; it < n_inner; ++it) {
+          tv.first_iter = it == 0;
+          timed(c, 7, s, [&] {
+            launch_tv_smooth(tv, s);
+            launch_tv_system(tv, s);
+          });
+          timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
+        }
+        timed(c, 9, s, [&] { launch_tv_final(tv, s); });
       }
-      timed(c, 9, s, [&] { launch_tv_final(tv, s); });
     }
     if (times) {
       HIP_OK(hipEventRecord(ev[3], s));
@@ -685,6 +692,14 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     c->opt_sor_generic = value != 0;
     return OFDIS_OK;
   }
+  if (std::strcmp(key, "wave_per_patch") == 0) {
+    c->opt_wave_per_patch = value != 0;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "tv_fused") == 0) {
+    c->opt_tv_fused = value != 0;
+    return OFDIS_OK;
+  }
   if (std::strcmp(key, "sor_pipe") == 0) {
     c->opt_sor_pipe = value != 0;
     return OFDIS_OK;
@@ -722,7 +737,12 @@ int ofdis_context_kernel_time(ofdis_context *c, const char *name, double *total_
 }
 
 const char *ofdis_kernel_names(void) {
-  return "pyr_base,pyr_down,pyr_pad_grad,patch,aggregate,tv_prep,tv_deriv,tv_system,tv_sor,tv_final,upsample";
+  static const std::string names = [] {
+    std::string r;
+    for (const char *k : kKernelNames) r += (r.empty() ? "" : ",") + std::string(k);
+    return r;
+  }();
+  return names.c_str();
 }
 
 // Byte model of SURVEY §8(d), per frame pair, for the roofline of each kernel family.
@@ -745,6 +765,11 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
     if (k == "aggregate") b += px * 4.0 * nop + (double)g.npatch * 4.0 * (nop + novals);
     if (k == "pyr_pad_grad") b += 2.0 * (px * 4.0 * noc + 3.0 * g.W * g.H * 4.0 * noc);
     if (k == "pyr_down" && g.level > p->sc_l) b += 2.0 * noc * 4.0 * (4.0 * px + px);
+    if (p->usetvref && k == "tv_level") {  // the fused level: prep + derivatives + n_inner x (system + SOR) + final
+      b += px * 4.0 * (4 * noc + 1 + 3 * nop) + px * 4.0 * noc * (2 + 4 + 2 + 3) + px * 4.0 * 3 * nop;
+      b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
+      b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
+    }
     if (p->usetvref) {
       if (k == "tv_prep") b += px * 4.0 * (4 * noc + 1 + 3 * nop);
       if (k == "tv_deriv") b += px * 4.0 * noc * (2 + 4 + 2 + 3);

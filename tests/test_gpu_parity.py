@@ -84,20 +84,28 @@ def test_pipeline_bitexact(oracle, od, ctx, w, h, noc, mode, op, over):
     assert_bitexact(got, ref, "full-resolution flow")
 
 
-@pytest.mark.parametrize("variant", ["sor_generic", "sor_pipe"])
+VARIANTS = [  # (option, value, default): non-default kernels
+    ("tv_fused", 1, 0),        # one launch per TV level (fused phases + sweep-per-wave SOR)
+    ("sor_pipe", 1, 0),        # one-wave register-pipeline SOR
+    ("sor_generic", 1, 0),     # generic global-memory SOR
+    ("wave_per_patch", 1, 0),  # one wave per DIS patch instead of eight lanes
+]
+
+
+@pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: v[0])
 @pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in CASES if c[0] <= 200 or c[1] > 256])
-def test_sor_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op, over):
-    """The generic global-memory SOR wavefront and the one-wave register pipeline give the same bits as
-    the default sweep-per-wave kernel (and as the oracle)."""
+def test_kernel_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op, over):
+    """Every kernel variant (TV / SOR / DIS patch) gives the same bits as the default path and the oracle."""
+    key, val, default = variant
     a, b = od.synth_pair(w, h, noc, 4, mode)
     p, q = _params(od, oracle, w, noc, mode, op, over)
     ref = oracle.run_u8(a, b, q)
-    ctx.set_option(variant, 1)
+    ctx.set_option(key, val)
     try:
         got = ctx.run_host(a, b, p)
     finally:
-        ctx.set_option(variant, 0)
-    assert_bitexact(got, ref, f"{variant} SOR path")
+        ctx.set_option(key, default)
+    assert_bitexact(got, ref, f"{key}={val}")
 
 
 @pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2)])
