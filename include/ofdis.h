@@ -137,6 +137,7 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        level fits one workgroup, instead of one launch per phase (same bits; slower
  *                        today: one workgroup per frame leaves the data-parallel phases latency-bound);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (same bits; A/B);
+ *   "sor_rows" (0, 1, 2, 4): rows per lane of the sweep-per-wave SOR (0 = automatic; same bits);
  *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into
  *                        chunks that run round-robin on that many HIP streams with separate workspaces,
  *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels.

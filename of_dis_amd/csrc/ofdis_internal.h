@@ -87,6 +87,7 @@ struct TvArgs {
   int camlr;
   int sor_generic;             // force the generic global-memory SOR wavefront (A/B testing)
   int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
+  int sor_rows;                // sweep-per-wave SOR rows per lane: 0 auto, 1/2/4/8 forced (A/B testing)
 };
 
 struct UpArgs {

@@ -1520,104 +1520,131 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_pipe(TvArgs a) {
 // x + y + 2 (S-1) > every read of it).  One barrier per step.  Splitting the sweeps over waves shortens
 // the per-step critical path S-fold and fills S times more SIMDs.  Arithmetic and order as SorPipe:
 // bit-identical.  MODE 0: OF block SOR (2x2 inverse precomputed), 2: DE point SOR.
-template <int S, int MODE, bool FIRST, bool LAST>
+template <int S, int MODE, bool FIRST, bool LAST, int R>
 struct SorWave {
   struct Ld {
     float4 c0, c1;
     float ou, ov, ru, rv, bu, bv;
   };
-  Ld L[2];
-  float pu, pv, phr;           // own results / sh of step t-1 (left neighbour of step t)
+  Ld L[2][R];
+  float pu[R], pv[R], phr[R], pvv[R];  // own results / sh / sv of step t-1 (left and, for r > 0, top)
   const float4 *C;
   float *du, *dv;
-  float4 *ring_s;              // [3][NR] this sweep's results
+  float4 *ring_s;              // [3][NR] this sweep's results (entry y + 1 for row y)
   const float4 *ring_p;        // [3][NR] previous sweep's results (s >= 1)
-  int w, h, y, s, NR;
+  int w, h, y0, s, NR;         // rows y0 .. y0 + R - 1
   unsigned dump;
   float omega;
-  bool has_top, has_bot, border, notop;
 
-  __device__ __forceinline__ void load(int t, Ld &B) {
-    const int x = t - y - 2 * s;
-    const bool in = y < h && x >= 0 && x < w;
-    const unsigned here = (unsigned)((x + y) * h + y);
-    const unsigned o = in ? here : dump;
-    if (MODE == 0) {
-      B.c0 = C[2 * o];
-      B.c1 = C[2 * o + 1];
-    } else {
-      B.c0 = C[o];
-    }
-    if (FIRST) {
-      B.ou = du[o];
-      const unsigned orr = in && x + 1 < w ? here + h : dump;
-      B.ru = du[orr];
-      const unsigned ob = in && has_bot ? here + h + 1 : dump;
-      B.bu = du[ob];
+  __device__ __forceinline__ void load(int t, Ld (&B)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int y = y0 + r;
+      const int x = t - y - 2 * s;
+      const bool in = y < h && x >= 0 && x < w;
+      const unsigned here = (unsigned)((x + y) * h + y);
+      const unsigned o = in ? here : dump;
       if (MODE == 0) {
-        B.ov = dv[o];
-        B.rv = dv[orr];
-        B.bv = dv[ob];
+        B[r].c0 = C[2 * o];
+        B[r].c1 = C[2 * o + 1];
+      } else {
+        B[r].c0 = C[o];
+      }
+      if (FIRST) {
+        B[r].ou = du[o];
+        const unsigned orr = in && x + 1 < w ? here + h : dump;
+        B[r].ru = du[orr];
+        const unsigned ob = in && y < h - 1 ? here + h + 1 : dump;
+        B[r].bu = du[ob];
+        if (MODE == 0) {
+          B[r].ov = dv[o];
+          B[r].rv = dv[orr];
+          B[r].bv = dv[ob];
+        }
       }
     }
   }
 
   template <int Q>
   __device__ __forceinline__ void step(const int t) {
-    Ld &B = L[Q];
-    float i11, i12 = 0, i22 = 0, b1, b2 = 0, hr, vv;
-    if (MODE == 0) {
-      i11 = B.c0.x; i12 = B.c0.y; i22 = B.c0.z; b1 = B.c0.w; b2 = B.c1.x; hr = B.c1.y; vv = B.c1.z;
-    } else {
-      i11 = B.c0.x; b1 = B.c0.y; hr = B.c0.z; vv = B.c0.w;
-    }
-    float ou, ov = 0, ru, rv = 0, bu, bv = 0;
+    Ld (&B)[R] = L[Q];
     const int m1 = (t + 2) % 3, m2 = (t + 1) % 3, m0 = t % 3;  // ring slots of steps t-1, t-2, t
-    if (FIRST) {
-      ou = B.ou; ru = B.ru; bu = B.bu;
-      if (MODE == 0) { ov = B.ov; rv = B.rv; bv = B.bv; }
-    } else {
-      const float4 o4 = ring_p[m2 * NR + y + 1], r4 = ring_p[m1 * NR + y + 1], b4 = ring_p[m1 * NR + y + 2];
-      ou = o4.x; ov = o4.y; ru = r4.x; rv = r4.y; bu = b4.x; bv = b4.y;
+    float i11[R], i12[R], i22[R], b1[R], b2[R], hr[R], vv[R];
+    float ou[R], ov[R], ru[R], rv[R], bu[R], bv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (MODE == 0) {
+        i11[r] = B[r].c0.x; i12[r] = B[r].c0.y; i22[r] = B[r].c0.z; b1[r] = B[r].c0.w;
+        b2[r] = B[r].c1.x; hr[r] = B[r].c1.y; vv[r] = B[r].c1.z;
+      } else {
+        i11[r] = B[r].c0.x; b1[r] = B[r].c0.y; hr[r] = B[r].c0.z; vv[r] = B[r].c0.w;
+        i12[r] = i22[r] = b2[r] = 0.0f;
+      }
+      if (FIRST) {
+        ou[r] = B[r].ou; ru[r] = B[r].ru; bu[r] = B[r].bu;
+        ov[r] = MODE == 0 ? B[r].ov : 0.0f; rv[r] = MODE == 0 ? B[r].rv : 0.0f;
+        bv[r] = MODE == 0 ? B[r].bv : 0.0f;
+      } else {
+        const int e = y0 + r + 1;
+        const float4 o4 = ring_p[m2 * NR + e], r4 = ring_p[m1 * NR + e], b4 = ring_p[m1 * NR + e + 1];
+        ou[r] = o4.x; ov[r] = o4.y; ru[r] = r4.x; rv[r] = r4.y; bu[r] = b4.x; bv[r] = b4.y;
+      }
     }
     load(t + 2, B);
-    const float4 t4 = ring_s[m1 * NR + y];   // lane y-1 (any row group) at step t-1
-    const int x = t - y - 2 * s;
-    const float hl = x > 0 ? phr : 0.0f;
-    const float vt = has_top ? t4.z : 0.0f;
-    const float ur = x < w - 1 ? ru : 0.0f;
-    float nu, nv = 0.0f;
-    if (MODE == 0) {
-      const float vr = x < w - 1 ? rv : 0.0f;
-      const float s1 = sor_rhs(border, notop, b1, hr * ur, vt * t4.x, vv * bu);
-      const float s2 = sor_rhs(border, notop, b2, hr * vr, vt * t4.y, vv * bv);
-      const float B1 = x > 0 ? hl * pu + s1 : s1;
-      const float B2 = x > 0 ? hl * pv + s2 : s2;
-      nu = ou + omega * (i11 * B1 + i12 * B2 - ou);
-      nv = ov + omega * (i12 * B1 + i22 * B2 - ov);
-    } else {
-      float su = 0.0f, sd = 0.0f;
-      su = has_top ? su - vt * t4.x : su;     sd = has_top ? sd + vt : sd;
-      su = x > 0 ? su - hl * pu : su;         sd = x > 0 ? sd + hl : sd;
-      su = has_bot ? su - vv * bu : su;       sd = has_bot ? sd + vv : sd;
-      su = x < w - 1 ? su - hr * ur : su;     sd = x < w - 1 ? sd + hr : sd;
-      const float A = i11 + sd, Bv = b1 - su;
-      nu = (1.0f - omega) * ou + omega * (Bv / A);
+    const float4 t4 = ring_s[m1 * NR + y0];   // row y0 - 1 (previous lane / row group) at step t-1
+    float nu[R], nv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int y = y0 + r;
+      const bool has_top = y > 0, has_bot = y < h - 1, notop = !has_top, border = notop || !has_bot;
+      const int x = t - y - 2 * s;
+      // top neighbour (x, y-1) after this sweep, and its sv: the lane's own row r-1 of step t-1 for r > 0
+      const float tu = r == 0 ? t4.x : pu[r > 0 ? r - 1 : 0];
+      const float tv = r == 0 ? t4.y : pv[r > 0 ? r - 1 : 0];
+      const float tsv = r == 0 ? t4.z : pvv[r > 0 ? r - 1 : 0];
+      const float hl = x > 0 ? phr[r] : 0.0f;
+      const float vt = has_top ? tsv : 0.0f;
+      const float ur = x < w - 1 ? ru[r] : 0.0f;
+      nv[r] = 0.0f;
+      if (MODE == 0) {
+        const float vr = x < w - 1 ? rv[r] : 0.0f;
+        const float s1 = sor_rhs(border, notop, b1[r], hr[r] * ur, vt * tu, vv[r] * bu[r]);
+        const float s2 = sor_rhs(border, notop, b2[r], hr[r] * vr, vt * tv, vv[r] * bv[r]);
+        const float B1 = x > 0 ? hl * pu[r] + s1 : s1;
+        const float B2 = x > 0 ? hl * pv[r] + s2 : s2;
+        nu[r] = ou[r] + omega * (i11[r] * B1 + i12[r] * B2 - ou[r]);
+        nv[r] = ov[r] + omega * (i12[r] * B1 + i22[r] * B2 - ov[r]);
+      } else {
+        float su = 0.0f, sd = 0.0f;
+        su = has_top ? su - vt * tu : su;           sd = has_top ? sd + vt : sd;
+        su = x > 0 ? su - hl * pu[r] : su;          sd = x > 0 ? sd + hl : sd;
+        su = has_bot ? su - vv[r] * bu[r] : su;     sd = has_bot ? sd + vv[r] : sd;
+        su = x < w - 1 ? su - hr[r] * ur : su;      sd = x < w - 1 ? sd + hr[r] : sd;
+        const float A = i11[r] + sd, Bv = b1[r] - su;
+        nu[r] = (1.0f - omega) * ou[r] + omega * (Bv / A);
+      }
     }
-    ring_s[m0 * NR + y + 1] = make_float4(nu, nv, vv, 0.0f);
-    if (LAST) {
-      const unsigned o = y < h && x >= 0 && x < w ? (unsigned)((x + y) * h + y) : dump;
-      du[o] = nu;
-      if (MODE == 0) dv[o] = nv;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int y = y0 + r;
+      ring_s[m0 * NR + y + 1] = make_float4(nu[r], nv[r], vv[r], 0.0f);
+      if (LAST) {
+        const int x = t - y - 2 * s;
+        const unsigned o = y < h && x >= 0 && x < w ? (unsigned)((x + y) * h + y) : dump;
+        du[o] = nu[r];
+        if (MODE == 0) dv[o] = nv[r];
+      }
+      pu[r] = nu[r];
+      pv[r] = nv[r];
+      phr[r] = hr[r];
+      pvv[r] = vv[r];
     }
-    pu = nu;
-    pv = nv;
-    phr = hr;
     __syncthreads();
   }
 
   __device__ __forceinline__ void run(int T) {
-    pu = pv = phr = 0.0f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) pu[r] = pv[r] = phr[r] = pvv[r] = 0.0f;
     load(0, L[0]);
     load(1, L[1]);
     for (int t = 0; t < T; t += 2) {
@@ -1627,14 +1654,22 @@ struct SorWave {
   }
 };
 
-// One frame's SOR call by the whole workgroup (64 * ceil(h/64) * S threads); ring: S * 3 * NR float4 of LDS.
-template <int S, int MODE>
+// Rows per lane of the sweep-per-wave SOR.  One row per lane and more waves measured faster than 2 or 4
+// rows per lane and fewer waves (1080p op2: 0.76 vs 0.91 ms per step), so 1 is the default; `forced`
+// (option "sor_rows") selects 2 or 4 for A/B runs.
+__host__ __device__ __forceinline__ int sor_rows_per_lane(int h, int forced) {
+  (void)h;
+  return forced > 0 ? forced : 1;
+}
+
+// One frame's SOR call by the whole workgroup (64 * G * S threads, G = ceil(h / (64 R))); ring: S * 3 * NR
+// float4 of LDS.
+template <int S, int MODE, int R>
 __device__ __forceinline__ void sor_waves_frame(const TvArgs &a, int frame, float4 *ring) {
-  const int G = (a.h + 63) >> 6;
-  const int NR = G * 64 + 2;
+  const int G = (a.h + 64 * R - 1) / (64 * R);
+  const int NR = G * 64 * R + 2;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = wid / S, s = wid - g * S;
-  const int y = g * 64 + lane;
   // clear the rings: pads and not-yet-written slots are read only by lanes whose selects discard the
   // values, but they are kept finite and deterministic anyway
   for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) ring[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1647,31 +1682,27 @@ __device__ __forceinline__ void sor_waves_frame(const TvArgs &a, int frame, floa
     st.dv = a.dv + fo;
     st.ring_s = ring + s * 3 * NR;
     st.ring_p = ring + (s > 0 ? s - 1 : 0) * 3 * NR;
-    st.w = a.w; st.h = a.h; st.y = y; st.s = s; st.NR = NR;
+    st.w = a.w; st.h = a.h; st.y0 = (g * 64 + lane) * R; st.s = s; st.NR = NR;
     st.dump = (unsigned)((a.w + a.h - 1) * a.h + lane);
     st.omega = a.omega;
-    st.has_top = y > 0;
-    st.has_bot = y < a.h - 1;
-    st.notop = !st.has_top;
-    st.border = !st.has_top || !st.has_bot;
     st.run(T2);
   };
   if (s == 0) {
-    SorWave<S, MODE, true, S == 1> st;
+    SorWave<S, MODE, true, S == 1, R> st;
     setup(st);
   } else if (s == S - 1) {
-    SorWave<S, MODE, false, true> st;
+    SorWave<S, MODE, false, true, R> st;
     setup(st);
   } else {
-    SorWave<S, MODE, false, false> st;
+    SorWave<S, MODE, false, false, R> st;
     setup(st);
   }
 }
 
-template <int S, int MODE>
-__global__ __launch_bounds__(1024) void k_tv_sor_waves(TvArgs a) {
+template <int S, int MODE, int R, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tv_sor_waves(TvArgs a) {
   extern __shared__ float4 ring[];  // [S][3][NR]
-  sor_waves_frame<S, MODE>(a, blockIdx.x, ring);
+  sor_waves_frame<S, MODE, R>(a, blockIdx.x, ring);
 }
 
 __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
@@ -1722,7 +1753,7 @@ __global__ __launch_bounds__(MAXT) void k_tv_level(TvArgs a, int n_inner) {
     __syncthreads();
     for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP>(a, f, kk);
     __syncthreads();
-    sor_waves_frame<S, MODE>(a, f, ring);
+    sor_waves_frame<S, MODE, 1>(a, f, ring);
     __syncthreads();
   }
   for (int p = tid; p < w * h; p += nt) tv_final_px(a, p % w, p / w, f);
@@ -1987,20 +2018,36 @@ static void sor_pipe(const TvArgs &a, hipStream_t s) {
       k_tv_sor_pipe<S, 2, 1024><<<a.n, threads, 0, s>>>(a);
   }
 }
+// MAXT: 512 threads leave 256 registers a lane (R = 2, 4 need them); R = 1 also runs up to 1024 threads.
+template <int S, int R, int MAXT>
+static void sor_waves_r(const TvArgs &a, hipStream_t s) {
+  const int G = (a.h + 64 * R - 1) / (64 * R);
+  const size_t lds = sizeof(float4) * S * 3 * (G * 64 * R + 2);
+  if (a.nop == 2)
+    k_tv_sor_waves<S, 0, R, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+  else
+    k_tv_sor_waves<S, 2, R, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+}
 template <int S>
 static void sor_waves(const TvArgs &a, hipStream_t s) {
-  const int G = (a.h + 63) / 64;
-  const size_t lds = sizeof(float4) * S * 3 * (G * 64 + 2);
-  if (a.nop == 2)
-    k_tv_sor_waves<S, 0><<<a.n, 64 * G * S, lds, s>>>(a);
-  else
-    k_tv_sor_waves<S, 2><<<a.n, 64 * G * S, lds, s>>>(a);
+  switch (sor_rows_per_lane(a.h, a.sor_rows)) {
+    case 1:
+      if (64 * S * ((a.h + 63) / 64) <= 512)
+        sor_waves_r<S, 1, 512>(a, s);
+      else
+        sor_waves_r<S, 1, 1024>(a, s);
+      return;
+    case 2: sor_waves_r<S, 2, 512>(a, s); return;
+    default: sor_waves_r<S, 4, 512>(a, s); return;
+  }
 }
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
   const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2);
-  const int G = (a.h + 63) / 64;
-  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && G * a.solverit <= 16) {
+  const int R = sor_rows_per_lane(a.h, a.sor_rows), G = (a.h + 64 * R - 1) / (64 * R);
+  const size_t lds = sizeof(float4) * a.solverit * 3 * (G * 64 * R + 2);
+  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 &&
+      G * a.solverit <= (R == 1 ? 16 : 8) && (R == 1 || R == 2 || R == 4) && lds <= 160 * 1024) {
     switch (a.solverit) {
       case 2: sor_waves<2>(a, s); return;
       case 3: sor_waves<3>(a, s); return;

@@ -59,6 +59,7 @@ struct ofdis_context {
   int opt_sor_generic = 0;
   int opt_sor_pipe = 0;  // 1: force the single-wave-per-row-group register pipeline (A/B)
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
+  int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
@@ -356,6 +357,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.camlr = 0;
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
+      tv.sor_rows = c->opt_sor_rows;
       if (c->opt_tv_fused && tv_level_fusable(tv)) {
         timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
       } else {
@@ -690,6 +692,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   std::lock_guard<std::mutex> lock(c->mu);
   if (std::strcmp(key, "sor_generic") == 0) {
     c->opt_sor_generic = value != 0;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "sor_rows") == 0 && (value == 0 || value == 1 || value == 2 || value == 4)) {
+    c->opt_sor_rows = value;
     return OFDIS_OK;
   }
   if (std::strcmp(key, "wave_per_patch") == 0) {

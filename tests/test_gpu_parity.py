@@ -89,10 +89,12 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_pipe", 1, 0),        # one-wave register-pipeline SOR
     ("sor_generic", 1, 0),     # generic global-memory SOR
     ("wave_per_patch", 1, 0),  # one wave per DIS patch instead of eight lanes
+    ("sor_rows", 1, 0),        # sweep-per-wave SOR with one row per lane
+    ("sor_rows", 4, 0),        # ... four rows per lane
 ]
 
 
-@pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: v[0])
+@pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: f"{v[0]}={v[1]}")
 @pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in CASES if c[0] <= 200 or c[1] > 256])
 def test_kernel_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op, over):
     """Every kernel variant (TV / SOR / DIS patch) gives the same bits as the default path and the oracle."""
