@@ -107,7 +107,6 @@ int ofdis_params_validate(const ofdis_params *p, int width, int height, int imgp
   if (p->sc_l < 0 || p->sc_f < p->sc_l || p->sc_f > 16) return OFDIS_ERR_INVALID_ARGUMENT;
   if (p->sc_l > 8) return OFDIS_ERR_UNSUPPORTED;  // exact box-mean pyramid
   if (p->costfct < 0 || p->costfct > 2) return OFDIS_ERR_UNSUPPORTED;  // 10 (NCC) unimplemented upstream
-  if (p->usefbcon) return OFDIS_ERR_UNSUPPORTED;                          // next round
   if (p->max_iter < 0 || p->min_iter < 0 || p->tv_innerit < 0 || p->tv_solverit < 0)
     return OFDIS_ERR_INVALID_ARGUMENT;
   if (!(p->patove >= 0.0f && p->patove < 1.0f)) return OFDIS_ERR_INVALID_ARGUMENT;

@@ -61,6 +61,7 @@ struct PatchArgs {
 
 struct AggArgs {
   const float *p_iter, *pweight;
+  const float *cg_p_iter, *cg_pweight;  // complementary (backward) grid for usefbcon, or NULL
   float *flow;  // planar [n][nop][h][w]
   int n, nop, noc, p, novals, steps;
   LevelGeom g;

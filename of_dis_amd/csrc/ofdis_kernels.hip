@@ -663,7 +663,10 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
-__device__ __forceinline__ void aggregate_px(const AggArgs &a, int x, int y, int f) {
+// Own-grid part of AggregateFlowDense (patchgrid.cpp:213-275) for pixel (x, y): the sums of weights and
+// weighted displacements, in the serial order (ascending patch id).
+__device__ __forceinline__ void aggregate_own(const AggArgs &a, int x, int y, int f, float &we, float &f0,
+                                              float &f1) {
   const LevelGeom &g = a.g;
   const int hp = a.p / 2;
   // patches whose footprint [pt - p/2, pt + p/2 - 1] covers x, visited in ascending patch id
@@ -671,7 +674,6 @@ __device__ __forceinline__ void aggregate_px(const AggArgs &a, int x, int y, int
   const int pxhi = min(g.nopw - 1, floordiv(x + hp - g.offw, a.steps));
   const int pylo = max(0, -floordiv(-(y - hp + 1 - g.offh), a.steps));
   const int pyhi = min(g.noph - 1, floordiv(y + hp - g.offh, a.steps));
-  float we = 0.0f, f0 = 0.0f, f1 = 0.0f;
   const float *PI = a.p_iter + (long)f * g.npatch * a.nop;
   const float *PW = a.pweight + (long)f * g.npatch * a.novals;
   for (int px = pxlo; px <= pxhi; ++px) {
@@ -703,23 +705,117 @@ __device__ __forceinline__ void aggregate_px(const AggArgs &a, int x, int y, int
       if (a.nop == 2) f1 = f1 + PI[ip * a.nop + 1] * absw;
     }
   }
-  if (we > 0) {
-    f0 = f0 / we;
-    f1 = f1 / we;
+}
+
+// Forward-backward merging (usefbcon, patchgrid.cpp:277-375): the complementary grid's patch q, at its
+// optimised position pos, splats -displacement * bilinear weight over its footprint; pixel (x, y) receives
+// the taps cc, fc, cf, ff of the loop positions (x, y), (x+1, y), (x, y+1), (x+1, y+1) in that order (the
+// serial loop's order).  Positions with the target outside [1, w-1) x [1, h-1) are skipped; RGB keeps the
+// weight-pointer quirk with those bounds.
+struct CgPatch {
+  int pos0, pos1;
+  float wb[4];
+  float fl0, fl1;
+};
+__device__ __forceinline__ void aggregate_cg_one(const AggArgs &a, const CgPatch &q, const float *pw, int x,
+                                                 int y, float &we, float &f0, float &f1) {
+  const LevelGeom &g = a.g;
+  const int hp = a.p / 2;
+  for (int k = 0; k < 4; ++k) {
+    const int xt = x + (k & 1), yt = y + (k >> 1);
+    const int lx = xt - q.pos0 + hp, ly = yt - q.pos1 + hp;
+    if (lx < 0 || lx >= a.p || ly < 0 || ly >= a.p) continue;
+    if (!(xt >= 1 && yt >= 1 && xt < g.w - 1 && yt < g.h - 1)) continue;
+    float absw;
+    if (a.noc == 1) {
+      absw = 1.0f / stdmaxf(2.0f, pw[ly * a.p + lx]);
+    } else {
+      const int lx0 = max(0, 1 - q.pos0 + hp), lx1 = min(a.p, g.w - 1 - q.pos0 + hp);
+      const int ly0 = max(0, 1 - q.pos1 + hp), ly1 = min(a.p, g.h - 1 - q.pos1 + hp);
+      const int nin = max(0, lx1 - lx0);
+      int before_in = max(0, min(ly, ly1) - ly0) * nin;
+      if (ly >= ly0 && ly < ly1) before_in += max(0, min(lx, lx1) - lx0);
+      const int off = ly * a.p + lx + 2 * before_in;
+      absw = stdmaxf(2.0f, pw[off]);
+      absw = absw + stdmaxf(2.0f, pw[off + 1]);
+      absw = absw + stdmaxf(2.0f, pw[off + 2]);
+      absw = 1.0f / absw;
+    }
+    const float n0 = q.fl0 * absw, n1 = q.fl1 * absw;
+    we = we + q.wb[k] * absw;
+    f0 = f0 - q.wb[k] * n0;
+    if (a.nop == 2) f1 = f1 - q.wb[k] * n1;
   }
-  const long plane = (long)g.w * g.h;
-  float *fl = a.flow + (long)f * a.nop * plane + (long)y * g.w + x;
-  fl[0] = f0;
-  if (a.nop == 2) fl[plane] = f1;
 }
 
 // 64 x 16 pixel tiles: the patch weights of one patch row are then read by one workgroup (one XCD's L2).
+// With a complementary grid, its patches are staged through LDS 256 at a time (all of them, in id order:
+// an optimised position is arbitrary) and each pixel tests its reach.
 __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
+  __shared__ CgPatch cgs[256];
+  const LevelGeom &g = a.g;
   const int x = blockIdx.x * 64 + (threadIdx.x & 63), f = blockIdx.z;
-  if (x >= a.g.w) return;
-  for (int r = threadIdx.x >> 6; r < 16; r += 4) {
-    const int y = blockIdx.y * 16 + r;
-    if (y < a.g.h) aggregate_px(a, x, y, f);
+  float we[4], f0[4], f1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    we[r] = f0[r] = f1[r] = 0.0f;
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * r;
+    if (x < g.w && y < g.h) aggregate_own(a, x, y, f, we[r], f0[r], f1[r]);
+  }
+  if (a.cg_p_iter) {
+    const int hp = a.p / 2;
+    const int tx0 = blockIdx.x * 64, ty0 = blockIdx.y * 16;
+    const float *CPI = a.cg_p_iter + (long)f * g.npatch * a.nop;
+    const float *CPW = a.cg_pweight + (long)f * g.npatch * a.novals;
+    for (int c0 = 0; c0 < g.npatch; c0 += 256) {
+      const int q = c0 + threadIdx.x;
+      if (q < g.npatch) {
+        const int pxi = q / g.noph, pyi = q % g.noph;
+        const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+        CgPatch e;
+        e.fl0 = CPI[q * a.nop];
+        e.fl1 = a.nop == 2 ? CPI[q * a.nop + 1] : 0.0f;
+        const float rp0 = ptr0 + e.fl0, rp1 = a.nop == 2 ? ptr1 + e.fl1 : ptr1;  // GetPointPos (pt_iter)
+        e.pos0 = (int)ceil((double)rp0 + .00001);
+        e.pos1 = (int)ceil((double)rp1 + .00001);
+        const float r0 = rp0 - (float)(int)floorf(rp0), r1 = rp1 - (float)(int)floorf(rp1);
+        e.wb[0] = r0 * r1;
+        e.wb[1] = (1 - r0) * r1;
+        e.wb[2] = r0 * (1 - r1);
+        e.wb[3] = (1 - r0) * (1 - r1);
+        cgs[threadIdx.x] = e;
+      }
+      __syncthreads();
+      const int nq = min(256, g.npatch - c0);
+      for (int j = 0; j < nq; ++j) {
+        const CgPatch &e = cgs[j];
+        // reach of the patch: x in [pos0 - p/2 - 1, pos0 + p/2 - 1] (tile-level reject first)
+        if (e.pos0 - hp - 1 > tx0 + 63 || e.pos0 + hp - 1 < tx0 || e.pos1 - hp - 1 > ty0 + 15 || e.pos1 + hp - 1 < ty0)
+          continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int y = ty0 + (threadIdx.x >> 6) + 4 * r;
+          if (x < g.w && y < g.h && x >= e.pos0 - hp - 1 && x <= e.pos0 + hp - 1 && y >= e.pos1 - hp - 1 &&
+              y <= e.pos1 + hp - 1)
+            aggregate_cg_one(a, e, CPW + (long)(c0 + j) * a.novals, x, y, we[r], f0[r], f1[r]);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const long plane = (long)g.w * g.h;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * r;
+    if (x >= g.w || y >= g.h) continue;
+    float v0 = f0[r], v1 = f1[r];
+    if (we[r] > 0) {
+      v0 = v0 / we[r];
+      v1 = v1 / we[r];
+    }
+    float *fl = a.flow + (long)f * a.nop * plane + (long)y * g.w + x;
+    fl[0] = v0;
+    if (a.nop == 2) fl[plane] = v1;
   }
 }
 

@@ -31,8 +31,9 @@ struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
   int nop = 2, noc = 1, pad = 8, sc_f = 0, sc_l = 0;
   std::vector<LevelGeom> lv;                       // index s - sc_l
-  std::vector<size_t> off_lvl, off_img, off_dx, off_dy, off_flow;
-  size_t off_piter = 0, off_pw = 0, off_tv = 0, tv_plane = 0;
+  std::vector<size_t> off_lvl, off_img, off_dx, off_dy, off_flow, off_flow_bw;
+  size_t off_piter = 0, off_pw = 0, off_piter_bw = 0, off_pw_bw = 0, off_tv = 0, tv_plane = 0;
+  bool fb = false;  // usefbcon: backward grid, flow and refinement
   size_t total = 0;
 };
 
@@ -173,6 +174,8 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
   P.off_dx.resize(nsc);
   P.off_dy.resize(nsc);
   P.off_flow.resize(nsc);
+  P.off_flow_bw.resize(nsc);
+  P.fb = p->usefbcon != 0;
   size_t off = 0;
   const int novals = p->noc * p->p_samp_s * p->p_samp_s;
   size_t max_np = 0, max_plane = 0;
@@ -190,6 +193,8 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
     off = align_up(off + sizeof(float) * 2 * (size_t)n * g.W * g.H * P.noc);
     P.off_flow[i] = off;
     off = align_up(off + sizeof(float) * (size_t)n * P.nop * g.w * g.h);
+    P.off_flow_bw[i] = off;
+    if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * P.nop * g.w * g.h);
     if ((size_t)g.npatch > max_np) max_np = g.npatch;
     if ((size_t)g.w * g.h > max_plane) max_plane = (size_t)g.w * g.h;
   }
@@ -197,6 +202,10 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
   off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
   P.off_pw = off;
   off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
+  P.off_piter_bw = off;
+  if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
+  P.off_pw_bw = off;
+  if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
   P.off_tv = off;
   size_t max_sp = 0;  // skewed TV plane (w + h - 1) * h
   for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, ((size_t)(g.w + g.h - 1) * g.h + 64 + 3) / 4 * 4);
@@ -295,6 +304,21 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.wave_per_patch = c->opt_wave_per_patch;
     pa.g = g;
     timed(c, 3, s, [&] { launch_patch(pa, s); });
+    // usefbcon: the backward grid -- template on image b, target image a, right camera (camlr = 1),
+    // initialised from the coarser backward flow (oflow.cpp:158-169, 193-196, 209-211, 231-233)
+    PatchArgs pb = pa;
+    if (P.fb) {
+      pb.img_a = img + (size_t)n * fsp;
+      pb.dx_a = dxp + (size_t)n * fsp;
+      pb.dy_a = dyp + (size_t)n * fsp;
+      pb.img_b = img;
+      pb.prev = nullptr;
+      if (sl < p->sc_f) pb.prev = (const float *)(ws + P.off_flow_bw[i + 1]);
+      pb.p_iter = (float *)(ws + P.off_piter_bw);
+      pb.pweight = (float *)(ws + P.off_pw_bw);
+      pb.camlr = 1;
+      timed(c, 3, s, [&] { launch_patch(pb, s); });
+    }
 
     AggArgs ag{};
     ag.p_iter = pa.p_iter;
@@ -307,21 +331,35 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     ag.novals = novals;
     ag.steps = steps;
     ag.g = g;
+    ag.cg_p_iter = P.fb ? pb.p_iter : nullptr;
+    ag.cg_pweight = P.fb ? pb.pweight : nullptr;
     if (times) HIP_OK(hipEventRecord(ev[1], s));
     timed(c, 4, s, [&] { launch_aggregate(ag, s); });
+    float *flow_bw = (float *)(ws + P.off_flow_bw[i]);
+    const bool bw_level = P.fb && sl > p->sc_l;  // the backward flow is not needed after the last scale
+    if (bw_level) {                               // patchgrid.cpp:213-397 with the roles swapped
+      AggArgs ab = ag;
+      ab.p_iter = pb.p_iter;
+      ab.pweight = pb.pweight;
+      ab.cg_p_iter = pa.p_iter;
+      ab.cg_pweight = pa.pweight;
+      ab.flow = flow_bw;
+      timed(c, 4, s, [&] { launch_aggregate(ab, s); });
+    }
     if (times) HIP_OK(hipEventRecord(ev[2], s));
     int rc = capture(c, s, c->cap_dis, sl, P, flow);
     if (rc) return rc;
 
     const int n_inner = p->tv_innerit * (sl + 1);  // refine_variational.cpp:36
-    if (p->usetvref && n_inner > 0) {
+    for (int dir = 0; dir < (bw_level ? 2 : 1) && p->usetvref && n_inner > 0; ++dir) {
+      // dir 1: VarRefClass on the backward flow with the images swapped (oflow.cpp:312-316)
       const long sp = ((long)(g.w + g.h - 1) * g.h + 64 + 3) / 4 * 4;  // + SOR dump slots; 16-B multiple
       const size_t pl = (size_t)n * sp;
       float *t0 = (float *)(ws + P.off_tv);
       TvArgs tv{};
-      tv.img_a = img;
-      tv.img_b = img + (size_t)n * fsp;
-      tv.flow = flow;
+      tv.img_a = dir == 0 ? img : img + (size_t)n * fsp;
+      tv.img_b = dir == 0 ? img + (size_t)n * fsp : img;
+      tv.flow = dir == 0 ? flow : flow_bw;
       tv.du = t0;
       tv.dv = t0 + pl;
       tv.mask = t0 + 2 * pl;
@@ -354,7 +392,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.hdo3 = p->tv_delta * 0.5f / 3.0f;
       tv.omega = p->tv_sor;
       tv.solverit = p->tv_solverit;
-      tv.camlr = 0;
+      tv.camlr = dir;
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_rows = c->opt_sor_rows;
@@ -793,13 +831,14 @@ int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx,
                         const float *const *im_bo, const float *const *im_bo_dx, const float *const *im_bo_dy,
                         int imgpadding, float *outflow, const float *initflow, int width, int height,
                         const ofdis_params *p) {
-  (void)im_bo_dx;
-  (void)im_bo_dy;  // used upstream only by the backward grid of usefbcon (oflow.cpp:193-196)
   if (!im_ao || !im_ao_dx || !im_ao_dy || !im_bo || !outflow) return OFDIS_ERR_INVALID_ARGUMENT;
   int rc = ofdis_params_validate(p, width, height, imgpadding);
   if (rc) return rc;
-  for (int s = p->sc_l; s <= p->sc_f; ++s)
+  for (int s = p->sc_l; s <= p->sc_f; ++s) {
     if (!im_ao[s] || !im_ao_dx[s] || !im_ao_dy[s] || !im_bo[s]) return OFDIS_ERR_INVALID_ARGUMENT;
+    // image b's gradients are read only by the backward grid of usefbcon (oflow.cpp:193-196)
+    if (p->usefbcon && (!im_bo_dx || !im_bo_dy || !im_bo_dx[s] || !im_bo_dy[s])) return OFDIS_ERR_INVALID_ARGUMENT;
+  }
   static std::mutex gmu;
   static ofdis_context *gctx = nullptr;
   std::lock_guard<std::mutex> glock(gmu);
@@ -823,6 +862,10 @@ int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx,
     HIP_OK(hipMemcpyAsync(img + fb, im_bo[sl], fb, hipMemcpyHostToDevice, s));
     HIP_OK(hipMemcpyAsync(c->ws + P.off_dx[sl - p->sc_l], im_ao_dx[sl], fb, hipMemcpyHostToDevice, s));
     HIP_OK(hipMemcpyAsync(c->ws + P.off_dy[sl - p->sc_l], im_ao_dy[sl], fb, hipMemcpyHostToDevice, s));
+    if (p->usefbcon) {
+      HIP_OK(hipMemcpyAsync(c->ws + P.off_dx[sl - p->sc_l] + fb, im_bo_dx[sl], fb, hipMemcpyHostToDevice, s));
+      HIP_OK(hipMemcpyAsync(c->ws + P.off_dy[sl - p->sc_l] + fb, im_bo_dy[sl], fb, hipMemcpyHostToDevice, s));
+    }
   }
   float *dinit = nullptr;
   if (initflow) {

@@ -448,9 +448,11 @@ static void grid_geometry(const cam_t *c, const opt_t *o, grid_t *g) {
   g->nopatches = g->nopw * g->noph;
 }
 
-/* AggregateFlowDense, forward grid only (patchgrid.cpp:213-275, 377-397).
- * params[ip*nop + k], pweight[ip*novals + i]. */
-static void aggregate(const cam_t *c, const opt_t *o, const grid_t *g, const patch_t *pats, float *flowout) {
+/* AggregateFlowDense (patchgrid.cpp:213-397): the grid's own patches, then -- forward-backward merging,
+ * usefbcon -- the complementary grid's patches splatted bilinearly at their optimised position with the
+ * NEGATED displacement (:277-375), then normalisation.  params[ip*nop + k], pweight[ip*novals + i]. */
+static void aggregate(const cam_t *c, const opt_t *o, const grid_t *g, const patch_t *pats, const patch_t *cg,
+                      float *flowout) {
   const int w = c->w, h = c->h, nop = o->nop, p = o->p;
   float *we = (float *)calloc((size_t)w * h, sizeof(float));
   memset(flowout, 0, sizeof(float) * (size_t)w * h * nop);
@@ -476,6 +478,38 @@ static void aggregate(const cam_t *c, const opt_t *o, const grid_t *g, const pat
           for (int k = 0; k < nop; ++k) flowout[nop * i + k] = flowout[nop * i + k] + P->p_iter[k] * absw;
         }
       }
+  }
+  if (cg) {
+    for (int ip = 0; ip < g->nopatches; ++ip) { /* both grids have the same geometry (oflow.cpp:155-164) */
+      const patch_t *P = &cg[ip];
+      const float *pw = P->pweight;
+      const float rp0 = P->pt_iter[0], rp1 = P->pt_iter[1]; /* GetPointPos: position after optimisation */
+      const int pos0 = (int)ceil((double)rp0 + .00001), pos1 = (int)ceil((double)rp1 + .00001);
+      const int pos2 = (int)floorf(rp0), pos3 = (int)floorf(rp1);
+      const float r0 = rp0 - (float)pos2, r1 = rp1 - (float)pos3;
+      const float wb[4] = {r0 * r1, (1 - r0) * r1, r0 * (1 - r1), (1 - r0) * (1 - r1)};
+      for (int y = -p / 2; y <= p / 2 - 1; ++y)
+        for (int x = -p / 2; x <= p / 2 - 1; ++x, ++pw) {
+          int yt = y + pos1, xt = x + pos0;
+          if (xt >= 1 && yt >= 1 && xt < w - 1 && yt < h - 1) {
+            float absw;
+            if (o->noc == 1) {
+              absw = 1.0f / stdmaxf(2.0f, *pw);
+            } else {
+              absw = stdmaxf(2.0f, *pw); ++pw;
+              absw = absw + stdmaxf(2.0f, *pw); ++pw;
+              absw = absw + stdmaxf(2.0f, *pw);
+              absw = 1.0f / absw;
+            }
+            float fl[2];
+            for (int k = 0; k < nop; ++k) fl[k] = P->p_iter[k] * absw;
+            const int idx[4] = {xt + yt * w, (xt - 1) + yt * w, xt + (yt - 1) * w, (xt - 1) + (yt - 1) * w};
+            for (int q = 0; q < 4; ++q) we[idx[q]] = we[idx[q]] + wb[q] * absw;
+            for (int q = 0; q < 4; ++q)
+              for (int k = 0; k < nop; ++k) flowout[nop * idx[q] + k] = flowout[nop * idx[q] + k] - wb[q] * fl[k];
+          }
+        }
+    }
   }
   for (int i = 0; i < w * h; ++i)
     if (we[i] > 0)
@@ -1037,58 +1071,84 @@ static void fill_cam(const ofdis_params *p, int width, int height, int imgpaddin
   c->camlr = 0;
 }
 
+/* One patch grid of a scale (PatGridClass: InitializeGrid, SetTargetImage, InitializeFromCoarserOF,
+ * Optimize; patchgrid.cpp:31-211).  prev: coarser flow of this grid's direction, or NULL. */
+static patch_t *run_grid(const cam_t *c, const opt_t *o, const grid_t *g, const float *im_a, const float *im_a_dx,
+                         const float *im_a_dy, const float *im_b, const float *prev, float **store_out) {
+  patch_t *pats = (patch_t *)calloc(g->nopatches, sizeof(patch_t));
+  float *store = (float *)malloc(sizeof(float) * (size_t)g->nopatches * o->novals * 5);
+  for (int x = 0, i = 0; x < g->nopw; ++x)
+    for (int y = 0; y < g->noph; ++y, ++i) {
+      pats[i].pt_ref[0] = (float)(x * g->steps + g->offw);
+      pats[i].pt_ref[1] = (float)(y * g->steps + g->offh);
+      float *s = store + (size_t)i * o->novals * 5;
+      pats[i].tmp = s; pats[i].dxx = s + o->novals; pats[i].dyy = s + 2 * o->novals;
+      pats[i].pdiff = s + 3 * o->novals; pats[i].pweight = s + 4 * o->novals;
+    }
+  for (int i = 0; i < g->nopatches; ++i) {
+    float pin[2] = {0.0f, 0.0f};
+    if (prev) {
+      int x = (int)floorf(pats[i].pt_ref[0] / 2), y = (int)floorf(pats[i].pt_ref[1] / 2);
+      int k = y * (c->w / 2) + x;
+      for (int d = 0; d < o->nop; ++d) pin[d] = prev[o->nop * k + d] * 2;
+    }
+    patch_run(c, o, im_a, im_a_dx, im_a_dy, im_b, pin, &pats[i]);
+  }
+  *store_out = store;
+  return pats;
+}
+
 int ofo_oflow(const float *const *im_ao, const float *const *im_ao_dx, const float *const *im_ao_dy,
               const float *const *im_bo, const float *const *im_bo_dx, const float *const *im_bo_dy,
               int imgpadding, float *outflow, const float *initflow, int width, int height,
               const ofdis_params *p, float *const *cap_dis, float *const *cap_tv) {
-  (void)im_bo_dx; (void)im_bo_dy;
-  if (p->usefbcon) return OFDIS_ERR_UNSUPPORTED;
   if (p->costfct < 0 || p->costfct > 2) return OFDIS_ERR_UNSUPPORTED;
+  const int fb = p->usefbcon != 0;
   opt_t o;
   fill_opt(p, &o);
   const int nsc = p->sc_f - p->sc_l + 1;
   float **flows = (float **)calloc(nsc, sizeof(float *));
+  float **flows_bw = (float **)calloc(nsc, sizeof(float *));
   int rc = 0;
   for (int sl = p->sc_f; sl >= p->sc_l; --sl) {
     const int ii = sl - p->sc_l;
-    cam_t c;
+    cam_t c, cr;
     fill_cam(p, width, height, imgpadding, sl, &c);
+    cr = c;
+    cr.camlr = 1; /* cpr: the right camera of the backward grid (oflow.cpp:155-157) */
     grid_t g;
     grid_geometry(&c, &o, &g);
-    flows[ii] = (float *)malloc(sizeof(float) * (size_t)c.w * c.h * o.nop);
-    patch_t *pats = (patch_t *)calloc(g.nopatches, sizeof(patch_t));
-    float *store = (float *)malloc(sizeof(float) * (size_t)g.nopatches * o.novals * 5);
-    for (int x = 0, i = 0; x < g.nopw; ++x)
-      for (int y = 0; y < g.noph; ++y, ++i) {
-        pats[i].pt_ref[0] = (float)(x * g.steps + g.offw);
-        pats[i].pt_ref[1] = (float)(y * g.steps + g.offh);
-        float *s = store + (size_t)i * o.novals * 5;
-        pats[i].tmp = s; pats[i].dxx = s + o.novals; pats[i].dyy = s + 2 * o.novals;
-        pats[i].pdiff = s + 3 * o.novals; pats[i].pweight = s + 4 * o.novals;
-      }
+    const size_t fsz = sizeof(float) * (size_t)c.w * c.h * o.nop;
+    flows[ii] = (float *)malloc(fsz);
+    if (fb) flows_bw[ii] = (float *)malloc(fsz);
     /* InitializeFromCoarserOF (patchgrid.cpp:195-211) or zero / initflow (oflow.cpp:206-217) */
-    const float *prev = (sl < p->sc_f) ? flows[ii + 1] : initflow;
-    for (int i = 0; i < g.nopatches; ++i) {
-      float pin[2] = {0.0f, 0.0f};
-      if (prev) {
-        int x = (int)floorf(pats[i].pt_ref[0] / 2), y = (int)floorf(pats[i].pt_ref[1] / 2);
-        int k = y * (c.w / 2) + x;
-        for (int d = 0; d < o.nop; ++d) pin[d] = prev[o.nop * k + d] * 2;
-      }
-      patch_run(&c, &o, im_ao[sl], im_ao_dx[sl], im_ao_dy[sl], im_bo[sl], pin, &pats[i]);
-    }
+    float *store = NULL, *store_bw = NULL;
+    patch_t *pats = run_grid(&c, &o, &g, im_ao[sl], im_ao_dx[sl], im_ao_dy[sl], im_bo[sl],
+                             (sl < p->sc_f) ? flows[ii + 1] : initflow, &store);
+    patch_t *pats_bw = NULL;
+    if (fb) /* grid_bw: template on image b, target image a, initialised from the coarser backward flow */
+      pats_bw = run_grid(&cr, &o, &g, im_bo[sl], im_bo_dx[sl], im_bo_dy[sl], im_ao[sl],
+                         (sl < p->sc_f) ? flows_bw[ii + 1] : NULL, &store_bw);
     float *dst = (sl == p->sc_l) ? outflow : flows[ii];
-    aggregate(&c, &o, &g, pats, dst);
-    if (cap_dis && cap_dis[sl]) memcpy(cap_dis[sl], dst, sizeof(float) * (size_t)c.w * c.h * o.nop);
-    if (p->usetvref) rc = var_refine(&c, &o, p, im_ao[sl], im_bo[sl], dst);
-    if (cap_tv && cap_tv[sl]) memcpy(cap_tv[sl], dst, sizeof(float) * (size_t)c.w * c.h * o.nop);
-    if (sl == p->sc_l && dst != flows[ii]) memcpy(flows[ii], dst, sizeof(float) * (size_t)c.w * c.h * o.nop);
-    free(store);
-    free(pats);
+    aggregate(&c, &o, &g, pats, pats_bw, dst);
+    if (fb && sl > p->sc_l) aggregate(&cr, &o, &g, pats_bw, pats, flows_bw[ii]); /* oflow.cpp:265-266 */
+    if (cap_dis && cap_dis[sl]) memcpy(cap_dis[sl], dst, fsz);
+    if (p->usetvref) {
+      rc = var_refine(&c, &o, p, im_ao[sl], im_bo[sl], dst);
+      if (!rc && fb && sl > p->sc_l) rc = var_refine(&cr, &o, p, im_bo[sl], im_ao[sl], flows_bw[ii]);
+    }
+    if (cap_tv && cap_tv[sl]) memcpy(cap_tv[sl], dst, fsz);
+    if (sl == p->sc_l && dst != flows[ii]) memcpy(flows[ii], dst, fsz);
+    free(store); free(pats);
+    free(store_bw); free(pats_bw);
     if (rc) break;
   }
-  for (int i = 0; i < nsc; ++i) free(flows[i]);
+  for (int i = 0; i < nsc; ++i) {
+    free(flows[i]);
+    free(flows_bw[i]);
+  }
   free(flows);
+  free(flows_bw);
   return rc;
 }
 

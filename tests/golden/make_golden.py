@@ -89,11 +89,12 @@ def make_sor():
 def pipe_cases():
     """(w, h, noc, mode, oppoint, overrides) -- small whole-pipeline regression vectors."""
     return [(160, 120, 1, 1, 2, {}), (173, 97, 1, 1, 2, {}), (96, 64, 3, 1, 3, {"costfct": 1}),
-            (120, 64, 1, 2, 4, {})]
+            (120, 64, 1, 2, 4, {}), (128, 96, 1, 1, 2, {"usefbcon": 1})]
 
 
-def pipe_name(w, h, noc, mode, op):
-    return os.path.join(HERE, f"pipe_m{mode}_c{noc}_op{op}_{w}x{h}.npz")
+def pipe_name(w, h, noc, mode, op, over=None):
+    fb = "_fb" if (over or {}).get("usefbcon") else ""
+    return os.path.join(HERE, f"pipe_m{mode}_c{noc}_op{op}_{w}x{h}{fb}.npz")
 
 
 def make_pipe(w, h, noc, mode, op, over):
@@ -103,7 +104,7 @@ def make_pipe(w, h, noc, mode, op, over):
     for k, v in over.items():
         setattr(q, k, v)
     out = O.run_u8(a, b, q)
-    np.savez_compressed(pipe_name(w, h, noc, mode, op), a=a, b=b, out=out, mode=mode, noc=noc, oppoint=op,
+    np.savez_compressed(pipe_name(w, h, noc, mode, op, over), a=a, b=b, out=out, mode=mode, noc=noc, oppoint=op,
                         overrides=json.dumps(over))
 
 

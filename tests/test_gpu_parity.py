@@ -51,6 +51,10 @@ CASES = [
     (160, 120, 1, 1, 2, {"patnorm": 0, "tv_innerit": 2, "tv_solverit": 4, "tv_sor": 1.3}),
     (240, 120, 1, 2, 4, {"max_iter": 16, "min_iter": 16}),    # depth from stereo, op4
     (240, 120, 3, 2, 2, {}),                                  # RGB depth
+    (160, 120, 1, 1, 2, {"usefbcon": 1}),                     # forward-backward merging (patchgrid.cpp:277-375)
+    (200, 150, 1, 1, 1, {"usefbcon": 1}),                     # ... without TV refinement
+    (192, 128, 3, 1, 3, {"usefbcon": 1, "costfct": 1}),       # ... RGB (weight-pointer quirk, bounds [1, w-1))
+    (240, 120, 1, 2, 4, {"usefbcon": 1, "max_iter": 16, "min_iter": 16}),  # ... depth (right camera clamp)
     (400, 300, 1, 1, 2, {"sc_l": 0, "sc_f": 2}),              # 300 rows: 5 row groups x 3 sweep waves
     (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows: register pipeline, 1024 threads
 ]
@@ -141,13 +145,15 @@ def test_ofclass_host_api_bitexact(oracle, od):
             lists.append(lst)
     rng = np.random.default_rng(0)
     init = (rng.standard_normal(((h >> (q.sc_f + 1)), (w >> (q.sc_f + 1)), 2)) * 0.5).astype(np.float32)
-    for initflow in (None, init):
+    for initflow, fb in ((None, 0), (init, 0), (init, 1)):
         out = np.zeros((h >> q.sc_l) * (w >> q.sc_l) * 2, np.float32)
         od.OFClass(*lists, 8, out, initflow, w, h, q.sc_f, q.sc_l, q.max_iter, q.min_iter, q.dp_thresh,
-                   q.dr_thresh, q.res_thresh, q.p_samp_s, q.patove, False, q.costfct, 1, q.patnorm, True,
+                   q.dr_thresh, q.res_thresh, q.p_samp_s, q.patove, bool(fb), q.costfct, 1, q.patnorm, True,
                    q.tv_alpha, q.tv_gamma, q.tv_delta, q.tv_innerit, q.tv_solverit, q.tv_sor, 0)
+        q.usefbcon = fb
         want = O.oflow(pa, pb, w, h, q, 8, initflow=initflow)
-        assert_bitexact(out.reshape(want.shape), want, f"OFClass initflow={initflow is not None}")
+        q.usefbcon = 0
+        assert_bitexact(out.reshape(want.shape), want, f"OFClass initflow={initflow is not None} usefbcon={fb}")
 
 
 def test_batch_equals_singles(od, ctx):

@@ -102,7 +102,6 @@ def test_params_from_strings_matches_readme_order():
     ({"p_samp_s": 22}, _lib.ERR_UNSUPPORTED),          # > 448 values per patch
     ({"sc_l": 7}, _lib.ERR_INVALID_ARGUMENT),          # sc_l > sc_f
     ({"costfct": 10}, _lib.ERR_UNSUPPORTED),           # NCC: unimplemented upstream too
-    ({"usefbcon": 1}, _lib.ERR_UNSUPPORTED),
     ({"patove": 1.0}, _lib.ERR_INVALID_ARGUMENT),
     ({"mode": 3}, _lib.ERR_INVALID_ARGUMENT),
     ({"noc": 2}, _lib.ERR_INVALID_ARGUMENT),
@@ -115,6 +114,7 @@ def test_validation_rejects(change, code):
 def test_validation_geometry():
     p = od.oppoint(2, 1920)
     assert od.validate(p, 1920, 1088, 8) == 0
+    assert od.validate(p.copy(usefbcon=1), 1920, 1088, 8) == 0  # forward-backward merging is supported
     assert od.validate(p, 1920, 1080, 8) == _lib.ERR_INVALID_ARGUMENT  # not divisible by 2^6
     assert od.validate(p, 1920, 1088, 4) == _lib.ERR_INVALID_ARGUMENT  # imgpadding < p
     rgb = od.oppoint(3, 1920, od.MODE_OF, 3)
