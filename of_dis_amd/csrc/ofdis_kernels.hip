@@ -1141,13 +1141,6 @@ __device__ __forceinline__ void data_de(int noc, long plane, float u, float m, c
 }
 
 // uu / vv of the current inner iteration (refine_variational.cpp:189-190,209-222,305-320)
-template <int NOP>
-__device__ __forceinline__ float uu_at(const TvArgs &a, long fk, bool first) {
-  const float wx = a.wxs[fk];
-  if (first) return wx;
-  if (NOP == 2) return wx + a.du[fk];
-  return a.camlr == 0 ? ssemin(wx + a.du[fk], 0.0f) : ssemax(wx + a.du[fk], 0.0f);
-}
 
 // compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
 template <int NOP>
@@ -1158,15 +1151,36 @@ __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, b
   const int w = a.w, h = a.h;
   const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h);
   const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h);
-  const float uc = uu_at<NOP>(a, idx, first);
-  const float ux = kK3[0] * uu_at<NOP>(a, kl, first) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kr, first));
-  const float uy = kK3[0] * uu_at<NOP>(a, ku, first) + (kK3[1] * uc + kK3[2] * uu_at<NOP>(a, kd, first));
+  const long k5[5] = {idx, kl, kr, ku, kd};
+  // gather everything first (one memory round trip), then uu = wx (first iteration) or wx + du
+  float wx5[5], du5[5], wy5[5], dv5[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    wx5[i] = a.wxs[k5[i]];
+    du5[i] = a.du[k5[i]];
+    if (NOP == 2) {
+      wy5[i] = a.wys[k5[i]];
+      dv5[i] = a.dv[k5[i]];
+    }
+  }
+  float uu5[5], vv5[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    if (NOP == 2) {
+      uu5[i] = first ? wx5[i] : wx5[i] + du5[i];
+      vv5[i] = first ? wy5[i] : wy5[i] + dv5[i];
+    } else {
+      uu5[i] = first ? wx5[i] : (a.camlr == 0 ? ssemin(wx5[i] + du5[i], 0.0f) : ssemax(wx5[i] + du5[i], 0.0f));
+    }
+  }
+  const float uc = uu5[0];
+  const float ux = kK3[0] * uu5[1] + (kK3[1] * uc + kK3[2] * uu5[2]);
+  const float uy = kK3[0] * uu5[3] + (kK3[1] * uc + kK3[2] * uu5[4]);
   float vx, vy;
   if (NOP == 2) {
-    auto vv = [&](long k) { return first ? a.wys[k] : a.wys[k] + a.dv[k]; };
-    const float vc = vv(idx);
-    vx = kK3[0] * vv(kl) + (kK3[1] * vc + kK3[2] * vv(kr));
-    vy = kK3[0] * vv(ku) + (kK3[1] * vc + kK3[2] * vv(kd));
+    const float vc = vv5[0];
+    vx = kK3[0] * vv5[1] + (kK3[1] * vc + kK3[2] * vv5[2]);
+    vy = kK3[0] * vv5[3] + (kK3[1] * vc + kK3[2] * vv5[4]);
   } else {  // wy_dummy = 0 (refine_variational.cpp:268,294)
     vx = kK3[0] * 0.0f + (kK3[1] * 0.0f + kK3[2] * 0.0f);
     vy = vx;
@@ -1177,54 +1191,61 @@ __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, b
 
 // One TV inner iteration's system (refine_variational.cpp:195-199): diffusivities from s
 // (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
-template <int NOP>
+// All of a pixel's inputs are gathered first with unconditional loads (border neighbours clamped to the
+// pixel itself and discarded by selects afterwards): one memory round trip per pixel instead of one per
+// data-dependent branch.  Same arithmetic, same order as before.
+template <int NOP, int NOC>
 __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
   const long idx = fr * a.sp + kk;
   int x, y;
   if (!skew_xy(kk, a.w, a.h, x, y)) return;
   const int w = a.w, h = a.h;
-  const float *S = a.s;
-  const float sc = S[idx];
-  const float shv = x < w - 1 ? sc + S[idx + h] : 0.0f;        // h[x] = s[x] + s[x+1]
-  const float svv = y < h - 1 ? sc + S[idx + h + 1] : 0.0f;    // v[y] = s[y] + s[y+1]
-  const long q = fr * a.noc * a.sp + kk;
-  const float m = a.mask[idx];
+  const bool hasl = x >= 1, hasr = x <= w - 2, hasu = y >= 1, hasd = y <= h - 2;
+  const long il = hasl ? idx - h : idx, ir = hasr ? idx + h : idx;
+  const long iu = hasu ? idx - h - 1 : idx, id = hasd ? idx + h + 1 : idx;
+  // ---- gather
+  const float *S = a.s, *WX = a.wxs, *WY = a.wys;
+  const float sc = S[idx], sl = S[il], sr = S[ir], su = S[iu], sd = S[id];
+  const float xc = WX[idx], xl = WX[il], xr = WX[ir], xu = WX[iu], xd = WX[id];
+  float yc = 0.0f, yl = 0.0f, yr = 0.0f, yu = 0.0f, yd = 0.0f;
+  if (NOP == 2) {
+    yc = WY[idx]; yl = WY[il]; yr = WY[ir]; yu = WY[iu]; yd = WY[id];
+  }
+  const float m = a.mask[idx], u = a.du[idx], v = NOP == 2 ? a.dv[idx] : 0.0f;
+  const long q = fr * NOC * a.sp + kk;
+  float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
+#pragma unroll
+  for (int c = 0; c < NOC; ++c) {
+    const long o = q + c * a.sp;
+    lIx[c] = a.Ix[o]; lIy[c] = a.Iy[o]; lIz[c] = a.Iz[o]; lIxx[c] = a.Ixx[o];
+    lIxy[c] = a.Ixy[o]; lIyy[c] = a.Iyy[o]; lIxz[c] = a.Ixz[o]; lIyz[c] = a.Iyz[o];
+  }
+  // ---- compute
+  const float shv = x < w - 1 ? sc + sr : 0.0f;  // h[x] = s[x] + s[x+1]
+  const float svv = y < h - 1 ? sc + sd : 0.0f;  // v[y] = s[y] + s[y+1]
   float A11, A12 = 0.0f, A22 = 0.0f, B1, B2 = 0.0f;
   if (NOP == 2)
-    data_of(a.noc, a.sp, a.du[idx], a.dv[idx], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q, a.Iyy + q,
-            a.Ixz + q, a.Iyz + q, a.hdo3, a.hgo3, A11, A12, A22, B1, B2);
+    data_of(NOC, 1, u, v, m, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz, lIyz, a.hdo3, a.hgo3, A11, A12, A22, B1, B2);
   else
-    data_de(a.noc, a.sp, a.du[idx], m, a.Ix + q, a.Iy + q, a.Iz + q, a.Ixx + q, a.Ixy + q, a.Iyy + q, a.Ixz + q,
-            a.Iyz + q, a.hdo3, a.hgo3, A11, B1);
+    data_de(NOC, 1, u, m, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz, lIyz, a.hdo3, a.hgo3, A11, B1);
   // b = ((((b - th[x-1]) + th[x]) - tv[y-1]) + tv[y]) with th[x] = h[x] (wx[x+1] - wx[x]) etc.
-  {
-    const float *WX = a.wxs;
-    const float c0 = WX[idx];
-    if (x >= 1) B1 = B1 - (S[idx - h] + sc) * (c0 - WX[idx - h]);
-    if (x <= w - 2) B1 = B1 + shv * (WX[idx + h] - c0);
-    if (y >= 1) B1 = B1 - (S[idx - h - 1] + sc) * (c0 - WX[idx - h - 1]);
-    if (y <= h - 2) B1 = B1 + svv * (WX[idx + h + 1] - c0);
-  }
+  B1 = hasl ? B1 - (sl + sc) * (xc - xl) : B1;
+  B1 = hasr ? B1 + shv * (xr - xc) : B1;
+  B1 = hasu ? B1 - (su + sc) * (xc - xu) : B1;
+  B1 = hasd ? B1 + svv * (xd - xc) : B1;
   if (NOP == 2) {
-    const float *WY = a.wys;
-    const float c0 = WY[idx];
-    if (x >= 1) B2 = B2 - (S[idx - h] + sc) * (c0 - WY[idx - h]);
-    if (x <= w - 2) B2 = B2 + shv * (WY[idx + h] - c0);
-    if (y >= 1) B2 = B2 - (S[idx - h - 1] + sc) * (c0 - WY[idx - h - 1]);
-    if (y <= h - 2) B2 = B2 + svv * (WY[idx + h + 1] - c0);
+    B2 = hasl ? B2 - (sl + sc) * (yc - yl) : B2;
+    B2 = hasr ? B2 + shv * (yr - yc) : B2;
+    B2 = hasu ? B2 - (su + sc) * (yc - yu) : B2;
+    B2 = hasd ? B2 + svv * (yd - yc) : B2;
     // sor_coupled's first sweep replaces a11/a12/a22 by the inverse of [[a11+d, a12], [a12, a22+d]] with
     // d = the sum of the four diffusivities (solver.c:122-128, border forms :131-190).  It depends on the
     // system only, so it is computed here, fully parallel, with the same expressions; every SOR sweep then
     // reads the inverse.  (w < 2 or h < 2 run the point-SOR fallback on the raw matrix, solver.c:34-78.)
     if (w >= 2 && h >= 2) {
-      const float hl = x > 0 ? S[idx - h] + sc : 0.0f;            // h[x-1]
-      float dpsis;
-      if (y == 0) {
-        dpsis = hl + (shv + svv);
-      } else {
-        const float vt = S[idx - h - 1] + sc;                       // v[y-1]
-        dpsis = y < h - 1 ? (hl + shv) + (vt + svv) : hl + (shv + vt);
-      }
+      const float hl = x > 0 ? sl + sc : 0.0f;  // h[x-1]
+      const float vt = su + sc;                  // v[y-1] (y > 0)
+      const float dpsis = y == 0 ? hl + (shv + svv) : (y < h - 1 ? (hl + shv) + (vt + svv) : hl + (shv + vt));
       const float M11 = A22 + dpsis, M22 = A11 + dpsis;
       const float det = M11 * M22 - A12 * A12;
       A11 = M11 / det;
@@ -1244,10 +1265,10 @@ __global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
   const int kk = blockIdx.x * blockDim.x + threadIdx.x;
   if (kk < a.sp) tv_smooth_px<NOP>(a, blockIdx.y, kk, a.first_iter != 0);
 }
-template <int NOP>
+template <int NOP, int NOC>
 __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
   const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk < a.sp) tv_system_px<NOP>(a, blockIdx.y, kk);
+  if (kk < a.sp) tv_system_px<NOP, NOC>(a, blockIdx.y, kk);
 }
 
 // Generic exact-order SOR (any size / sweep count): one workgroup per frame, in-place skewed arrays in
@@ -1847,7 +1868,10 @@ __global__ __launch_bounds__(MAXT) void k_tv_level(TvArgs a, int n_inner) {
   for (int it = 0; it < n_inner; ++it) {
     for (int kk = tid; kk < sp; kk += nt) tv_smooth_px<NOP>(a, f, kk, it == 0);
     __syncthreads();
-    for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP>(a, f, kk);
+    if (a.noc == 1)
+      for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP, 1>(a, f, kk);
+    else
+      for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP, 3>(a, f, kk);
     __syncthreads();
     sor_waves_frame<S, MODE, 1>(a, f, ring);
     __syncthreads();
@@ -2089,10 +2113,18 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
     k_tv_smooth<1><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
 }
 void launch_tv_system(const TvArgs &a, hipStream_t s) {
-  if (a.nop == 2)
-    k_tv_system<2><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
-  else
-    k_tv_system<1><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
+  const dim3 grid(ceil_div(a.sp, 256), a.n);
+  if (a.nop == 2) {
+    if (a.noc == 1)
+      k_tv_system<2, 1><<<grid, 256, 0, s>>>(a);
+    else
+      k_tv_system<2, 3><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (a.noc == 1)
+      k_tv_system<1, 1><<<grid, 256, 0, s>>>(a);
+    else
+      k_tv_system<1, 3><<<grid, 256, 0, s>>>(a);
+  }
 }
 template <int S>
 static void sor_pipe(const TvArgs &a, hipStream_t s) {

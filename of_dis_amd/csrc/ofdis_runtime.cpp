@@ -59,6 +59,13 @@ struct ofdis_context {
   std::map<int, std::pair<double, long>> acc;
   int opt_sor_generic = 0;
   int opt_sor_pipe = 0;  // 1: force the single-wave-per-row-group register pipeline (A/B)
+  int opt_graph = 1;           // replay the whole batch as one HIP graph (captured once per shape / pointers)
+  struct GraphKey {
+    const void *a = nullptr, *b = nullptr, *out = nullptr, *ws = nullptr;
+    int n = 0, w = 0, h = 0;
+    ofdis_params p{};
+  } gkey;
+  hipGraphExec_t gexec = nullptr;
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
   int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
@@ -543,6 +550,11 @@ int ofdis_context_create(int device, ofdis_context **out) {
 void ofdis_context_destroy(ofdis_context *c) {
   if (!c) return;
   hipSetDevice(c->device);
+  if (c->gexec) {  // it may still run on a caller stream
+    hipDeviceSynchronize();
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
   if (c->stream) hipStreamSynchronize(c->stream);
   drain_timing(c);
   for (auto e : c->pool) hipEventDestroy(e);
@@ -623,7 +635,39 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
   if (c->opt_streams <= 1 || nchunks <= 1 || capturing) {
     rc = ensure_ws(c, P.total);
     if (rc) return rc;
-    return run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, s);
+    if (!c->opt_graph || capturing || c->timing) return run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, s);
+    // ~80 dependent launches per batch: record them once as a HIP graph (on the context's own stream --
+    // the caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's
+    // stream while the pointers, sizes and parameters stay the same.
+    ofdis_context::GraphKey key;
+    std::memset(&key, 0, sizeof(key));  // padding included: the key is compared bytewise
+    key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = c->ws;
+    key.n = n; key.w = width; key.h = height; key.p = *p;
+    if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
+      if (c->gexec) {  // the previous graph may still be running on a caller stream
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipGraphExecDestroy(c->gexec));
+        c->gexec = nullptr;
+      }
+      hipGraph_t graph = nullptr;
+      HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      rc = run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, c->stream);
+      const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
+      if (rc) {
+        if (graph) hipGraphDestroy(graph);
+        return rc;
+      }
+      if (ce != hipSuccess || !graph) return OFDIS_ERR_DEVICE;
+      const hipError_t ie = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
+      hipGraphDestroy(graph);
+      if (ie != hipSuccess) {
+        c->gexec = nullptr;
+        return OFDIS_ERR_DEVICE;
+      }
+      std::memcpy(&c->gkey, &key, sizeof(key));
+    }
+    HIP_OK(hipGraphLaunch(c->gexec, s));
+    return OFDIS_OK;
   }
   const int k = std::min(c->opt_streams, nchunks);
   Plan PC = batch_plan(p, chunk, width, height);
@@ -738,6 +782,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   }
   if (std::strcmp(key, "wave_per_patch") == 0) {
     c->opt_wave_per_patch = value != 0;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "graph") == 0) {
+    c->opt_graph = value != 0;
     return OFDIS_OK;
   }
   if (std::strcmp(key, "tv_fused") == 0) {

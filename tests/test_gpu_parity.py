@@ -165,12 +165,15 @@ def test_batch_equals_singles(od, ctx):
     b = torch.from_numpy(np.stack([x[1] for x in pairs])).cuda()
     p = od.oppoint(2, w, 1, 1)
     outs = []
-    for streams, chunk in ((1, 0), (3, 2), (4, 1)):  # whole batch on one stream; chunks over streams
+    for streams, chunk, graph in ((1, 0, 1), (1, 0, 1), (1, 0, 0), (3, 2, 1), (4, 1, 1)):
+        # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams
         ctx.set_option("streams", streams)
         ctx.set_option("chunk", chunk)
+        ctx.set_option("graph", graph)
         o = ctx.run(a, b, p)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
+    ctx.set_option("graph", 1)
     ctx.set_option("streams", 1)
     ctx.set_option("chunk", 0)
     for f in range(n):
