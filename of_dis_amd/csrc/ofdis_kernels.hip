@@ -825,16 +825,19 @@ __device__ __forceinline__ long skw(int x, int y, int h) { return (long)(x + y) 
 
 // image_warp (opticalflow_aux.c:31-75) + the mean / temporal images of get_derivatives (:88-99), plus the
 // skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
-__device__ __forceinline__ void tv_prep_px(const TvArgs &a, int x, int y, int f) {
+// image_warp (opticalflow_aux.c:31-75) + the t / It inputs of get_derivatives (:77-132) for pixel (x, y):
+// v = {mask, wx, wy, t[0..noc), dt[0..noc)}.
+__device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, int f, float *v) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
-  const long fk = (long)f * a.sp + skw(x, y, a.h);
   const float wx = a.flow[(long)f * a.nop * plane + o];
   const float wy = a.nop == 2 ? a.flow[(long)f * a.nop * plane + plane + o] : 0.0f;
   const float xx = (float)x + wx, yy = (float)y + wy;
   const int xi = (int)floorf(xx), yi = (int)floorf(yy);
   const float dx = xx - (float)xi, dy = yy - (float)yi;
-  a.mask[fk] = (xx >= 0 && xx <= (float)(a.w - 1) && yy >= 0 && yy <= (float)(a.h - 1)) ? 1.0f : 0.0f;
+  v[0] = (xx >= 0 && xx <= (float)(a.w - 1) && yy >= 0 && yy <= (float)(a.h - 1)) ? 1.0f : 0.0f;
+  v[1] = wx;
+  v[2] = wy;
   const int x1 = clampi(xi, 0, a.w - 1), x2 = clampi(xi + 1, 0, a.w - 1);
   const int y1 = clampi(yi, 0, a.h - 1), y2 = clampi(yi + 1, 0, a.h - 1);
   const long fs = (long)a.W * (a.h + 2 * a.pad) * a.noc;
@@ -844,29 +847,58 @@ __device__ __forceinline__ void tv_prep_px(const TvArgs &a, int x, int y, int f)
     const float w2 = SB(x1, y1) * (1.0f - dx) * (1.0f - dy) + SB(x2, y1) * dx * (1.0f - dy) +
                      SB(x1, y2) * (1.0f - dx) * dy + SB(x2, y2) * dx * dy;
     const float i1 = A[((long)(y + a.pad) * a.W + x + a.pad) * a.noc + ch];
-    const long q = ((long)f * a.noc + ch) * a.sp + skw(x, y, a.h);
-    a.t[q] = 0.5f * (w2 + i1);
-    a.dt[q] = w2 - i1;
+    v[3 + ch] = 0.5f * (w2 + i1);
+    v[3 + a.noc + ch] = w2 - i1;
   }
 #undef SB
-  a.wxs[fk] = wx;
+}
+// The values of pixel (x, y) into the skewed planes (du = dv = 0: the increment starts at zero).
+__device__ __forceinline__ void tv_prep_store(const TvArgs &a, int x, int y, int f, const float *v) {
+  const long sk = skw(x, y, a.h), fk = (long)f * a.sp + sk;
+  a.mask[fk] = v[0];
+  a.wxs[fk] = v[1];
   a.du[fk] = 0.0f;
   if (a.nop == 2) {
-    a.wys[fk] = wy;
+    a.wys[fk] = v[2];
     a.dv[fk] = 0.0f;
   }
+  for (int ch = 0; ch < a.noc; ++ch) {
+    const long q = ((long)f * a.noc + ch) * a.sp + sk;
+    a.t[q] = v[3 + ch];
+    a.dt[q] = v[3 + a.noc + ch];
+  }
+}
+__device__ __forceinline__ void tv_prep_px(const TvArgs &a, int x, int y, int f) {
+  float v[9];
+  tv_prep_values(a, x, y, f, v);
+  tv_prep_store(a, x, y, f, v);
 }
 
-// Row-major <-> skewed conversions run on 64 x 16 pixel tiles: every 64-byte line of the skewed planes
-// (16 pixels of one anti-diagonal) and of the row-major planes is then touched by ONE workgroup, so partial
-// lines merge in that XCD's L2 instead of being written / fetched once per XCD.
-constexpr int kTileW = 64, kTileH = 16;
+// Row-major <-> skewed conversions run on 64 x 16 pixel tiles transposed through LDS: the row-major side
+// is read / written by rows, the skewed side by anti-diagonal segments of the tile (16 consecutive floats),
+// so neither side scatters 4-byte accesses over 64 cache lines per instruction.  Row pitch 66: the
+// diagonal-order accesses (row yy, column dd - yy) hit 16 different banks.
+constexpr int kTileW = 64, kTileH = 16, kTileP = 66, kTileD = kTileW + kTileH - 1;
 __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
-  const int x = blockIdx.x * kTileW + (threadIdx.x & 63), f = blockIdx.z;
-  if (x >= a.w) return;
-  for (int r = threadIdx.x >> 6; r < kTileH; r += 4) {
-    const int y = blockIdx.y * kTileH + r;
-    if (y < a.h) tv_prep_px(a, x, y, f);
+  __shared__ float sm[9][kTileH][kTileP];  // mask, wx, wy, t[noc], dt[noc]
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH, f = blockIdx.z;
+  const int tx = threadIdx.x & 63, np = 3 + 2 * a.noc;
+  for (int yl = threadIdx.x >> 6; yl < kTileH; yl += 4) {
+    const int x = x0 + tx, y = y0 + yl;
+    if (x < a.w && y < a.h) {
+      float v[9];
+      tv_prep_values(a, x, y, f, v);
+      for (int k = 0; k < np; ++k) sm[k][yl][tx] = v[k];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kTileD * kTileH; i += 256) {
+    const int yy = i & (kTileH - 1), dd = i / kTileH, xl = dd - yy;
+    const int x = x0 + xl, y = y0 + yy;
+    if (xl < 0 || xl >= kTileW || x >= a.w || y >= a.h) continue;
+    float v[9];
+    for (int k = 0; k < np; ++k) v[k] = sm[k][yy][xl];
+    tv_prep_store(a, x, y, f, v);
   }
 }
 
@@ -1837,11 +1869,31 @@ __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f
 }
 
 __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
-  const int x = blockIdx.x * kTileW + (threadIdx.x & 63), f = blockIdx.z;
-  if (x >= a.w) return;
-  for (int r = threadIdx.x >> 6; r < kTileH; r += 4) {
-    const int y = blockIdx.y * kTileH + r;
-    if (y < a.h) tv_final_px(a, x, y, f);
+  __shared__ float sm[2][kTileH][kTileP];
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH, f = blockIdx.z;
+  for (int i = threadIdx.x; i < kTileD * kTileH; i += 256) {  // skewed side: diagonal segments
+    const int yy = i & (kTileH - 1), dd = i / kTileH, xl = dd - yy;
+    const int x = x0 + xl, y = y0 + yy;
+    if (xl < 0 || xl >= kTileW || x >= a.w || y >= a.h) continue;
+    const long fk = (long)f * a.sp + skw(x, y, a.h);
+    if (a.nop == 2) {
+      sm[0][yy][xl] = a.wxs[fk] + a.du[fk];
+      sm[1][yy][xl] = a.wys[fk] + a.dv[fk];
+    } else {
+      const float s = a.wxs[fk] + a.du[fk];
+      sm[0][yy][xl] = a.camlr == 0 ? ssemin(s, 0.0f) : ssemax(s, 0.0f);
+    }
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 63, x = x0 + tx;
+  const long plane = (long)a.w * a.h;
+  float *WX = a.flow + (long)f * a.nop * plane;
+  for (int yl = threadIdx.x >> 6; yl < kTileH; yl += 4) {  // row-major side: rows
+    const int y = y0 + yl;
+    if (x >= a.w || y >= a.h) continue;
+    const long o = (long)y * a.w + x;
+    WX[o] = sm[0][yl][tx];
+    if (a.nop == 2) WX[plane + o] = sm[1][yl][tx];
   }
 }
 
