@@ -80,6 +80,60 @@ __global__ __launch_bounds__(256) void k_pyr_base(PyrBaseArgs a) {
   }
 }
 
+// Intensity images, 2^L = 4..32: one output pixel per thread over the flattened [2n][h][w] range (full
+// waves even for narrow levels), the 2^L rows of the block unrolled so all loads are in flight at once,
+// 4 / 8 / 16-byte loads summed with v_sad_u8.  Blocks that need horizontal clamping take the byte loop.
+template <int L>
+__global__ __launch_bounds__(256) void k_pyr_base_gray(PyrBaseArgs a) {
+  constexpr int B = 1 << L;
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2L * a.n * a.h * a.w) return;
+  const int x = (int)(t % a.w);
+  const long r = t / a.w;
+  const int y = (int)(r % a.h), f = (int)(r / a.h);
+  const long fs = (long)a.H0 * a.W0;
+  const uint8_t *src = f < a.n ? a.img_a + (long)f * fs : a.img_b + (long)(f - a.n) * fs;
+  const float scale = 1.0f / (float)(1 << (2 * L));
+  const int x0 = x * B - a.padl;
+  constexpr int VB = B >= 16 ? 16 : B;  // bytes per load
+  unsigned sum = 0;
+  if (x0 >= 0 && x0 + B <= a.W0 && ((((uintptr_t)src) + x0) % VB) == 0 && (a.W0 % VB) == 0) {
+    unsigned acc[B];
+#pragma unroll
+    for (int by = 0; by < B; ++by) {
+      const int yy = clampi(y * B + by - a.padt, 0, a.H0 - 1);
+      const uint8_t *row = src + (long)yy * a.W0 + x0;
+      unsigned s2 = 0;
+      if (VB == 16) {
+#pragma unroll
+        for (int q = 0; q < B / 16; ++q) {
+          const uint4 v = reinterpret_cast<const uint4 *>(row)[q];
+          s2 = __builtin_amdgcn_sad_u8(v.x, 0u, s2);
+          s2 = __builtin_amdgcn_sad_u8(v.y, 0u, s2);
+          s2 = __builtin_amdgcn_sad_u8(v.z, 0u, s2);
+          s2 = __builtin_amdgcn_sad_u8(v.w, 0u, s2);
+        }
+      } else if (VB == 8) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(row);
+        s2 = __builtin_amdgcn_sad_u8(v.x, 0u, s2);
+        s2 = __builtin_amdgcn_sad_u8(v.y, 0u, s2);
+      } else {
+        s2 = __builtin_amdgcn_sad_u8(*reinterpret_cast<const unsigned *>(row), 0u, s2);
+      }
+      acc[by] = s2;
+    }
+#pragma unroll
+    for (int by = 0; by < B; ++by) sum += acc[by];  // integer sum: order-free
+  } else {
+    for (int by = 0; by < B; ++by) {
+      const int yy = clampi(y * B + by - a.padt, 0, a.H0 - 1);
+      const uint8_t *row = src + (long)yy * a.W0;
+      for (int bx = 0; bx < B; ++bx) sum += row[clampi(x0 + bx, 0, a.W0 - 1)];
+    }
+  }
+  a.out[t] = (float)sum * scale;
+}
+
 __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a) {
   const int xc = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
   if (xc >= a.w * a.noc) return;
@@ -1394,6 +1448,12 @@ __device__ __forceinline__ float dpp_from_next_lane(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
 }
 
+// A register move the compiler cannot look through (see SorWave::step): an identity DPP quad permutation,
+// an ordinary VALU op for the wait-count pass (it waits only for its own operand).
+__device__ __forceinline__ float opaque_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xE4, 0xF, 0xF, true));
+}
+
 // Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later (register ring).
 struct SorPix {
   float i11, i12, i22, b1, b2, hl, hr, vv, vt;
@@ -1720,25 +1780,32 @@ struct SorWave {
     const int m1 = (t + 2) % 3, m2 = (t + 1) % 3, m0 = t % 3;  // ring slots of steps t-1, t-2, t
     float i11[R], i12[R], i22[R], b1[R], b2[R], hr[R], vv[R];
     float ou[R], ov[R], ru[R], rv[R], bu[R], bv[R];
+    // The prefetched values are moved out of the load buffers by opaque register moves before the next
+    // prefetch is issued into them: the buffers' old and new values then never overlap, so the register
+    // allocator keeps each buffer in the same registers across the loop back-edge and the loads stay in
+    // flight there (a back-edge copy would have to wait for them).
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (MODE == 0) {
-        i11[r] = B[r].c0.x; i12[r] = B[r].c0.y; i22[r] = B[r].c0.z; b1[r] = B[r].c0.w;
-        b2[r] = B[r].c1.x; hr[r] = B[r].c1.y; vv[r] = B[r].c1.z;
+        i11[r] = opaque_mov(B[r].c0.x); i12[r] = opaque_mov(B[r].c0.y); i22[r] = opaque_mov(B[r].c0.z);
+        b1[r] = opaque_mov(B[r].c0.w); b2[r] = opaque_mov(B[r].c1.x); hr[r] = opaque_mov(B[r].c1.y);
+        vv[r] = opaque_mov(B[r].c1.z);
       } else {
-        i11[r] = B[r].c0.x; b1[r] = B[r].c0.y; hr[r] = B[r].c0.z; vv[r] = B[r].c0.w;
+        i11[r] = opaque_mov(B[r].c0.x); b1[r] = opaque_mov(B[r].c0.y); hr[r] = opaque_mov(B[r].c0.z);
+        vv[r] = opaque_mov(B[r].c0.w);
         i12[r] = i22[r] = b2[r] = 0.0f;
       }
       if (FIRST) {
-        ou[r] = B[r].ou; ru[r] = B[r].ru; bu[r] = B[r].bu;
-        ov[r] = MODE == 0 ? B[r].ov : 0.0f; rv[r] = MODE == 0 ? B[r].rv : 0.0f;
-        bv[r] = MODE == 0 ? B[r].bv : 0.0f;
+        ou[r] = opaque_mov(B[r].ou); ru[r] = opaque_mov(B[r].ru); bu[r] = opaque_mov(B[r].bu);
+        ov[r] = MODE == 0 ? opaque_mov(B[r].ov) : 0.0f; rv[r] = MODE == 0 ? opaque_mov(B[r].rv) : 0.0f;
+        bv[r] = MODE == 0 ? opaque_mov(B[r].bv) : 0.0f;
       } else {
         const int e = y0 + r + 1;
         const float4 o4 = ring_p[m2 * NR + e], r4 = ring_p[m1 * NR + e], b4 = ring_p[m1 * NR + e + 1];
         ou[r] = o4.x; ov[r] = o4.y; ru[r] = r4.x; rv[r] = r4.y; bu[r] = b4.x; bv[r] = b4.y;
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
     load(t + 2, B);
     const float4 t4 = ring_s[m1 * NR + y0];   // row y0 - 1 (previous lane / row group) at step t-1
     float nu[R], nv[R];
@@ -2100,6 +2167,16 @@ __global__ __launch_bounds__(256) void k_upsample(UpArgs a) {
 // ------------------------------------------------------------------------------------------------ launchers
 
 void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s) {
+  const long total = 2L * a.n * a.h * a.w;
+  if (a.noc == 1 && a.log2s >= 2 && a.log2s <= 5) {
+    const unsigned blocks = (unsigned)ceil_div(total, 256);
+    switch (a.log2s) {
+      case 2: k_pyr_base_gray<2><<<blocks, 256, 0, s>>>(a); return;
+      case 3: k_pyr_base_gray<3><<<blocks, 256, 0, s>>>(a); return;
+      case 4: k_pyr_base_gray<4><<<blocks, 256, 0, s>>>(a); return;
+      case 5: k_pyr_base_gray<5><<<blocks, 256, 0, s>>>(a); return;
+    }
+  }
   k_pyr_base<<<dim3(ceil_div(a.w, 256), a.h, 2 * a.n), 256, 0, s>>>(a);
 }
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {

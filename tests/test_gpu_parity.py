@@ -114,7 +114,8 @@ def test_kernel_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op,
     assert_bitexact(got, ref, f"{key}={val}")
 
 
-@pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2)])
+@pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2),
+                                         (640, 480, 1, 2), (330, 250, 1, 2), (2000, 1000, 1, 2)])
 def test_pyramid_bitexact(oracle, od, ctx, w, h, noc, op):
     O = oracle
     a, _ = od.synth_pair(w, h, noc, 1, 1)
