@@ -1774,7 +1774,7 @@ struct SorWave {
     }
   }
 
-  template <int Q>
+  template <int Q, bool PREF>
   __device__ __forceinline__ void step(const int t) {
     Ld (&B)[R] = L[Q];
     const int m1 = (t + 2) % 3, m2 = (t + 1) % 3, m0 = t % 3;  // ring slots of steps t-1, t-2, t
@@ -1806,7 +1806,7 @@ struct SorWave {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    load(t + 2, B);
+    if (PREF) load(t + 2, B);
     const float4 t4 = ring_s[m1 * NR + y0];   // row y0 - 1 (previous lane / row group) at step t-1
     float nu[R], nv[R];
 #pragma unroll
@@ -1858,14 +1858,29 @@ struct SorWave {
     __syncthreads();
   }
 
+  // U steps with the prefetch distance 2 kept inside the block: no load is in flight across the loop's
+  // back-edge (a loop-carried in-flight register forces a wait or a copy there), at the price of one
+  // exposed load latency per block.
+  template <int J, int U>
+  __device__ __forceinline__ void block(const int t) {
+    step<J & 1, (J + 2 < U)>(t + J);
+    if constexpr (J + 1 < U) block<J + 1, U>(t);
+  }
+
   __device__ __forceinline__ void run(int T) {
 #pragma unroll
     for (int r = 0; r < R; ++r) pu[r] = pv[r] = phr[r] = pvv[r] = 0.0f;
-    load(0, L[0]);
-    load(1, L[1]);
-    for (int t = 0; t < T; t += 2) {
-      step<0>(t);
-      step<1>(t + 1);
+    constexpr int U = 8;
+    int t = 0;
+    for (; t + U <= T; t += U) {
+      load(t, L[0]);
+      load(t + 1, L[1]);
+      block<0, U>(t);
+    }
+    for (; t < T; t += 2) {  // T is even
+      load(t, L[0]);
+      load(t + 1, L[1]);
+      block<0, 2>(t);
     }
   }
 };
