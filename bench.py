@@ -27,7 +27,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # BASELINE.json configs -> (binary, width, height, noc, mode, oppoint, explicit 20 parameters or None, batch)
 CONFIGS = {
     "A": ("run_OF_INT", 640, 480, 1, 1, 2, None, 256),
-    "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 256),
+    "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 512),
     # op-point 3 as the config text states it ("finer scale, L1 cost"): op3 values with costfct = 1
     "C": ("run_OF_RGB", 1920, 1080, 3, 1, 3, "6 2 16 16 0.05 0.95 0 12 0.75 0 1 1 1 10 10 5 1 3 1.6 2", 64),
     "D": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 32),
@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the batch's chunks round-robin over")
     ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = whole batch in one chunk)")
     ap.add_argument("--tv-fused", type=int, default=-1, help="1/0: force the fused TV level kernel on/off")
+    ap.add_argument("--option", action="append", default=[], help="context option key=value (A/B runs)")
     ap.add_argument("--host-io", action="store_true",
                     help="also time the host-buffer entry point (PCIe-inclusive rate, reported separately)")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -119,6 +120,9 @@ def main():
     ctx.set_option("chunk", args.chunk)
     if args.tv_fused >= 0:
         ctx.set_option("tv_fused", args.tv_fused)
+    for kv in args.option:
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
 
     # synthetic inputs, resident in HBM before timing: distinct pairs per rank, tiled over the batch
     first = odd.shard_range(B * world, rank, world)[0]
@@ -232,6 +236,7 @@ def main():
                                    + f", {B} pairs/GPU/step", "name": args.config,
                        "width": W, "height": H, "channels": noc, "oppoint": op, "batch_per_gpu": B,
                        "streams": args.streams, "chunk": args.chunk, "tv_fused": args.tv_fused,
+                       "options": args.option,
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,
             "host_io": host_io, "kernels": kernels,

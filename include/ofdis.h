@@ -138,6 +138,7 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        today: one workgroup per frame leaves the data-parallel phases latency-bound);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (same bits; A/B);
  *   "sor_rows" (0, 1, 2, 4): rows per lane of the sweep-per-wave SOR (0 = automatic; same bits);
+ *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
  *   "graph" (0/1, default 1): replay a single-stream batch as one captured HIP graph while its pointers,
  *                        sizes and parameters repeat (re-captured when they change; same bits);
  *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into

@@ -80,7 +80,9 @@ struct TvArgs {
   float *coef;                 // AoS per pixel: OF (a11,a12,a22,b1)(b2,sh,sv,-) = 8 floats; DE (a11,b1,sh,sv)
   float *t, *dt;               // skewed [n][noc][sp]
   float *Ix, *Iy, *Iz, *Ixx, *Ixy, *Iyy, *Ixz, *Iyz;  // skewed [n][noc][sp]
-  long sp;                     // skewed plane stride: (w + h - 1) * h pixels + 64 dump slots (SOR)
+  long sp;                     // skewed plane stride: skew_slots + 64 dump slots (SOR), multiple of 4
+  int wrap;                    // rows folded modulo w (h <= w): skew_slots = w * h, else (w + h - 1) * h
+  int skew_slots;
   int n, nop, noc, w, h, pad, W;
   float quarter_alpha, hdo3, hgo3, omega;
   int first_iter;              // uu = wx (memcpy) on the first inner iteration
@@ -95,6 +97,7 @@ struct UpArgs {
   const float *flow;  // planar [n][nop][hl][wl]
   float *out;         // [n][H0][W0][nop]
   int n, nop, wl, hl, log2s, W0, H0, offx, offy;
+  int nt_store;       // non-temporal output stores (A/B option "nt_store")
 };
 
 void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s);

@@ -875,7 +875,13 @@ __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
 
 // ------------------------------------------------------------------------------------------------ variational
 
-__device__ __forceinline__ long skw(int x, int y, int h) { return (long)(x + y) * h + y; }
+// Pixel (x, y) of a w x h level sits in row d = x + y (its anti-diagonal), column y.  With `wrap` (h <= w)
+// the rows are folded modulo w: row d mod w then holds exactly one pixel of every column, the plane has no
+// holes (w * h slots instead of (w + h - 1) * h) and the pixels of one wavefront step stay contiguous.
+__device__ __forceinline__ int skrow(int d, int w, int wrap) { return wrap && d >= w ? d - w : d; }
+__device__ __forceinline__ long skw(int x, int y, int h, int w, int wrap) {
+  return (long)skrow(x + y, w, wrap) * h + y;
+}
 
 // image_warp (opticalflow_aux.c:31-75) + the mean / temporal images of get_derivatives (:88-99), plus the
 // skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
@@ -908,7 +914,7 @@ __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, in
 }
 // The values of pixel (x, y) into the skewed planes (du = dv = 0: the increment starts at zero).
 __device__ __forceinline__ void tv_prep_store(const TvArgs &a, int x, int y, int f, const float *v) {
-  const long sk = skw(x, y, a.h), fk = (long)f * a.sp + sk;
+  const long sk = skw(x, y, a.h, a.w, a.wrap), fk = (long)f * a.sp + sk;
   a.mask[fk] = v[0];
   a.wxs[fk] = v[1];
   a.du[fk] = 0.0f;
@@ -960,45 +966,49 @@ __constant__ float kK5[5] = {1.0f / 12.0f, -8.0f / 12.0f, -0.0f, 8.0f / 12.0f, -
 __constant__ float kK3[3] = {-0.5f, -0.0f, 0.5f};
 
 // 5-tap filters (image.cpp:419-624 fast paths) with replicate border, on a skewed plane.
-__device__ __forceinline__ float conv5h(const float *s, int x, int y, int w, int h) {
-  const float s0 = s[skw(clampi(x - 2, 0, w - 1), y, h)], s1 = s[skw(clampi(x - 1, 0, w - 1), y, h)];
-  const float s2 = s[skw(x, y, h)];
-  const float s3 = s[skw(clampi(x + 1, 0, w - 1), y, h)], s4 = s[skw(clampi(x + 2, 0, w - 1), y, h)];
+__device__ __forceinline__ float conv5h(const float *s, int x, int y, int w, int h, int wr) {
+  const float s0 = s[skw(clampi(x - 2, 0, w - 1), y, h, w, wr)], s1 = s[skw(clampi(x - 1, 0, w - 1), y, h, w, wr)];
+  const float s2 = s[skw(x, y, h, w, wr)];
+  const float s3 = s[skw(clampi(x + 1, 0, w - 1), y, h, w, wr)], s4 = s[skw(clampi(x + 2, 0, w - 1), y, h, w, wr)];
   return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
 }
-__device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int h) {
-  const float s0 = s[skw(x, clampi(y - 2, 0, h - 1), h)], s1 = s[skw(x, clampi(y - 1, 0, h - 1), h)];
-  const float s2 = s[skw(x, y, h)];
-  const float s3 = s[skw(x, clampi(y + 1, 0, h - 1), h)], s4 = s[skw(x, clampi(y + 2, 0, h - 1), h)];
+__device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int h, int wr) {
+  const float s0 = s[skw(x, clampi(y - 2, 0, h - 1), h, w, wr)], s1 = s[skw(x, clampi(y - 1, 0, h - 1), h, w, wr)];
+  const float s2 = s[skw(x, y, h, w, wr)];
+  const float s3 = s[skw(x, clampi(y + 1, 0, h - 1), h, w, wr)], s4 = s[skw(x, clampi(y + 2, 0, h - 1), h, w, wr)];
   return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
 }
 
-// decode a skewed-plane thread index; false for the padding triangles
-__device__ __forceinline__ bool skew_xy(int kk, int w, int h, int &x, int &y) {
+// decode a skewed-plane thread index; false for holes (unwrapped layout) and the dump slots
+__device__ __forceinline__ bool skew_xy(int kk, int w, int h, int wrap, int &x, int &y) {
   const int t = kk / h;
   y = kk - t * h;
   x = t - y;
+  if (wrap) {
+    if (x < 0) x += w;
+    return t < w;
+  }
   return x >= 0 && x < w;
 }
 
 __device__ __forceinline__ void tv_deriv1_px(const TvArgs &a, long pl, int kk) {
   const long idx = pl * a.sp + kk;
   int x, y;
-  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
   const float *t = a.t + pl * a.sp, *dt = a.dt + pl * a.sp;
-  a.Ix[idx] = conv5h(t, x, y, a.w, a.h);
-  a.Iy[idx] = conv5v(t, x, y, a.w, a.h);
-  a.Ixz[idx] = conv5h(dt, x, y, a.w, a.h);
-  a.Iyz[idx] = conv5v(dt, x, y, a.w, a.h);
+  a.Ix[idx] = conv5h(t, x, y, a.w, a.h, a.wrap);
+  a.Iy[idx] = conv5v(t, x, y, a.w, a.h, a.wrap);
+  a.Ixz[idx] = conv5h(dt, x, y, a.w, a.h, a.wrap);
+  a.Iyz[idx] = conv5v(dt, x, y, a.w, a.h, a.wrap);
 }
 
 __device__ __forceinline__ void tv_deriv2_px(const TvArgs &a, long pl, int kk) {
   const long idx = pl * a.sp + kk;
   int x, y;
-  if (!skew_xy(kk, a.w, a.h, x, y)) return;
-  a.Ixx[idx] = conv5h(a.Ix + pl * a.sp, x, y, a.w, a.h);
-  a.Ixy[idx] = conv5v(a.Ix + pl * a.sp, x, y, a.w, a.h);
-  a.Iyy[idx] = conv5v(a.Iy + pl * a.sp, x, y, a.w, a.h);
+  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
+  a.Ixx[idx] = conv5h(a.Ix + pl * a.sp, x, y, a.w, a.h, a.wrap);
+  a.Ixy[idx] = conv5v(a.Ix + pl * a.sp, x, y, a.w, a.h, a.wrap);
+  a.Iyy[idx] = conv5v(a.Iy + pl * a.sp, x, y, a.w, a.h, a.wrap);
 }
 
 __global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
@@ -1233,10 +1243,11 @@ template <int NOP>
 __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, bool first) {
   const long f0 = fr * a.sp, idx = f0 + kk;
   int x, y;
-  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
   const int w = a.w, h = a.h;
-  const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h);
-  const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h);
+  const int wr = a.wrap;
+  const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h, w, wr), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h, w, wr);
+  const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h, w, wr), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h, w, wr);
   const long k5[5] = {idx, kl, kr, ku, kd};
   // gather everything first (one memory round trip), then uu = wx (first iteration) or wx + du
   float wx5[5], du5[5], wy5[5], dv5[5];
@@ -1284,11 +1295,12 @@ template <int NOP, int NOC>
 __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
   const long idx = fr * a.sp + kk;
   int x, y;
-  if (!skew_xy(kk, a.w, a.h, x, y)) return;
+  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
   const int w = a.w, h = a.h;
   const bool hasl = x >= 1, hasr = x <= w - 2, hasu = y >= 1, hasd = y <= h - 2;
-  const long il = hasl ? idx - h : idx, ir = hasr ? idx + h : idx;
-  const long iu = hasu ? idx - h - 1 : idx, id = hasd ? idx + h + 1 : idx;
+  const long f0 = fr * a.sp;
+  const long il = hasl ? f0 + skw(x - 1, y, h, w, a.wrap) : idx, ir = hasr ? f0 + skw(x + 1, y, h, w, a.wrap) : idx;
+  const long iu = hasu ? f0 + skw(x, y - 1, h, w, a.wrap) : idx, id = hasd ? f0 + skw(x, y + 1, h, w, a.wrap) : idx;
   // ---- gather
   const float *S = a.s, *WX = a.wxs, *WY = a.wys;
   const float sc = S[idx], sl = S[il], sr = S[ir], su = S[iu], sd = S[id];
@@ -1376,37 +1388,39 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
   const float omega = a.omega;
   const int items = S * h;
   const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
-  const int L = h, U = h + 1;  // skewed offsets of the left (x-1) and upper (y-1) neighbours
   for (int t = 0; t < T; ++t) {
     for (int k = threadIdx.x; k < items; k += blockDim.x) {
       const int s = k / h, y = k - s * h;
       const int x = t - y - 2 * s;
       if (x < 0 || x >= w) continue;
-      const long o = skw(x, y, h);
+      const long o = skw(x, y, h, w, a.wrap);
+      // neighbours (clamped coordinates: only read when they exist)
+      const long oL = skw(x > 0 ? x - 1 : x, y, h, w, a.wrap), oR = skw(x < w - 1 ? x + 1 : x, y, h, w, a.wrap);
+      const long oU = skw(x, y > 0 ? y - 1 : y, h, w, a.wrap), oD = skw(x, y < h - 1 ? y + 1 : y, h, w, a.wrap);
       if (MODE == 0) {
         const float4 c0 = C[2 * o];
         const float4 c1 = C[2 * o + 1];
         const float b1 = c0.w, b2 = c1.x, hr = c1.y, vo = c1.z;
-        const float hl = x > 0 ? SH_(o - L) : 0.0f;
-        const float ur = x < w - 1 ? du[o + L] : 0.0f, vr = x < w - 1 ? dv[o + L] : 0.0f;
+        const float hl = x > 0 ? SH_(oL) : 0.0f;
+        const float ur = x < w - 1 ? du[oR] : 0.0f, vr = x < w - 1 ? dv[oR] : 0.0f;
         float s1, s2;
         if (y == 0) {
-          s1 = (b1 + hr * ur) + vo * du[o + U];
-          s2 = (b2 + hr * vr) + vo * dv[o + U];
+          s1 = (b1 + hr * ur) + vo * du[oD];
+          s2 = (b2 + hr * vr) + vo * dv[oD];
         } else if (y < h - 1) {
-          const float vt = SV_(o - U);
-          s1 = ((hr * ur) + vt * du[o - U]) + (b1 + vo * du[o + U]);
-          s2 = ((hr * vr) + vt * dv[o - U]) + (b2 + vo * dv[o + U]);
+          const float vt = SV_(oU);
+          s1 = ((hr * ur) + vt * du[oU]) + (b1 + vo * du[oD]);
+          s2 = ((hr * vr) + vt * dv[oU]) + (b2 + vo * dv[oD]);
         } else {
-          const float vt = SV_(o - U);
-          s1 = (b1 + hr * ur) + vt * du[o - U];
-          s2 = (b2 + hr * vr) + vt * dv[o - U];
+          const float vt = SV_(oU);
+          s1 = (b1 + hr * ur) + vt * du[oU];
+          s2 = (b2 + hr * vr) + vt * dv[oU];
         }
         const float i11 = c0.x, i12 = c0.y, i22 = c0.z;  // inverse precomputed by k_tv_system
         float B1 = s1, B2 = s2;
         if (x > 0) {
-          B1 = hl * du[o - L] + s1;
-          B2 = hl * dv[o - L] + s2;
+          B1 = hl * du[oL] + s1;
+          B2 = hl * dv[oL] + s2;
         }
         const float u0 = du[o], v0 = dv[o];
         du[o] = u0 + omega * (i11 * B1 + i12 * B2 - u0);
@@ -1414,10 +1428,10 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
       } else if (MODE == 1) {
         const float4 c0 = C[2 * o], c1 = C[2 * o + 1];
         float su = 0.0f, sv = 0.0f, sd = 0.0f;
-        if (y > 0) { const float q = SV_(o - U); su -= q * du[o - U]; sv -= q * dv[o - U]; sd += q; }
-        if (x > 0) { const float q = SH_(o - L); su -= q * du[o - L]; sv -= q * dv[o - L]; sd += q; }
-        if (y < h - 1) { su -= c1.z * du[o + U]; sv -= c1.z * dv[o + U]; sd += c1.z; }
-        if (x < w - 1) { su -= c1.y * du[o + L]; sv -= c1.y * dv[o + L]; sd += c1.y; }
+        if (y > 0) { const float q = SV_(oU); su -= q * du[oU]; sv -= q * dv[oU]; sd += q; }
+        if (x > 0) { const float q = SH_(oL); su -= q * du[oL]; sv -= q * dv[oL]; sd += q; }
+        if (y < h - 1) { su -= c1.z * du[oD]; sv -= c1.z * dv[oD]; sd += c1.z; }
+        if (x < w - 1) { su -= c1.y * du[oR]; sv -= c1.y * dv[oR]; sd += c1.y; }
         const float A11 = c0.x + sd, A12 = c0.y, A22 = c0.z + sd;
         const float B1 = c0.w - su, B2 = c1.x - sv;
         du[o] = (1.0f - omega) * du[o] + omega / A11 * (B1 - A12 * dv[o]);
@@ -1425,10 +1439,10 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
       } else {
         const float4 c0 = C[o];
         float su = 0.0f, sd = 0.0f;
-        if (y > 0) { const float q = SV_(o - U); su -= q * du[o - U]; sd += q; }
-        if (x > 0) { const float q = SH_(o - L); su -= q * du[o - L]; sd += q; }
-        if (y < h - 1) { su -= c0.w * du[o + U]; sd += c0.w; }
-        if (x < w - 1) { su -= c0.z * du[o + L]; sd += c0.z; }
+        if (y > 0) { const float q = SV_(oU); su -= q * du[oU]; sd += q; }
+        if (x > 0) { const float q = SH_(oL); su -= q * du[oL]; sd += q; }
+        if (y < h - 1) { su -= c0.w * du[oD]; sd += c0.w; }
+        if (x < w - 1) { su -= c0.z * du[oR]; sd += c0.z; }
         const float A11 = c0.x + sd, B1 = c0.y - su;
         du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
       }
@@ -1500,7 +1514,7 @@ struct SorPipe {
   const float4 *C;
   float *du, *dv;
   float4 (*xtop)[16][NV4], (*xbot)[16][NV4];
-  int w, h, y, lane, wv, nw;
+  int w, h, y, lane, wv, nw, wrap;
   unsigned dump;
   float omega;
   bool has_top, has_bot, border, notop, get_top, get_bot;
@@ -1508,7 +1522,8 @@ struct SorPipe {
   __device__ __forceinline__ void load(int t, Ld &B) {
     const int x0 = t - y;
     const bool in = y < h && x0 >= 0 && x0 < w;
-    const unsigned here = (unsigned)(t * h + y);
+    const unsigned here = (unsigned)(skrow(t, w, wrap) * h + y);
+    const unsigned next = (unsigned)(skrow(t + 1, w, wrap) * h + y);  // row of diagonal t + 1
     const unsigned o = in ? here : dump;
     if (MODE == 0) {
       B.c0 = C[2 * o];
@@ -1516,10 +1531,10 @@ struct SorPipe {
     } else {
       B.c0 = C[o];
     }
-    const unsigned ob = in && has_bot ? here + h + 1 : dump;
+    const unsigned ob = in && has_bot ? next + 1 : dump;
     B.bu = du[ob];
     if (MODE == 0) B.bv = dv[ob];
-    const unsigned orr = y < h && x0 + 1 >= 0 && x0 + 1 < w ? here + h : dump;
+    const unsigned orr = y < h && x0 + 1 >= 0 && x0 + 1 < w ? next : dump;
     B.ru = du[orr];
     if (MODE == 0) B.rv = dv[orr];
   }
@@ -1631,7 +1646,7 @@ struct SorPipe {
     // ---- the last sweep's result is final (unconditional store: inactive lanes hit the dump slots)
     {
       const int xl = x0 - 2 * (S - 1);
-      const unsigned o = y < h && xl >= 0 && xl < w ? (unsigned)((t - 2 * (S - 1)) * h + y) : dump;
+      const unsigned o = y < h && xl >= 0 && xl < w ? (unsigned)(skrow(t - 2 * (S - 1), w, wrap) * h + y) : dump;
       du[o] = nu[S - 1];
       if (MODE == 0) dv[o] = nvv[S - 1];
     }
@@ -1700,7 +1715,8 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_pipe(TvArgs a) {
   st.border = !st.has_top || !st.has_bot;
   st.get_top = st.lane == 0 && st.wv > 0;
   st.get_bot = st.lane == 63 && st.wv < st.nw - 1;
-  st.dump = (unsigned)((a.w + a.h - 1) * a.h + st.lane);
+  st.wrap = a.wrap;
+  st.dump = (unsigned)(a.skew_slots + st.lane);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -1741,7 +1757,7 @@ struct SorWave {
   float *du, *dv;
   float4 *ring_s;              // [3][NR] this sweep's results (entry y + 1 for row y)
   const float4 *ring_p;        // [3][NR] previous sweep's results (s >= 1)
-  int w, h, y0, s, NR;         // rows y0 .. y0 + R - 1
+  int w, h, y0, s, NR, wrap;   // rows y0 .. y0 + R - 1
   unsigned dump;
   float omega;
 
@@ -1751,7 +1767,8 @@ struct SorWave {
       const int y = y0 + r;
       const int x = t - y - 2 * s;
       const bool in = y < h && x >= 0 && x < w;
-      const unsigned here = (unsigned)((x + y) * h + y);
+      const unsigned here = (unsigned)(skrow(t - 2 * s, w, wrap) * h + y);
+      const unsigned next = (unsigned)(skrow(t - 2 * s + 1, w, wrap) * h + y);  // diagonal + 1
       const unsigned o = in ? here : dump;
       if (MODE == 0) {
         B[r].c0 = C[2 * o];
@@ -1761,9 +1778,9 @@ struct SorWave {
       }
       if (FIRST) {
         B[r].ou = du[o];
-        const unsigned orr = in && x + 1 < w ? here + h : dump;
+        const unsigned orr = in && x + 1 < w ? next : dump;
         B[r].ru = du[orr];
-        const unsigned ob = in && y < h - 1 ? here + h + 1 : dump;
+        const unsigned ob = in && y < h - 1 ? next + 1 : dump;
         B[r].bu = du[ob];
         if (MODE == 0) {
           B[r].ov = dv[o];
@@ -1846,7 +1863,7 @@ struct SorWave {
       ring_s[m0 * NR + y + 1] = make_float4(nu[r], nv[r], vv[r], 0.0f);
       if (LAST) {
         const int x = t - y - 2 * s;
-        const unsigned o = y < h && x >= 0 && x < w ? (unsigned)((x + y) * h + y) : dump;
+        const unsigned o = y < h && x >= 0 && x < w ? (unsigned)(skrow(t - 2 * s, w, wrap) * h + y) : dump;
         du[o] = nu[r];
         if (MODE == 0) dv[o] = nv[r];
       }
@@ -1914,7 +1931,8 @@ __device__ __forceinline__ void sor_waves_frame(const TvArgs &a, int frame, floa
     st.ring_s = ring + s * 3 * NR;
     st.ring_p = ring + (s > 0 ? s - 1 : 0) * 3 * NR;
     st.w = a.w; st.h = a.h; st.y0 = (g * 64 + lane) * R; st.s = s; st.NR = NR;
-    st.dump = (unsigned)((a.w + a.h - 1) * a.h + lane);
+    st.wrap = a.wrap;
+    st.dump = (unsigned)(a.skew_slots + lane);
     st.omega = a.omega;
     st.run(T2);
   };
@@ -1939,7 +1957,7 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_waves(TvArgs a) {
 __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
-  const long fk = (long)f * a.sp + skw(x, y, a.h);
+  const long fk = (long)f * a.sp + skw(x, y, a.h, a.w, a.wrap);
   float *WX = a.flow + (long)f * a.nop * plane;
   if (a.nop == 2) {
     WX[o] = a.wxs[fk] + a.du[fk];
@@ -1957,7 +1975,7 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
     const int yy = i & (kTileH - 1), dd = i / kTileH, xl = dd - yy;
     const int x = x0 + xl, y = y0 + yy;
     if (xl < 0 || xl >= kTileW || x >= a.w || y >= a.h) continue;
-    const long fk = (long)f * a.sp + skw(x, y, a.h);
+    const long fk = (long)f * a.sp + skw(x, y, a.h, a.w, a.wrap);
     if (a.nop == 2) {
       sm[0][yy][xl] = a.wxs[fk] + a.du[fk];
       sm[1][yy][xl] = a.wys[fk] + a.dv[fk];
@@ -2142,7 +2160,11 @@ __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
     for (int hh = 0; hh < 2; ++hh) {
       const int x = xs[hh];
       if (x + 2 <= a.W0) {
-        *reinterpret_cast<v4f *>(row + 2 * x) = v4f{v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]};
+        const v4f val = v4f{v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]};
+        if (a.nt_store)
+          __builtin_nontemporal_store(val, reinterpret_cast<v4f *>(row + 2 * x));
+        else
+          *reinterpret_cast<v4f *>(row + 2 * x) = val;
       } else if (x < a.W0) {
         row[2 * x] = v[4 * hh];
         row[2 * x + 1] = v[4 * hh + 1];

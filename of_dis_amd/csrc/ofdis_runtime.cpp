@@ -39,6 +39,13 @@ struct Plan {
 
 inline size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Skewed TV plane: w * h slots when the anti-diagonal rows fold modulo w (h <= w), else (w + h - 1) * h,
+// plus 64 per-lane dump slots for the SOR kernels; a multiple of 4 floats (16-byte AoS coefficients).
+inline long skew_plane(int w, int h) {
+  const long slots = h <= w ? (long)w * h : (long)(w + h - 1) * h;
+  return (slots + 64 + 3) / 4 * 4;
+}
+
 }  // namespace
 
 struct ofdis_context {
@@ -67,6 +74,7 @@ struct ofdis_context {
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
+  int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
@@ -214,8 +222,8 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
   P.off_pw_bw = off;
   if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
   P.off_tv = off;
-  size_t max_sp = 0;  // skewed TV plane (w + h - 1) * h
-  for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, ((size_t)(g.w + g.h - 1) * g.h + 64 + 3) / 4 * 4);
+  size_t max_sp = 0;  // skewed TV plane
+  for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, (size_t)skew_plane(g.w, g.h));
   P.tv_plane = max_sp;
   if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_sp * (14 + 9 * (size_t)P.noc));
   P.total = off;
@@ -360,7 +368,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     const int n_inner = p->tv_innerit * (sl + 1);  // refine_variational.cpp:36
     for (int dir = 0; dir < (bw_level ? 2 : 1) && p->usetvref && n_inner > 0; ++dir) {
       // dir 1: VarRefClass on the backward flow with the images swapped (oflow.cpp:312-316)
-      const long sp = ((long)(g.w + g.h - 1) * g.h + 64 + 3) / 4 * 4;  // + SOR dump slots; 16-B multiple
+      const long sp = skew_plane(g.w, g.h);
       const size_t pl = (size_t)n * sp;
       float *t0 = (float *)(ws + P.off_tv);
       TvArgs tv{};
@@ -375,6 +383,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.wxs = t0 + 12 * pl;
       tv.wys = t0 + 13 * pl;
       tv.sp = sp;
+      tv.wrap = g.h <= g.w;
+      tv.skew_slots = tv.wrap ? g.w * g.h : (g.w + g.h - 1) * g.h;
       float *cp = t0 + 14 * pl;
       const size_t cpl = pl * noc;
       tv.t = cp;
@@ -591,6 +601,7 @@ int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, 
   up.H0 = P.H0;
   up.offx = P.padl;
   up.offy = P.padt;
+  up.nt_store = c->opt_nt_store;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
@@ -782,6 +793,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   }
   if (std::strcmp(key, "wave_per_patch") == 0) {
     c->opt_wave_per_patch = value != 0;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "nt_store") == 0) {
+    c->opt_nt_store = value != 0;
     return OFDIS_OK;
   }
   if (std::strcmp(key, "graph") == 0) {
