@@ -979,6 +979,12 @@ __device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int
   return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
 }
 
+// Load base[idx] through a 32-bit byte offset on a wave-uniform base: global_load's SGPR-base form, no
+// 64-bit address arithmetic per load.  The runtime keeps every TV plane group below 2^30 floats.
+__device__ __forceinline__ float ldu(const float *base, unsigned idx) {
+  return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(base) + (size_t)(idx * 4u));
+}
+
 // decode a skewed-plane thread index; false for holes (unwrapped layout) and the dump slots
 __device__ __forceinline__ bool skew_xy(int kk, int w, int h, int wrap, int &x, int &y) {
   const int t = kk / h;
@@ -1248,16 +1254,16 @@ __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, b
   const int wr = a.wrap;
   const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h, w, wr), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h, w, wr);
   const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h, w, wr), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h, w, wr);
-  const long k5[5] = {idx, kl, kr, ku, kd};
+  const unsigned k5[5] = {(unsigned)idx, (unsigned)kl, (unsigned)kr, (unsigned)ku, (unsigned)kd};
   // gather everything first (one memory round trip), then uu = wx (first iteration) or wx + du
   float wx5[5], du5[5], wy5[5], dv5[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    wx5[i] = a.wxs[k5[i]];
-    du5[i] = a.du[k5[i]];
+    wx5[i] = ldu(a.wxs, k5[i]);
+    du5[i] = ldu(a.du, k5[i]);
     if (NOP == 2) {
-      wy5[i] = a.wys[k5[i]];
-      dv5[i] = a.dv[k5[i]];
+      wy5[i] = ldu(a.wys, k5[i]);
+      dv5[i] = ldu(a.dv, k5[i]);
     }
   }
   float uu5[5], vv5[5];
@@ -1298,25 +1304,27 @@ __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
   if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
   const int w = a.w, h = a.h;
   const bool hasl = x >= 1, hasr = x <= w - 2, hasu = y >= 1, hasd = y <= h - 2;
-  const long f0 = fr * a.sp;
-  const long il = hasl ? f0 + skw(x - 1, y, h, w, a.wrap) : idx, ir = hasr ? f0 + skw(x + 1, y, h, w, a.wrap) : idx;
-  const long iu = hasu ? f0 + skw(x, y - 1, h, w, a.wrap) : idx, id = hasd ? f0 + skw(x, y + 1, h, w, a.wrap) : idx;
+  const unsigned f0 = (unsigned)(fr * a.sp), ui = (unsigned)idx;
+  const unsigned il = hasl ? f0 + (unsigned)skw(x - 1, y, h, w, a.wrap) : ui;
+  const unsigned ir = hasr ? f0 + (unsigned)skw(x + 1, y, h, w, a.wrap) : ui;
+  const unsigned iu = hasu ? f0 + (unsigned)skw(x, y - 1, h, w, a.wrap) : ui;
+  const unsigned id = hasd ? f0 + (unsigned)skw(x, y + 1, h, w, a.wrap) : ui;
   // ---- gather
   const float *S = a.s, *WX = a.wxs, *WY = a.wys;
-  const float sc = S[idx], sl = S[il], sr = S[ir], su = S[iu], sd = S[id];
-  const float xc = WX[idx], xl = WX[il], xr = WX[ir], xu = WX[iu], xd = WX[id];
+  const float sc = ldu(S, ui), sl = ldu(S, il), sr = ldu(S, ir), su = ldu(S, iu), sd = ldu(S, id);
+  const float xc = ldu(WX, ui), xl = ldu(WX, il), xr = ldu(WX, ir), xu = ldu(WX, iu), xd = ldu(WX, id);
   float yc = 0.0f, yl = 0.0f, yr = 0.0f, yu = 0.0f, yd = 0.0f;
   if (NOP == 2) {
-    yc = WY[idx]; yl = WY[il]; yr = WY[ir]; yu = WY[iu]; yd = WY[id];
+    yc = ldu(WY, ui); yl = ldu(WY, il); yr = ldu(WY, ir); yu = ldu(WY, iu); yd = ldu(WY, id);
   }
-  const float m = a.mask[idx], u = a.du[idx], v = NOP == 2 ? a.dv[idx] : 0.0f;
-  const long q = fr * NOC * a.sp + kk;
+  const float m = ldu(a.mask, ui), u = ldu(a.du, ui), v = NOP == 2 ? ldu(a.dv, ui) : 0.0f;
+  const unsigned q = (unsigned)(fr * NOC * a.sp + kk);
   float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
 #pragma unroll
   for (int c = 0; c < NOC; ++c) {
-    const long o = q + c * a.sp;
-    lIx[c] = a.Ix[o]; lIy[c] = a.Iy[o]; lIz[c] = a.Iz[o]; lIxx[c] = a.Ixx[o];
-    lIxy[c] = a.Ixy[o]; lIyy[c] = a.Iyy[o]; lIxz[c] = a.Ixz[o]; lIyz[c] = a.Iyz[o];
+    const unsigned o = q + (unsigned)(c * a.sp);
+    lIx[c] = ldu(a.Ix, o); lIy[c] = ldu(a.Iy, o); lIz[c] = ldu(a.Iz, o); lIxx[c] = ldu(a.Ixx, o);
+    lIxy[c] = ldu(a.Ixy, o); lIyy[c] = ldu(a.Iyy, o); lIxz[c] = ldu(a.Ixz, o); lIyz[c] = ldu(a.Iyz, o);
   }
   // ---- compute
   const float shv = x < w - 1 ? sc + sr : 0.0f;  // h[x] = s[x] + s[x+1]
