@@ -8,8 +8,8 @@
  * (CMakeLists.txt:36-61) and are forwarded as the runtime fields of ofdis_params.
  *
  * Differences, all at the error channel only: the reference never validates and exit(1)s on OOM; this
- * wrapper throws OFC::OFDisError (with the ofdis_status) for invalid parameters, usefbcon = true
- * (not yet built) or a missing gfx950 device.  No CPU fallback exists.
+ * wrapper throws OFC::OFDisError (with the ofdis_status) for invalid parameters or a missing gfx950
+ * device.  No CPU fallback exists.  usefbcon = true runs forward-backward merging on the GPU.
  */
 #ifndef OFDIS_OFLOW_HPP
 #define OFDIS_OFLOW_HPP
