@@ -143,8 +143,12 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        sizes and parameters repeat (re-captured when they change; same bits);
  *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into
  *                        chunks that run round-robin on that many HIP streams with separate workspaces,
- *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels.
- * Results never depend on these settings (frames are independent). */
+ *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels;
+ *   "pipeline" (0/1, default 0): with "chunk" > 0, a two-stream software pipeline instead: one stream runs
+ *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
+ *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
+ * Setting any option drops the captured graph.  Results never depend on these settings (frames are
+ * independent). */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);
 
 /* HIP-event timing of individual kernels on the launch stream (used by bench.py for the roofline). */

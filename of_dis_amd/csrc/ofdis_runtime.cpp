@@ -71,6 +71,7 @@ struct ofdis_context {
     const void *a = nullptr, *b = nullptr, *out = nullptr, *ws = nullptr;
     int n = 0, w = 0, h = 0;
     ofdis_params p{};
+    int pipelined = 0, chunk = 0;
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
@@ -80,6 +81,8 @@ struct ofdis_context {
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
   int opt_streams = 1, opt_chunk = 0;
+  int opt_pipeline = 0;              // two-stream pipeline: streaming stages beside the DIS + TV chain
+  std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
     hipStream_t s = nullptr;
     char *ws = nullptr;
@@ -576,19 +579,15 @@ void ofdis_context_destroy(ofdis_context *c) {
     if (L.s) hipStreamDestroy(L.s);
   }
   if (c->entry) hipEventDestroy(c->entry);
+  for (auto e : c->pipe_ev) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
 namespace {
 
-// One chunk of frames through the whole pipeline on stream s with workspace ws.
-int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
-              const uint8_t *img_b, float *flow_out, hipStream_t s) {
-  int rc = run_pyramid(c, ws, P, img_a, img_b, s);
-  if (rc) return rc;
-  rc = run_levels(c, ws, P, p, s, nullptr, nullptr);
-  if (rc) return rc;
+// x 2^sc_l + INTER_LINEAR upsample + crop of the finest level's flow in workspace ws (run_dense.cpp:407-415).
+int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, float *flow_out, hipStream_t s) {
   UpArgs up{};
   up.flow = (const float *)(ws + P.off_flow[0]);
   up.out = flow_out;
@@ -604,6 +603,16 @@ int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, 
   up.nt_store = c->opt_nt_store;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+}
+
+// One chunk of frames through the whole pipeline on stream s with workspace ws.
+int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
+              const uint8_t *img_b, float *flow_out, hipStream_t s) {
+  int rc = run_pyramid(c, ws, P, img_a, img_b, s);
+  if (rc) return rc;
+  rc = run_levels(c, ws, P, p, s, nullptr, nullptr);
+  if (rc) return rc;
+  return run_upsample(c, ws, P, p, flow_out, s);
 }
 
 int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
@@ -627,6 +636,86 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
   return OFDIS_OK;
 }
 
+// Chunks round-robin over opt_streams streams, each chunk's whole pipeline on one stream ("streams").
+int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
+                    const uint8_t *img_b, float *flow_out, int n, int width, int height, int chunk) {
+  const int nchunks = (n + chunk - 1) / chunk;
+  const int k = std::min(c->opt_streams, nchunks);
+  Plan PC = batch_plan(p, chunk, width, height);
+  int rc = ensure_lanes(c, k, PC.total);
+  if (rc) return rc;
+  HIP_OK(hipEventRecord(c->entry, s));
+  for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
+  const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * PC.nop;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int f0 = ch * chunk, m = std::min(chunk, n - f0);
+    auto &L = c->lanes[ch % k];
+    Plan PM = m == chunk ? PC : batch_plan(p, m, width, height);
+    rc = run_chunk(c, L.ws, PM, p, img_a + f0 * in_frame, img_b + f0 * in_frame, flow_out + f0 * out_frame, L.s);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < k; ++i) {
+    HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
+    HIP_OK(hipStreamWaitEvent(s, c->lanes[i].done, 0));
+  }
+  return OFDIS_OK;
+}
+
+int pipeline_resources(ofdis_context *c, const ofdis_params *p, int width, int height, int chunk, int nchunks) {
+  int rc = ensure_lanes(c, 2, batch_plan(p, chunk, width, height).total);
+  if (rc) return rc;
+  while ((int)c->pipe_ev.size() < 2 * nchunks) {
+    hipEvent_t e = nullptr;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->pipe_ev.push_back(e);
+  }
+  return OFDIS_OK;
+}
+
+// Two-stream software pipeline over chunks ("pipeline" option).  Lane 0 runs the HBM-streaming stages --
+// the pyramid from the u8 frames and the full-resolution upsample -- and lane 1 the latency-bound
+// DIS + TV chain (run_levels), so chunk ch's chain overlaps chunk ch+1's pyramid and chunk ch-1's
+// upsample.  Issue order on lane 0: pyr 0, pyr 1, up 0, pyr 2, up 1, ...; chunk ch uses workspace
+// ch % 2, which pyr(ch+2) reuses only after up(ch) (same stream, issued before it), which waits for
+// levels(ch).  Every hand-over is an event, so each kernel sees the data of the single-stream order.
+int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
+                  const uint8_t *img_b, float *flow_out, int n, int width, int height, int chunk) {
+  const int nchunks = (n + chunk - 1) / chunk;
+  int rc = pipeline_resources(c, p, width, height, chunk, nchunks);
+  if (rc) return rc;
+  std::vector<Plan> plans;
+  plans.reserve(nchunks);
+  for (int ch = 0; ch < nchunks; ++ch) plans.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height));
+  const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * plans[0].nop;
+  hipStream_t S = c->lanes[0].s, L = c->lanes[1].s;
+  hipEvent_t *ev_pyr = c->pipe_ev.data(), *ev_lev = c->pipe_ev.data() + nchunks;
+  HIP_OK(hipEventRecord(c->entry, s));
+  HIP_OK(hipStreamWaitEvent(S, c->entry, 0));
+  HIP_OK(hipStreamWaitEvent(L, c->entry, 0));
+  auto pyr = [&](int ch) -> int {
+    const size_t f0 = (size_t)ch * chunk;
+    int r = run_pyramid(c, c->lanes[ch & 1].ws, plans[ch], img_a + f0 * in_frame, img_b + f0 * in_frame, S);
+    if (r) return r;
+    HIP_OK(hipEventRecord(ev_pyr[ch], S));
+    return OFDIS_OK;
+  };
+  if ((rc = pyr(0))) return rc;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    char *ws = c->lanes[ch & 1].ws;
+    HIP_OK(hipStreamWaitEvent(L, ev_pyr[ch], 0));
+    if ((rc = run_levels(c, ws, plans[ch], p, L, nullptr, nullptr))) return rc;
+    HIP_OK(hipEventRecord(ev_lev[ch], L));
+    if (ch + 1 < nchunks && (rc = pyr(ch + 1))) return rc;
+    HIP_OK(hipStreamWaitEvent(S, ev_lev[ch], 0));
+    if ((rc = run_upsample(c, ws, plans[ch], p, flow_out + (size_t)ch * chunk * out_frame, S))) return rc;
+  }
+  for (int i = 0; i < 2; ++i) {
+    HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
+    HIP_OK(hipStreamWaitEvent(s, c->lanes[i].done, 0));
+  }
+  return OFDIS_OK;
+}
+
 }  // namespace
 
 int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width, int height,
@@ -641,63 +730,58 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
   rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
   if (rc) return rc;
   const bool capturing = !c->cap_dis.empty() || !c->cap_tv.empty();
-  const int chunk = c->opt_chunk > 0 ? c->opt_chunk : n;
+  const int chunk = c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : n;
   const int nchunks = (n + chunk - 1) / chunk;
-  if (c->opt_streams <= 1 || nchunks <= 1 || capturing) {
+  // pipelined: the streaming stages of neighbouring chunks overlap the DIS + TV chain of the current one
+  const bool pipelined = c->opt_pipeline && nchunks > 1 && !capturing && !c->timing;
+  if (!pipelined && (c->opt_streams > 1 && nchunks > 1 && !capturing))
+    return run_round_robin(c, s, p, img_a, img_b, flow_out, n, width, height, chunk);
+  if (!pipelined) {
     rc = ensure_ws(c, P.total);
     if (rc) return rc;
-    if (!c->opt_graph || capturing || c->timing) return run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, s);
-    // ~80 dependent launches per batch: record them once as a HIP graph (on the context's own stream --
-    // the caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's
-    // stream while the pointers, sizes and parameters stay the same.
-    ofdis_context::GraphKey key;
-    std::memset(&key, 0, sizeof(key));  // padding included: the key is compared bytewise
-    key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = c->ws;
-    key.n = n; key.w = width; key.h = height; key.p = *p;
-    if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
-      if (c->gexec) {  // the previous graph may still be running on a caller stream
-        HIP_OK(hipDeviceSynchronize());
-        HIP_OK(hipGraphExecDestroy(c->gexec));
-        c->gexec = nullptr;
-      }
-      hipGraph_t graph = nullptr;
-      HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-      rc = run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, c->stream);
-      const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
-      if (rc) {
-        if (graph) hipGraphDestroy(graph);
-        return rc;
-      }
-      if (ce != hipSuccess || !graph) return OFDIS_ERR_DEVICE;
-      const hipError_t ie = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
-      hipGraphDestroy(graph);
-      if (ie != hipSuccess) {
-        c->gexec = nullptr;
-        return OFDIS_ERR_DEVICE;
-      }
-      std::memcpy(&c->gkey, &key, sizeof(key));
+  }
+  auto issue = [&](hipStream_t st) {
+    return pipelined ? run_pipelined(c, st, p, img_a, img_b, flow_out, n, width, height, chunk)
+                     : run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, st);
+  };
+  if (!c->opt_graph || capturing || c->timing) return issue(s);
+  // ~80 dependent launches per chunk: record them once as a HIP graph (on the context's own stream --
+  // the caller's may be the legacy NULL stream, which cannot capture; the pipeline's two streams join the
+  // capture through its entry event) and replay it on the caller's stream while the pointers, sizes,
+  // parameters and options stay the same (set_option drops the graph).
+  ofdis_context::GraphKey key;
+  std::memset(&key, 0, sizeof(key));  // padding included: the key is compared bytewise
+  key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = pipelined ? nullptr : c->ws;
+  key.n = n; key.w = width; key.h = height; key.p = *p;
+  key.pipelined = pipelined; key.chunk = chunk;
+  if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
+    if (c->gexec) {  // the previous graph may still be running on a caller stream
+      HIP_OK(hipDeviceSynchronize());
+      HIP_OK(hipGraphExecDestroy(c->gexec));
+      c->gexec = nullptr;
     }
-    HIP_OK(hipGraphLaunch(c->gexec, s));
-    return OFDIS_OK;
+    if (pipelined) {  // allocate lanes / events outside the capture
+      rc = pipeline_resources(c, p, width, height, chunk, nchunks);
+      if (rc) return rc;
+    }
+    hipGraph_t graph = nullptr;
+    HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    rc = issue(c->stream);
+    const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
+    if (rc) {
+      if (graph) hipGraphDestroy(graph);
+      return rc;
+    }
+    if (ce != hipSuccess || !graph) return OFDIS_ERR_DEVICE;
+    const hipError_t ie = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    if (ie != hipSuccess) {
+      c->gexec = nullptr;
+      return OFDIS_ERR_DEVICE;
+    }
+    std::memcpy(&c->gkey, &key, sizeof(key));
   }
-  const int k = std::min(c->opt_streams, nchunks);
-  Plan PC = batch_plan(p, chunk, width, height);
-  rc = ensure_lanes(c, k, PC.total);
-  if (rc) return rc;
-  HIP_OK(hipEventRecord(c->entry, s));
-  for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
-  const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * P.nop;
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int f0 = ch * chunk, m = std::min(chunk, n - f0);
-    auto &L = c->lanes[ch % k];
-    Plan PM = m == chunk ? PC : batch_plan(p, m, width, height);
-    rc = run_chunk(c, L.ws, PM, p, img_a + f0 * in_frame, img_b + f0 * in_frame, flow_out + f0 * out_frame, L.s);
-    if (rc) return rc;
-  }
-  for (int i = 0; i < k; ++i) {
-    HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
-    HIP_OK(hipStreamWaitEvent(s, c->lanes[i].done, 0));
-  }
+  HIP_OK(hipGraphLaunch(c->gexec, s));
   return OFDIS_OK;
 }
 
@@ -783,6 +867,16 @@ int ofdis_context_set_stage_capture(ofdis_context *c, float *const *dis_flow, fl
 int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   if (!c || !key) return OFDIS_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lock(c->mu);
+  if (c->gexec) {  // a captured graph bakes in the options it was recorded with
+    HIP_OK(hipSetDevice(c->device));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipGraphExecDestroy(c->gexec));
+    c->gexec = nullptr;
+  }
+  if (std::strcmp(key, "pipeline") == 0) {
+    c->opt_pipeline = value != 0;
+    return OFDIS_OK;
+  }
   if (std::strcmp(key, "sor_generic") == 0) {
     c->opt_sor_generic = value != 0;
     return OFDIS_OK;

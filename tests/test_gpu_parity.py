@@ -166,17 +166,22 @@ def test_batch_equals_singles(od, ctx):
     b = torch.from_numpy(np.stack([x[1] for x in pairs])).cuda()
     p = od.oppoint(2, w, 1, 1)
     outs = []
-    for streams, chunk, graph in ((1, 0, 1), (1, 0, 1), (1, 0, 0), (3, 2, 1), (4, 1, 1)):
-        # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams
+    configs = ((1, 0, 1, 0), (1, 0, 1, 0), (1, 0, 0, 0), (3, 2, 1, 0), (4, 1, 1, 0),
+               (1, 2, 1, 1), (1, 2, 1, 1), (1, 2, 0, 1), (1, 1, 1, 1), (1, 3, 0, 1))
+    for streams, chunk, graph, pipeline in configs:
+        # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams;
+        # the two-stream pipeline (ragged last chunk; captured + replayed, and eager)
         ctx.set_option("streams", streams)
         ctx.set_option("chunk", chunk)
         ctx.set_option("graph", graph)
+        ctx.set_option("pipeline", pipeline)
         o = ctx.run(a, b, p)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
     ctx.set_option("graph", 1)
     ctx.set_option("streams", 1)
     ctx.set_option("chunk", 0)
+    ctx.set_option("pipeline", 0)
     for f in range(n):
         single = ctx.run_host(pairs[f][0], pairs[f][1], p)
         for k, out in enumerate(outs):
