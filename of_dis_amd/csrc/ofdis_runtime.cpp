@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -71,7 +72,6 @@ struct ofdis_context {
     const void *a = nullptr, *b = nullptr, *out = nullptr, *ws = nullptr;
     int n = 0, w = 0, h = 0;
     ofdis_params p{};
-    int pipelined = 0, chunk = 0;
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
@@ -95,6 +95,20 @@ struct ofdis_context {
 };
 
 namespace {
+
+// OFDIS_TRACE=1: host-side progress lines on stderr (debugging the multi-stream paths)
+bool trace_on() {
+  static const bool on = std::getenv("OFDIS_TRACE") && std::getenv("OFDIS_TRACE")[0] == '1';
+  return on;
+}
+#define OFDIS_TRACE(...)                  \
+  do {                                    \
+    if (trace_on()) {                     \
+      std::fprintf(stderr, "ofdis: " __VA_ARGS__); \
+      std::fputc('\n', stderr);           \
+      std::fflush(stderr);                \
+    }                                     \
+  } while (0)
 
 #define HIP_OK(x)                                                                                \
   do {                                                                                           \
@@ -699,11 +713,17 @@ int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const 
     HIP_OK(hipEventRecord(ev_pyr[ch], S));
     return OFDIS_OK;
   };
+  static const bool dbg_sync = std::getenv("OFDIS_PIPE_SYNC") && std::getenv("OFDIS_PIPE_SYNC")[0] == '1';
+  OFDIS_TRACE("pipeline: %d chunks of %d, lanes ws %p %p", nchunks, chunk, (void *)c->lanes[0].ws,
+              (void *)c->lanes[1].ws);
   if ((rc = pyr(0))) return rc;
   for (int ch = 0; ch < nchunks; ++ch) {
     char *ws = c->lanes[ch & 1].ws;
+    OFDIS_TRACE("pipeline: chunk %d (%d frames)", ch, plans[ch].n);
     HIP_OK(hipStreamWaitEvent(L, ev_pyr[ch], 0));
+    if (dbg_sync) HIP_OK(hipDeviceSynchronize());
     if ((rc = run_levels(c, ws, plans[ch], p, L, nullptr, nullptr))) return rc;
+    if (dbg_sync) HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipEventRecord(ev_lev[ch], L));
     if (ch + 1 < nchunks && (rc = pyr(ch + 1))) return rc;
     HIP_OK(hipStreamWaitEvent(S, ev_lev[ch], 0));
@@ -744,30 +764,29 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
     return pipelined ? run_pipelined(c, st, p, img_a, img_b, flow_out, n, width, height, chunk)
                      : run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, st);
   };
-  if (!c->opt_graph || capturing || c->timing) return issue(s);
-  // ~80 dependent launches per chunk: record them once as a HIP graph (on the context's own stream --
-  // the caller's may be the legacy NULL stream, which cannot capture; the pipeline's two streams join the
-  // capture through its entry event) and replay it on the caller's stream while the pointers, sizes,
-  // parameters and options stay the same (set_option drops the graph).
+  // The pipeline is issued eagerly: its two streams would have to join the capture through events, which
+  // this HIP runtime does not survive (hipStreamEndCapture faults); eager and graph kernel boundaries
+  // cost the same on one stream, and the host issues far ahead of the device.
+  if (!c->opt_graph || capturing || c->timing || pipelined) return issue(s);
+  // ~80 dependent launches per batch: record them once as a HIP graph (on the context's own stream --
+  // the caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's
+  // stream while the pointers, sizes, parameters and options stay the same (set_option drops the graph).
   ofdis_context::GraphKey key;
   std::memset(&key, 0, sizeof(key));  // padding included: the key is compared bytewise
-  key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = pipelined ? nullptr : c->ws;
+  key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = c->ws;
   key.n = n; key.w = width; key.h = height; key.p = *p;
-  key.pipelined = pipelined; key.chunk = chunk;
   if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
     if (c->gexec) {  // the previous graph may still be running on a caller stream
       HIP_OK(hipDeviceSynchronize());
       HIP_OK(hipGraphExecDestroy(c->gexec));
       c->gexec = nullptr;
     }
-    if (pipelined) {  // allocate lanes / events outside the capture
-      rc = pipeline_resources(c, p, width, height, chunk, nchunks);
-      if (rc) return rc;
-    }
     hipGraph_t graph = nullptr;
+    OFDIS_TRACE("graph: capture (pipelined %d, chunk %d)", (int)pipelined, chunk);
     HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     rc = issue(c->stream);
     const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
+    OFDIS_TRACE("graph: captured rc %d end %d", rc, (int)ce);
     if (rc) {
       if (graph) hipGraphDestroy(graph);
       return rc;
@@ -781,6 +800,7 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
     }
     std::memcpy(&c->gkey, &key, sizeof(key));
   }
+  OFDIS_TRACE("graph: launch");
   HIP_OK(hipGraphLaunch(c->gexec, s));
   return OFDIS_OK;
 }

@@ -161,6 +161,10 @@ class Context:
             out = torch.empty((n, h, w, p.nop), dtype=torch.float32, device=a.device)
         stream = torch.cuda.current_stream(a.device).cuda_stream
         self.run_ptr(a.data_ptr(), b.data_ptr(), n, w, h, p, out.data_ptr(), stream)
+        if not stream:
+            # torch's default stream is the legacy NULL stream, which the C-ABI reads as "the context's own
+            # (non-blocking) stream": nothing would order later torch work after the flow, so wait here.
+            torch.cuda.synchronize(a.device)
         return out
 
     def run_host(self, a: np.ndarray, b: np.ndarray, p: Params) -> np.ndarray:
