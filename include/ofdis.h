@@ -171,6 +171,12 @@ int ofdis_write_pfm(const char *path, const float *depth, int width, int height)
 int ofdis_read_flo(const char *path, float *flow, int *width, int *height, int nc);
 /* Binary PGM (P5, noc = 1) / PPM (P6, noc = 3, returned in BGR order like cv::imread). */
 int ofdis_read_pnm(const char *path, uint8_t *pixels, int *width, int *height, int *noc, size_t capacity);
+/* cv::imread(path, want_noc == 1 ? CV_LOAD_IMAGE_GRAYSCALE : CV_LOAD_IMAGE_COLOR) (run_dense.cpp:202-206)
+ * for PNG (zlib inflate; gray / RGB / palette / alpha, 1-16 bit, Adam7; libpng's transform chain as
+ * OpenCV configures it, incl. png_set_rgb_to_gray(0.299, 0.587)) and Netpbm P1-P6 (colour -> gray with
+ * OpenCV's fixed-point BGR2Gray).  Output [h][w][want_noc], BGR for 3.  pixels may be NULL to query the
+ * size.  OFDIS_ERR_UNSUPPORTED for other formats (JPEG, BMP, ...), OFDIS_ERR_IO for corrupt files. */
+int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height, int want_noc, size_t capacity);
 
 /* Deterministic synthetic frame pair: band-limited texture + noise, frame b is frame
  * a moved along a known smooth flow (OF) or a horizontal disparity (DE).  Host buffers [h][w][noc]. */

@@ -111,6 +111,7 @@ def lib():
         "ofdis_write_pfm": ([C.c_char_p, vp, i, i], i),
         "ofdis_read_flo": ([C.c_char_p, vp, C.POINTER(i), C.POINTER(i), i], i),
         "ofdis_read_pnm": ([C.c_char_p, vp, C.POINTER(i), C.POINTER(i), C.POINTER(i), C.c_size_t], i),
+        "ofdis_read_image": ([C.c_char_p, vp, C.POINTER(i), C.POINTER(i), i, C.c_size_t], i),
         "ofdis_synth_pair_u8": ([vp, vp, i, i, i, i, i], i),
     }
     for name, (args, res) in sig.items():

@@ -1,0 +1,380 @@
+// ofdis_image.cpp -- the on-disk image formats on the input side of the path: what run_dense.cpp's
+// cv::imread(path, CV_LOAD_IMAGE_GRAYSCALE / CV_LOAD_IMAGE_COLOR) (run_dense.cpp:202-206) returns, for
+// PNG and the Netpbm family, without OpenCV or libpng (neither is in the image; zlib is).
+//
+// Restated semantics (OpenCV 3.x/4.x grfmt_png.cpp / grfmt_pxm.cpp over libpng 1.6; both absent here, so
+// parity with them is unpinned and pinned instead by tests/test_image_io.py's independent decodes):
+//   PNG  every colour type (gray, RGB, palette, gray+alpha, RGBA), bit depths 1/2/4/8/16, Adam7.  The
+//        transforms OpenCV asks libpng for, in libpng's order: palette -> RGB, gray 1/2/4 -> 8 bit
+//        (x255 / x85 / x17), alpha stripped (not composited), then RGB -> gray (png_set_rgb_to_gray with
+//        0.299 / 0.587 -> 15-bit coefficients 9797 / 19234 / 3737: truncating for 8 bit, rounded for 16
+//        bit, through libpng's 8-bit gamma tables when a gAMA / sRGB chunk makes the file gamma
+//        significant), or gray -> RGB by replication; 16 bit -> 8 bit keeps the high byte
+//        (png_set_strip_16); colour output is BGR (png_set_bgr).  CRCs of critical chunks are checked.
+//   PNM  P1-P6 (ASCII and binary bitmaps / graymaps / pixmaps), maxval <= 255 taken as is, 65535 -> high
+//        byte; colour -> gray by OpenCV's fixed-point icvCvt_BGR2Gray_8u_C3C1R
+//        ((1868 B + 9617 G + 4899 R + 8192) >> 14); colour output is BGR.
+#include <zlib.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/ofdis.h"
+
+namespace {
+
+struct Image {
+  int w = 0, h = 0, c = 0;  // c = 1 or 3 (BGR), 8 bit
+  std::vector<uint8_t> px;
+};
+
+bool read_file(const char *path, std::vector<uint8_t> &buf) {
+  FILE *f = std::fopen(path, "rb");
+  if (!f) return false;
+  uint8_t tmp[1 << 16];
+  size_t k;
+  while ((k = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + k);
+  const bool ok = !std::ferror(f);
+  std::fclose(f);
+  return ok;
+}
+
+// ------------------------------------------------------------------------------------------- PNG
+
+inline uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+// png_gamma_8bit_correct (libpng png.c): floor(255 * (v/255)^(g/1e5) + .5) for 0 < v < 255.
+uint8_t gamma8(unsigned v, double g) {
+  if (v == 0 || v >= 255) return (uint8_t)v;
+  return (uint8_t)std::floor(255.0 * std::pow(v / 255.0, g * 0.00001) + 0.5);
+}
+// png_reciprocal: floor(1e10 / a + .5)
+long reciprocal(long a) { return (long)std::floor(1e10 / (double)a + 0.5); }
+bool gamma_significant(long g) { return g < 100000 - 5000 || g > 100000 + 5000; }
+
+int paeth(int a, int b, int c) {
+  const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+  if (pa <= pb && pa <= pc) return a;
+  return pb <= pc ? b : c;
+}
+
+// Reverse the per-row filters of one (sub-)image in place; rows of `rb` bytes, `bpp` bytes per pixel
+// (at least 1).  Returns false on an unknown filter type.
+bool unfilter(uint8_t *data, int rows, size_t rb, int bpp) {
+  std::vector<uint8_t> prev(rb, 0);
+  uint8_t *out = data;  // rows are compacted in place: out lags the input by one byte per row
+  const uint8_t *in = data;
+  for (int y = 0; y < rows; ++y) {
+    const int ft = *in++;
+    uint8_t *cur = out;
+    std::memmove(cur, in, rb);
+    in += rb;
+    for (size_t i = 0; i < rb; ++i) {
+      const int a = i >= (size_t)bpp ? cur[i - bpp] : 0, b = prev[i], c = i >= (size_t)bpp ? prev[i - bpp] : 0;
+      int v = cur[i];
+      switch (ft) {
+        case 0: break;
+        case 1: v += a; break;
+        case 2: v += b; break;
+        case 3: v += (a + b) >> 1; break;
+        case 4: v += paeth(a, b, c); break;
+        default: return false;
+      }
+      cur[i] = (uint8_t)v;
+    }
+    std::memcpy(prev.data(), cur, rb);
+    out += rb;
+  }
+  return true;
+}
+
+// Sample s of row `row` (unpacked, big-endian for 16 bit) -> value in [0, 2^depth).
+inline unsigned sample(const uint8_t *row, size_t s, int depth) {
+  switch (depth) {
+    case 16: return (unsigned)row[2 * s] << 8 | row[2 * s + 1];
+    case 8: return row[s];
+    default: {
+      const size_t bit = s * depth;
+      return (row[bit >> 3] >> (8 - depth - (bit & 7))) & ((1u << depth) - 1);
+    }
+  }
+}
+
+int decode_png(const std::vector<uint8_t> &f, int want, Image &img) {
+  static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+  if (f.size() < 8 || std::memcmp(f.data(), sig, 8) != 0) return OFDIS_ERR_IO;
+  uint32_t W = 0, H = 0;
+  int depth = 0, ctype = -1, interlace = 0;
+  std::vector<uint8_t> idat, plte;
+  long file_gamma = 0;  // 1e5 units, 0 = none
+  bool srgb = false, seen_ihdr = false, seen_iend = false;
+  size_t pos = 8;
+  while (pos + 12 <= f.size()) {
+    const uint32_t len = be32(&f[pos]);
+    if (len > f.size() - pos - 12) return OFDIS_ERR_IO;
+    const uint8_t *type = &f[pos + 4], *data = &f[pos + 8];
+    const bool critical = !(type[0] & 0x20);
+    const uint32_t crc = be32(&f[pos + 8 + len]);
+    if (critical && (uint32_t)crc32(crc32(0L, Z_NULL, 0), type, len + 4) != crc) return OFDIS_ERR_IO;
+    if (!std::memcmp(type, "IHDR", 4)) {
+      if (len != 13) return OFDIS_ERR_IO;
+      W = be32(data);
+      H = be32(data + 4);
+      depth = data[8];
+      ctype = data[9];
+      interlace = data[12];
+      if (data[10] != 0 || data[11] != 0 || interlace > 1) return OFDIS_ERR_IO;
+      seen_ihdr = true;
+    } else if (!std::memcmp(type, "PLTE", 4)) {
+      plte.assign(data, data + len);
+    } else if (!std::memcmp(type, "IDAT", 4)) {
+      idat.insert(idat.end(), data, data + len);
+    } else if (!std::memcmp(type, "gAMA", 4)) {
+      if (len == 4) file_gamma = (long)be32(data);
+    } else if (!std::memcmp(type, "sRGB", 4)) {
+      srgb = true;
+    } else if (!std::memcmp(type, "IEND", 4)) {
+      seen_iend = true;
+      break;
+    }
+    pos += 12 + len;
+  }
+  if (!seen_ihdr || !seen_iend || W == 0 || H == 0 || W > (1u << 24) || H > (1u << 24)) return OFDIS_ERR_IO;
+  int nch;
+  switch (ctype) {
+    case 0: nch = 1; if (depth != 1 && depth != 2 && depth != 4 && depth != 8 && depth != 16) return OFDIS_ERR_IO; break;
+    case 2: nch = 3; if (depth != 8 && depth != 16) return OFDIS_ERR_IO; break;
+    case 3: nch = 1; if (depth != 1 && depth != 2 && depth != 4 && depth != 8) return OFDIS_ERR_IO; break;
+    case 4: nch = 2; if (depth != 8 && depth != 16) return OFDIS_ERR_IO; break;
+    case 6: nch = 4; if (depth != 8 && depth != 16) return OFDIS_ERR_IO; break;
+    default: return OFDIS_ERR_IO;
+  }
+  if (ctype == 3 && (plte.empty() || plte.size() % 3)) return OFDIS_ERR_IO;
+  const int bpp = std::max(1, nch * depth / 8);
+  auto row_bytes = [&](uint32_t w) { return ((size_t)w * nch * depth + 7) / 8; };
+
+  // inflate: the exact size of the filtered stream is known
+  static const int ax0[7] = {0, 4, 0, 2, 0, 1, 0}, ay0[7] = {0, 0, 4, 0, 2, 0, 1};
+  static const int adx[7] = {8, 8, 4, 4, 2, 2, 1}, ady[7] = {8, 8, 8, 4, 4, 2, 2};
+  size_t raw_size = 0;
+  if (!interlace) {
+    raw_size = (row_bytes(W) + 1) * H;
+  } else {
+    for (int pss = 0; pss < 7; ++pss) {
+      const uint32_t pw = (W + adx[pss] - 1 - ax0[pss]) / adx[pss], ph = (H + ady[pss] - 1 - ay0[pss]) / ady[pss];
+      if (pw && ph) raw_size += (row_bytes(pw) + 1) * ph;
+    }
+  }
+  std::vector<uint8_t> raw(raw_size + 1);
+  z_stream zs;
+  std::memset(&zs, 0, sizeof(zs));
+  if (inflateInit(&zs) != Z_OK) return OFDIS_ERR_OUT_OF_MEMORY;
+  zs.next_in = idat.data();
+  zs.avail_in = (uInt)idat.size();
+  zs.next_out = raw.data();
+  zs.avail_out = (uInt)raw.size();
+  const int zr = inflate(&zs, Z_FINISH);
+  const size_t got = raw.size() - zs.avail_out;
+  inflateEnd(&zs);
+  if ((zr != Z_STREAM_END && zr != Z_BUF_ERROR) || got < raw_size) return OFDIS_ERR_IO;
+
+  // unfilter and de-interlace into full-size unpacked rows of samples (16-bit values kept)
+  std::vector<uint16_t> smp((size_t)W * H * nch);
+  auto put_rows = [&](uint8_t *sub, uint32_t pw, uint32_t ph, int x0, int y0, int dx, int dy) -> bool {
+    const size_t rb = row_bytes(pw);
+    if (!unfilter(sub, (int)ph, rb, bpp)) return false;
+    for (uint32_t y = 0; y < ph; ++y) {
+      const uint8_t *r = sub + y * rb;
+      uint16_t *dst = &smp[((size_t)(y0 + y * dy) * W) * nch];
+      for (uint32_t x = 0; x < pw; ++x)
+        for (int k = 0; k < nch; ++k) dst[(size_t)(x0 + x * dx) * nch + k] = (uint16_t)sample(r, (size_t)x * nch + k, depth);
+    }
+    return true;
+  };
+  if (!interlace) {
+    if (!put_rows(raw.data(), W, H, 0, 0, 1, 1)) return OFDIS_ERR_IO;
+  } else {
+    uint8_t *p = raw.data();
+    for (int pss = 0; pss < 7; ++pss) {
+      const uint32_t pw = (W + adx[pss] - 1 - ax0[pss]) / adx[pss], ph = (H + ady[pss] - 1 - ay0[pss]) / ady[pss];
+      if (!pw || !ph) continue;
+      if (!put_rows(p, pw, ph, ax0[pss], ay0[pss], adx[pss], ady[pss])) return OFDIS_ERR_IO;
+      p += (row_bytes(pw) + 1) * ph;
+    }
+  }
+
+  // libpng's transform chain as OpenCV configures it
+  const bool color_src = (ctype & 2) != 0;  // PNG_COLOR_MASK_COLOR (palette included)
+  const bool d16 = depth == 16;
+  // gamma: png_init_read_transformations -- no gAMA/sRGB: gamma = screen = 1 (tables unused)
+  long g = file_gamma > 0 ? file_gamma : (srgb ? 45455 : 0);
+  const bool use_gamma = color_src && want == 1 && g > 0 && gamma_significant(g);
+  if (use_gamma && d16) return OFDIS_ERR_UNSUPPORTED;  // libpng's 16-bit gamma tables: not restated
+  uint8_t to1[256], from1[256];
+  if (use_gamma) {
+    const long screen = reciprocal(g);  // "assume the output matches the input"
+    const long g_to1 = reciprocal(g), g_from1 = reciprocal(screen);
+    for (unsigned v = 0; v < 256; ++v) {
+      to1[v] = gamma_significant(g_to1) ? gamma8(v, (double)g_to1) : (uint8_t)v;
+      from1[v] = gamma_significant(g_from1) ? gamma8(v, (double)g_from1) : (uint8_t)v;
+    }
+  }
+  const uint32_t rc = 9797, gc = 19234, bc = 32768 - rc - gc;  // png_set_rgb_to_gray(png, 1, 0.299, 0.587)
+  img.w = (int)W;
+  img.h = (int)H;
+  img.c = want;
+  img.px.assign((size_t)W * H * want, 0);
+  for (size_t i = 0; i < (size_t)W * H; ++i) {
+    const uint16_t *s = &smp[i * nch];
+    unsigned r, gg, b;  // at the stream's depth after expansion (8, or 16 for 16-bit files)
+    if (ctype == 3) {
+      const unsigned idx = s[0];
+      if ((size_t)idx * 3 + 2 >= plte.size()) return OFDIS_ERR_IO;
+      r = plte[3 * idx]; gg = plte[3 * idx + 1]; b = plte[3 * idx + 2];
+    } else if (color_src) {
+      r = s[0]; gg = s[1]; b = s[2];
+    } else {
+      unsigned v = s[0];
+      if (depth < 8) v *= depth == 1 ? 255 : (depth == 2 ? 0x55 : 0x11);  // png_do_expand
+      r = gg = b = v;
+    }
+    if (want == 1) {
+      unsigned gray;
+      if (!color_src) {
+        gray = r;
+      } else if (d16) {
+        gray = (rc * r + gc * gg + bc * b + 16384) >> 15;  // 16-bit: rounded (libpng >= 1.5.5)
+      } else if (r == gg && r == b) {
+        gray = r;
+      } else if (use_gamma) {
+        gray = from1[(rc * to1[r] + gc * to1[gg] + bc * to1[b] + 16384) >> 15];
+      } else {
+        gray = (rc * r + gc * gg + bc * b) >> 15;  // "the historical approach which simply truncates"
+      }
+      img.px[i] = (uint8_t)(d16 ? gray >> 8 : gray);  // png_set_strip_16
+    } else {
+      uint8_t *d = &img.px[i * 3];
+      d[0] = (uint8_t)(d16 ? b >> 8 : b);  // png_set_bgr
+      d[1] = (uint8_t)(d16 ? gg >> 8 : gg);
+      d[2] = (uint8_t)(d16 ? r >> 8 : r);
+    }
+  }
+  return OFDIS_OK;
+}
+
+// ------------------------------------------------------------------------------------------- PNM
+
+struct Cursor {
+  const std::vector<uint8_t> &f;
+  size_t p = 0;
+  int token() {  // next decimal integer, skipping whitespace and # comments; -1 on error
+    while (p < f.size()) {
+      const int c = f[p];
+      if (c == '#') {
+        while (p < f.size() && f[p] != '\n' && f[p] != '\r') ++p;
+      } else if (c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f') {
+        ++p;
+      } else {
+        break;
+      }
+    }
+    if (p >= f.size() || f[p] < '0' || f[p] > '9') return -1;
+    long v = 0;
+    while (p < f.size() && f[p] >= '0' && f[p] <= '9') {
+      v = v * 10 + (f[p++] - '0');
+      if (v > (1 << 24)) return -1;
+    }
+    return (int)v;
+  }
+};
+
+int decode_pnm(const std::vector<uint8_t> &f, int want, Image &img) {
+  if (f.size() < 3 || f[0] != 'P' || f[1] < '1' || f[1] > '6') return OFDIS_ERR_IO;
+  const int kind = f[1] - '0';
+  const bool ascii = kind <= 3, bitmap = kind == 1 || kind == 4;
+  const int nch = (kind == 3 || kind == 6) ? 3 : 1;
+  Cursor cur{f, 2};
+  const int w = cur.token(), h = cur.token();
+  const int maxv = bitmap ? 1 : cur.token();
+  if (w <= 0 || h <= 0 || maxv <= 0 || (maxv > 255 && maxv != 65535)) return OFDIS_ERR_IO;
+  const size_t n = (size_t)w * h * nch;
+  std::vector<unsigned> v(n);
+  if (ascii) {
+    for (size_t i = 0; i < n; ++i) {
+      if (kind == 1) {  // P1 digits may be unseparated
+        while (cur.p < f.size() && !(f[cur.p] == '0' || f[cur.p] == '1')) {
+          if (f[cur.p] == '#')
+            while (cur.p < f.size() && f[cur.p] != '\n') ++cur.p;
+          else
+            ++cur.p;
+        }
+        if (cur.p >= f.size()) return OFDIS_ERR_IO;
+        v[i] = f[cur.p++] == '1' ? 0 : 255;  // PBM: 1 = black
+      } else {
+        const int t = cur.token();
+        if (t < 0 || t > maxv) return OFDIS_ERR_IO;
+        v[i] = maxv == 65535 ? (unsigned)t >> 8 : (unsigned)t;
+      }
+    }
+  } else {
+    size_t p = cur.p + 1;  // exactly one whitespace byte after the header
+    if (kind == 4) {
+      const size_t rb = ((size_t)w + 7) / 8;
+      if (p + rb * h > f.size()) return OFDIS_ERR_IO;
+      for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) v[(size_t)y * w + x] = (f[p + y * rb + (x >> 3)] >> (7 - (x & 7))) & 1 ? 0 : 255;
+    } else if (maxv == 65535) {
+      if (p + 2 * n > f.size()) return OFDIS_ERR_IO;
+      for (size_t i = 0; i < n; ++i) v[i] = f[p + 2 * i];  // high byte of the big-endian sample
+    } else {
+      if (p + n > f.size()) return OFDIS_ERR_IO;
+      for (size_t i = 0; i < n; ++i) v[i] = f[p + i];
+    }
+  }
+  img.w = w;
+  img.h = h;
+  img.c = want;
+  img.px.assign((size_t)w * h * want, 0);
+  for (size_t i = 0; i < (size_t)w * h; ++i) {
+    if (nch == 1) {
+      for (int k = 0; k < want; ++k) img.px[i * want + k] = (uint8_t)v[i];
+    } else if (want == 3) {
+      img.px[3 * i] = (uint8_t)v[3 * i + 2];  // RGB file -> BGR
+      img.px[3 * i + 1] = (uint8_t)v[3 * i + 1];
+      img.px[3 * i + 2] = (uint8_t)v[3 * i];
+    } else {  // icvCvt_BGR2Gray_8u_C3C1R, SCALE 14: cB 1868, cG 9617, cR 4899, descale with rounding
+      img.px[i] = (uint8_t)((v[3 * i + 2] * 1868u + v[3 * i + 1] * 9617u + v[3 * i] * 4899u + 8192u) >> 14);
+    }
+  }
+  return OFDIS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height, int want_noc, size_t capacity) {
+  if (!path || !width || !height || (want_noc != 1 && want_noc != 3)) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::vector<uint8_t> f;
+  if (!read_file(path, f)) return OFDIS_ERR_IO;
+  Image img;
+  int rc;
+  if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G')
+    rc = decode_png(f, want_noc, img);
+  else if (f.size() >= 2 && f[0] == 'P' && f[1] >= '1' && f[1] <= '6')
+    rc = decode_pnm(f, want_noc, img);
+  else
+    rc = OFDIS_ERR_UNSUPPORTED;
+  if (rc) return rc;
+  *width = img.w;
+  *height = img.h;
+  if (!pixels) return OFDIS_OK;
+  if (capacity < img.px.size()) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::memcpy(pixels, img.px.data(), img.px.size());
+  return OFDIS_OK;
+}
+
+}  // extern "C"

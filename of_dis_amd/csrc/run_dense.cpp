@@ -5,9 +5,9 @@
 //   run_OF_INT img1 img2 out.flo p1 .. p20  all 20 parameters explicitly (README.md:54-86)
 //
 // SELECTMODE (1 flow -> .flo, 2 depth -> .pfm) and SELECTCHANNEL (1 gray, 3 BGR) are compile-time, as in
-// the reference's CMakeLists.txt:36-61.  Images: binary PGM (P5) / PPM (P6); OpenCV's imread is not
-// available in this image (PNG decoding is out of scope).  Unlike the reference, argv is
-// validated (the reference reads past argv for 6 <= argc < 24, run_dense.cpp:270-295).
+// the reference's CMakeLists.txt:36-61.  Images: PNG and Netpbm, decoded with cv::imread's semantics
+// (ofdis_read_image; OpenCV is not in this image).  Unlike the reference, argv is validated (the
+// reference reads past argv for 6 <= argc < 24, run_dense.cpp:270-295).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -22,25 +22,19 @@
 #define SELECTCHANNEL 1
 #endif
 
+// cv::imread(path, CV_LOAD_IMAGE_GRAYSCALE / CV_LOAD_IMAGE_COLOR) (run_dense.cpp:202-206)
 static std::vector<uint8_t> load(const char *path, int &w, int &h) {
-  int noc = 0;
-  if (ofdis_read_pnm(path, nullptr, &w, &h, &noc, 0) != OFDIS_OK) {
-    std::fprintf(stderr, "cannot read %s (binary PGM/PPM expected)\n", path);
+  int rc = ofdis_read_image(path, nullptr, &w, &h, SELECTCHANNEL, 0);
+  std::vector<uint8_t> px;
+  if (rc == OFDIS_OK) {
+    px.resize((size_t)w * h * SELECTCHANNEL);
+    rc = ofdis_read_image(path, px.data(), &w, &h, SELECTCHANNEL, px.size());
+  }
+  if (rc != OFDIS_OK) {
+    std::fprintf(stderr, "cannot read %s (PNG or Netpbm expected): %s\n", path, ofdis_status_string(rc));
     std::exit(1);
   }
-  std::vector<uint8_t> raw((size_t)w * h * noc);
-  ofdis_read_pnm(path, raw.data(), &w, &h, &noc, raw.size());
-  if (noc == SELECTCHANNEL) return raw;
-  std::vector<uint8_t> out((size_t)w * h * SELECTCHANNEL);
-  for (size_t i = 0; i < (size_t)w * h; ++i) {
-    if (SELECTCHANNEL == 1) {  // cv::COLOR_BGR2GRAY weights (ITU-R 601), rounded
-      const double g = 0.114 * raw[3 * i] + 0.587 * raw[3 * i + 1] + 0.299 * raw[3 * i + 2];
-      out[i] = (uint8_t)(g + 0.5);
-    } else {
-      out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = raw[i];
-    }
-  }
-  return out;
+  return px;
 }
 
 int main(int argc, char **argv) {

@@ -74,6 +74,16 @@ def read_flo(path: str, nc: int = 2) -> np.ndarray:
     return out
 
 
+def read_image(path: str, noc: int = 1) -> np.ndarray:
+    """cv::imread(path, GRAYSCALE if noc == 1 else COLOR) for PNG / Netpbm: u8 [h, w, noc], BGR for 3."""
+    w, h = C.c_int(), C.c_int()
+    check(lib().ofdis_read_image(path.encode(), None, C.byref(w), C.byref(h), noc, 0), "read_image")
+    out = np.empty((h.value, w.value, noc), np.uint8)
+    check(lib().ofdis_read_image(path.encode(), out.ctypes.data, C.byref(w), C.byref(h), noc, out.size),
+          "read_image")
+    return out
+
+
 def _ptr_list(arrs, n=32):
     out = (C.c_void_p * n)()
     keep = []
@@ -231,5 +241,5 @@ def algorithmic_bytes(p: Params, width: int, height: int, kernel: str) -> float:
 
 
 __all__ = ["OFClass", "Context", "Params", "oppoint", "params_from_strings", "validate", "synth_pair",
-           "write_flo", "write_pfm", "read_flo", "auto_first_scale", "kernel_names", "algorithmic_bytes",
+           "write_flo", "write_pfm", "read_flo", "read_image", "auto_first_scale", "kernel_names", "algorithmic_bytes",
            "MODE_OF", "MODE_DE"]

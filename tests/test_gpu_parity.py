@@ -214,3 +214,34 @@ def test_oflow_hpp_dropin_program(oracle, od, tmp_path):
     q = oracle.oppoint(2, w, 1, 1)
     want = oracle.oflow(oracle.build_pyramid(a, q, 8), oracle.build_pyramid(b, q, 8), w, h, q, 8)
     assert_bitexact(od.read_flo(str(out)), want, "OFC::OFClass drop-in program")
+
+
+@pytest.mark.parametrize("exe_name,noc,mode", [("run_OF_INT", 1, 1), ("run_OF_RGB", 3, 1), ("run_DE_INT", 1, 2)])
+def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode):
+    """The CLI reads colour PNGs with cv::imread's semantics (GRAYSCALE conversion for *_INT) and writes
+    the oracle's flow (.flo) / depth (.pfm) for the decoded pixels, bit for bit."""
+    import os
+    import subprocess
+    from test_image_io import encode_png
+    w, h = 176, 112
+    a3, b3 = od.synth_pair(w, h, 3, 4, mode)  # BGR
+    for name, im in (("a.png", a3), ("b.png", b3)):
+        (tmp_path / name).write_bytes(encode_png(im[..., ::-1].astype(np.int64), 2, 8, interlace=name == "b.png"))
+    a = od.read_image(str(tmp_path / "a.png"), noc)
+    b = od.read_image(str(tmp_path / "b.png"), noc)
+    if noc == 3:
+        assert np.array_equal(a, a3) and np.array_equal(b, b3)
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "of_dis_amd", "bin", exe_name)
+    out = tmp_path / ("o.flo" if mode == 1 else "o.pfm")
+    r = subprocess.run([exe, str(tmp_path / "a.png"), str(tmp_path / "b.png"), str(out), "2"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    want = oracle.run_u8(a, b, oracle.oppoint(2, w, mode, noc))
+    if mode == 1:
+        got = od.read_flo(str(out))
+    else:
+        raw = out.read_bytes()
+        head = f"Pf\n{w} {h}\n-1.000000\n".encode()
+        assert raw.startswith(head)
+        got = -np.frombuffer(raw[len(head):], np.float32).reshape(h, w)[::-1][..., None]
+    assert_bitexact(got, want, f"{exe_name} on PNG inputs")
