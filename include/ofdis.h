@@ -118,6 +118,18 @@ int ofdis_run_batch_u8(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *
 int ofdis_run_batch_u8_host(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
                             int height, const ofdis_params *p, float *flow_out);
 
+/* The same with an initial flow per pair (OFClass's initflow, oflow.h:106 / oflow.cpp:215-217, fed the way
+ * run_dense.cpp's commented-out code prepares it, :293-294, :302, :356-379): init_flow is device float
+ * [n][height][width][nop] at full resolution, or NULL (= ofdis_run_batch_u8).  With an initial flow the
+ * frames are padded to a multiple of 2^(sc_f+1) and the flow is replicate-padded, scaled by 2^-(sc_f+1)
+ * and INTER_AREA-reduced to the grid below the coarsest scale -- e.g. the previous frame's output for
+ * video (temporal propagation). */
+int ofdis_run_batch_u8_init(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b, const float *init_flow,
+                            int n, int width, int height, const ofdis_params *p, float *flow_out, void *stream);
+int ofdis_run_batch_u8_init_host(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b,
+                                 const float *init_flow, int n, int width, int height, const ofdis_params *p,
+                                 float *flow_out);
+
 /* Device pyramid only (run_dense.cpp:131-179 + :299-312): writes, for each level s in [sc_l, sc_f],
  * padded image/dx/dy of frame 0 to host arrays (same layout as ofdis_oflow_compute's inputs). */
 int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int height, const ofdis_params *p,

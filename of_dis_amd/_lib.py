@@ -100,6 +100,8 @@ def lib():
         "ofdis_context_destroy": ([vp], None),
         "ofdis_run_batch_u8": ([vp, vp, vp, i, i, i, P, vp, vp], i),
         "ofdis_run_batch_u8_host": ([vp, vp, vp, i, i, i, P, vp], i),
+        "ofdis_run_batch_u8_init": ([vp, vp, vp, vp, i, i, i, P, vp, vp], i),
+        "ofdis_run_batch_u8_init_host": ([vp, vp, vp, vp, i, i, i, P, vp], i),
         "ofdis_pyramid_u8_host": ([vp, vp, i, i, P, i, vp, vp, vp], i),
         "ofdis_context_set_stage_capture": ([vp, vp, vp, i], i),
         "ofdis_context_set_option": ([vp, C.c_char_p, i], i),

@@ -100,6 +100,16 @@ struct UpArgs {
   int nt_store;       // non-temporal output stores (A/B option "nt_store")
 };
 
+// Initial flow (run_dense.cpp:356-379): full-resolution [n][H0][W0][nop] -> replicate-padded, x sc,
+// INTER_AREA by k = 2^(sc_f+1) -> [n][ho][wo][nop] interleaved (OFClass's initflow layout).
+struct InitArgs {
+  const float *init;  // [n][H0][W0][nop]
+  float *out;         // [n][ho][wo][nop]
+  int n, nop, W0, H0, padl, padt, log2k, wo, ho;
+  float sc, scale;    // 2^-(sc_f+1), 1 / k^2
+};
+
+void launch_init_area(const InitArgs &a, hipStream_t s);
 void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s);
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s);
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s);

@@ -2402,6 +2402,38 @@ void launch_tv_level(const TvArgs &a, int n_inner, hipStream_t s) {
 void launch_tv_final(const TvArgs &a, hipStream_t s) {
   k_tv_final<<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, kTileH), a.n), 256, 0, s>>>(a);
 }
+// OpenCV resizeAreaFast for the initial flow (oracle: ofo_init_flow_area): one thread per output value,
+// the k x k block in row-major order, sum += ((a + b) + c) + d four at a time, then x 1/k^2.  The chain is
+// serial by definition (exact order); it runs once per batch on the coarsest grid (a few hundred values
+// per frame), its loads are issued four ahead of the adds.
+__global__ __launch_bounds__(256) void k_init_area(InitArgs a) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)a.wo * a.ho * a.nop;
+  if (i >= per * a.n) return;
+  const int f = (int)(i / per), r = (int)(i - f * per);
+  const int c = r % a.nop, px = r / a.nop, x = px % a.wo, y = px / a.wo;
+  const int k = 1 << a.log2k, area = k * k;
+  const float *src = a.init + (size_t)f * a.W0 * a.H0 * a.nop + c;
+  auto val = [&](int j) {
+    const int sy = clampi(y * k + (j >> a.log2k) - a.padt, 0, a.H0 - 1);
+    const int sx = clampi(x * k + (j & (k - 1)) - a.padl, 0, a.W0 - 1);
+    return src[((size_t)sy * a.W0 + sx) * a.nop] * a.sc;
+  };
+  float sum = 0.0f;
+  int j = 0;
+  for (; j <= area - 4; j += 4) {
+    const float v0 = val(j), v1 = val(j + 1), v2 = val(j + 2), v3 = val(j + 3);
+    sum += ((v0 + v1) + v2) + v3;
+  }
+  for (; j < area; ++j) sum += val(j);
+  a.out[i] = sum * a.scale;
+}
+
+void launch_init_area(const InitArgs &a, hipStream_t s) {
+  const long total = (long)a.n * a.wo * a.ho * a.nop;
+  k_init_area<<<dim3(ceil_div(total, 256)), 256, 0, s>>>(a);
+}
+
 void launch_upsample(const UpArgs &a, hipStream_t s) {
   if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
     k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);

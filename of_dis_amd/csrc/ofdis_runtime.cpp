@@ -34,7 +34,9 @@ struct Plan {
   std::vector<LevelGeom> lv;                       // index s - sc_l
   std::vector<size_t> off_lvl, off_img, off_dx, off_dy, off_flow, off_flow_bw;
   size_t off_piter = 0, off_pw = 0, off_piter_bw = 0, off_pw_bw = 0, off_tv = 0, tv_plane = 0;
-  bool fb = false;  // usefbcon: backward grid, flow and refinement
+  size_t off_init = 0;  // initial flow at the coarsest scale - 1, [n][Hp >> (sc_f+1)][Wp >> (sc_f+1)][nop]
+  bool init = false;    // an initial flow is given: divisibility 2^(sc_f+1) (run_dense.cpp:302)
+  bool fb = false;      // usefbcon: backward grid, flow and refinement
   size_t total = 0;
 };
 
@@ -69,7 +71,7 @@ struct ofdis_context {
   int opt_sor_pipe = 0;  // 1: force the single-wave-per-row-group register pipeline (A/B)
   int opt_graph = 1;           // replay the whole batch as one HIP graph (captured once per shape / pointers)
   struct GraphKey {
-    const void *a = nullptr, *b = nullptr, *out = nullptr, *ws = nullptr;
+    const void *a = nullptr, *b = nullptr, *out = nullptr, *ws = nullptr, *init = nullptr;
     int n = 0, w = 0, h = 0;
     ofdis_params p{};
   } gkey;
@@ -189,7 +191,7 @@ int steps_of(const ofdis_params *p) {
   return st0 > 1 ? st0 : 1;
 }
 
-Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
+Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad, bool init = false) {
   Plan P;
   P.n = n;
   P.Wp = Wp;
@@ -243,6 +245,11 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad) {
   for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, (size_t)skew_plane(g.w, g.h));
   P.tv_plane = max_sp;
   if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_sp * (14 + 9 * (size_t)P.noc));
+  P.off_init = off;
+  if (init) {
+    P.init = true;
+    off = align_up(off + sizeof(float) * (size_t)n * P.nop * (Wp >> (p->sc_f + 1)) * (Hp >> (p->sc_f + 1)));
+  }
   P.total = off;
   return P;
 }
@@ -541,10 +548,10 @@ int run_pyramid(ofdis_context *c, char *ws, const Plan &P, const uint8_t *a, con
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
 
-Plan batch_plan(const ofdis_params *p, int n, int width, int height) {
-  const int d = 1 << p->sc_f;
+Plan batch_plan(const ofdis_params *p, int n, int width, int height, bool init = false) {
+  const int d = 1 << (p->sc_f + (init ? 1 : 0));  // run_dense.cpp:301-302
   const int padw = (width % d) ? d - width % d : 0, padh = (height % d) ? d - height % d : 0;
-  Plan P = make_plan(p, n, width + padw, height + padh, p->p_samp_s);
+  Plan P = make_plan(p, n, width + padw, height + padh, p->p_samp_s, init);
   P.W0 = width;
   P.H0 = height;
   P.padw = padw;
@@ -619,12 +626,34 @@ int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
 
+// The initial flow of a chunk (device, full resolution [n][H0][W0][nop]) -> OFClass's initflow input in the
+// workspace (run_dense.cpp:356-379, restated: ofo_init_flow_area).
+int run_init(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const float *init, hipStream_t s) {
+  InitArgs ia{};
+  ia.init = init;
+  ia.out = (float *)(ws + P.off_init);
+  ia.n = P.n;
+  ia.nop = P.nop;
+  ia.W0 = P.W0;
+  ia.H0 = P.H0;
+  ia.padl = P.padl;
+  ia.padt = P.padt;
+  ia.log2k = p->sc_f + 1;
+  ia.wo = P.Wp >> (p->sc_f + 1);
+  ia.ho = P.Hp >> (p->sc_f + 1);
+  ia.sc = (float)std::pow(2.0, -p->sc_f - 1);  // flowinit *= sc_fct (float)
+  ia.scale = 1.f / (float)(1 << (2 * (p->sc_f + 1)));
+  launch_init_area(ia, s);
+  return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
+}
+
 // One chunk of frames through the whole pipeline on stream s with workspace ws.
 int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
-              const uint8_t *img_b, float *flow_out, hipStream_t s) {
+              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s) {
   int rc = run_pyramid(c, ws, P, img_a, img_b, s);
   if (rc) return rc;
-  rc = run_levels(c, ws, P, p, s, nullptr, nullptr);
+  if (init && (rc = run_init(c, ws, P, p, init, s))) return rc;
+  rc = run_levels(c, ws, P, p, s, init ? (const float *)(ws + P.off_init) : nullptr, nullptr);
   if (rc) return rc;
   return run_upsample(c, ws, P, p, flow_out, s);
 }
@@ -652,10 +681,11 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
 
 // Chunks round-robin over opt_streams streams, each chunk's whole pipeline on one stream ("streams").
 int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
-                    const uint8_t *img_b, float *flow_out, int n, int width, int height, int chunk) {
+                    const uint8_t *img_b, const float *init, float *flow_out, int n, int width, int height,
+                    int chunk) {
   const int nchunks = (n + chunk - 1) / chunk;
   const int k = std::min(c->opt_streams, nchunks);
-  Plan PC = batch_plan(p, chunk, width, height);
+  Plan PC = batch_plan(p, chunk, width, height, init != nullptr);
   int rc = ensure_lanes(c, k, PC.total);
   if (rc) return rc;
   HIP_OK(hipEventRecord(c->entry, s));
@@ -664,8 +694,9 @@ int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, cons
   for (int ch = 0; ch < nchunks; ++ch) {
     const int f0 = ch * chunk, m = std::min(chunk, n - f0);
     auto &L = c->lanes[ch % k];
-    Plan PM = m == chunk ? PC : batch_plan(p, m, width, height);
-    rc = run_chunk(c, L.ws, PM, p, img_a + f0 * in_frame, img_b + f0 * in_frame, flow_out + f0 * out_frame, L.s);
+    Plan PM = m == chunk ? PC : batch_plan(p, m, width, height, init != nullptr);
+    rc = run_chunk(c, L.ws, PM, p, img_a + f0 * in_frame, img_b + f0 * in_frame, init ? init + f0 * out_frame : nullptr,
+                   flow_out + f0 * out_frame, L.s);
     if (rc) return rc;
   }
   for (int i = 0; i < k; ++i) {
@@ -675,8 +706,9 @@ int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, cons
   return OFDIS_OK;
 }
 
-int pipeline_resources(ofdis_context *c, const ofdis_params *p, int width, int height, int chunk, int nchunks) {
-  int rc = ensure_lanes(c, 2, batch_plan(p, chunk, width, height).total);
+int pipeline_resources(ofdis_context *c, const ofdis_params *p, int width, int height, int chunk, int nchunks,
+                       bool init) {
+  int rc = ensure_lanes(c, 2, batch_plan(p, chunk, width, height, init).total);
   if (rc) return rc;
   while ((int)c->pipe_ev.size() < 2 * nchunks) {
     hipEvent_t e = nullptr;
@@ -693,13 +725,15 @@ int pipeline_resources(ofdis_context *c, const ofdis_params *p, int width, int h
 // ch % 2, which pyr(ch+2) reuses only after up(ch) (same stream, issued before it), which waits for
 // levels(ch).  Every hand-over is an event, so each kernel sees the data of the single-stream order.
 int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
-                  const uint8_t *img_b, float *flow_out, int n, int width, int height, int chunk) {
+                  const uint8_t *img_b, const float *init, float *flow_out, int n, int width, int height,
+                  int chunk) {
   const int nchunks = (n + chunk - 1) / chunk;
-  int rc = pipeline_resources(c, p, width, height, chunk, nchunks);
+  int rc = pipeline_resources(c, p, width, height, chunk, nchunks, init != nullptr);
   if (rc) return rc;
   std::vector<Plan> plans;
   plans.reserve(nchunks);
-  for (int ch = 0; ch < nchunks; ++ch) plans.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height));
+  for (int ch = 0; ch < nchunks; ++ch)
+    plans.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height, init != nullptr));
   const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * plans[0].nop;
   hipStream_t S = c->lanes[0].s, L = c->lanes[1].s;
   hipEvent_t *ev_pyr = c->pipe_ev.data(), *ev_lev = c->pipe_ev.data() + nchunks;
@@ -710,6 +744,7 @@ int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const 
     const size_t f0 = (size_t)ch * chunk;
     int r = run_pyramid(c, c->lanes[ch & 1].ws, plans[ch], img_a + f0 * in_frame, img_b + f0 * in_frame, S);
     if (r) return r;
+    if (init && (r = run_init(c, c->lanes[ch & 1].ws, plans[ch], p, init + f0 * out_frame, S))) return r;
     HIP_OK(hipEventRecord(ev_pyr[ch], S));
     return OFDIS_OK;
   };
@@ -722,7 +757,9 @@ int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const 
     OFDIS_TRACE("pipeline: chunk %d (%d frames)", ch, plans[ch].n);
     HIP_OK(hipStreamWaitEvent(L, ev_pyr[ch], 0));
     if (dbg_sync) HIP_OK(hipDeviceSynchronize());
-    if ((rc = run_levels(c, ws, plans[ch], p, L, nullptr, nullptr))) return rc;
+    if ((rc = run_levels(c, ws, plans[ch], p, L, init ? (const float *)(ws + plans[ch].off_init) : nullptr,
+                         nullptr)))
+      return rc;
     if (dbg_sync) HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipEventRecord(ev_lev[ch], L));
     if (ch + 1 < nchunks && (rc = pyr(ch + 1))) return rc;
@@ -740,13 +777,18 @@ int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const 
 
 int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width, int height,
                        const ofdis_params *p, float *flow_out, void *stream) {
+  return ofdis_run_batch_u8_init(c, img_a, img_b, nullptr, n, width, height, p, flow_out, stream);
+}
+
+int ofdis_run_batch_u8_init(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, const float *init, int n,
+                            int width, int height, const ofdis_params *p, float *flow_out, void *stream) {
   if (!c || !img_a || !img_b || !flow_out || n <= 0 || width <= 0 || height <= 0) return OFDIS_ERR_INVALID_ARGUMENT;
   int rc = ofdis_params_validate(p, -1, -1, -1);
   if (rc) return rc;
   std::lock_guard<std::mutex> lock(c->mu);
   HIP_OK(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  Plan P = batch_plan(p, n, width, height);
+  Plan P = batch_plan(p, n, width, height, init != nullptr);
   rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
   if (rc) return rc;
   const bool capturing = !c->cap_dis.empty() || !c->cap_tv.empty();
@@ -755,14 +797,14 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
   // pipelined: the streaming stages of neighbouring chunks overlap the DIS + TV chain of the current one
   const bool pipelined = c->opt_pipeline && nchunks > 1 && !capturing && !c->timing;
   if (!pipelined && (c->opt_streams > 1 && nchunks > 1 && !capturing))
-    return run_round_robin(c, s, p, img_a, img_b, flow_out, n, width, height, chunk);
+    return run_round_robin(c, s, p, img_a, img_b, init, flow_out, n, width, height, chunk);
   if (!pipelined) {
     rc = ensure_ws(c, P.total);
     if (rc) return rc;
   }
   auto issue = [&](hipStream_t st) {
-    return pipelined ? run_pipelined(c, st, p, img_a, img_b, flow_out, n, width, height, chunk)
-                     : run_chunk(c, c->ws, P, p, img_a, img_b, flow_out, st);
+    return pipelined ? run_pipelined(c, st, p, img_a, img_b, init, flow_out, n, width, height, chunk)
+                     : run_chunk(c, c->ws, P, p, img_a, img_b, init, flow_out, st);
   };
   // The pipeline is issued eagerly: its two streams would have to join the capture through events, which
   // this HIP runtime does not survive (hipStreamEndCapture faults); eager and graph kernel boundaries
@@ -773,7 +815,7 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
   // stream while the pointers, sizes, parameters and options stay the same (set_option drops the graph).
   ofdis_context::GraphKey key;
   std::memset(&key, 0, sizeof(key));  // padding included: the key is compared bytewise
-  key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = c->ws;
+  key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = c->ws; key.init = init;
   key.n = n; key.w = width; key.h = height; key.p = *p;
   if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
     if (c->gexec) {  // the previous graph may still be running on a caller stream
@@ -807,29 +849,40 @@ int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *im
 
 int ofdis_run_batch_u8_host(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
                             int height, const ofdis_params *p, float *flow_out) {
+  return ofdis_run_batch_u8_init_host(c, img_a, img_b, nullptr, n, width, height, p, flow_out);
+}
+
+int ofdis_run_batch_u8_init_host(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, const float *init,
+                                 int n, int width, int height, const ofdis_params *p, float *flow_out) {
   if (!c || !img_a || !img_b || !flow_out || n <= 0 || width <= 0 || height <= 0 || !p)
     return OFDIS_ERR_INVALID_ARGUMENT;
   HIP_OK(hipSetDevice(c->device));
   const size_t in = (size_t)n * width * height * p->noc;
   const size_t out = (size_t)n * width * height * (p->mode == OFDIS_MODE_OF ? 2 : 1);
   uint8_t *da = nullptr, *db = nullptr;
-  float *dout = nullptr;
-  HIP_OK(hipMalloc(&da, in));
-  HIP_OK(hipMalloc(&db, in));
-  HIP_OK(hipMalloc(&dout, out * sizeof(float)));
-  HIP_OK(hipMemcpyAsync(da, img_a, in, hipMemcpyHostToDevice, c->stream));
-  HIP_OK(hipMemcpyAsync(db, img_b, in, hipMemcpyHostToDevice, c->stream));
-  auto t0 = std::chrono::steady_clock::now();
-  int rc = ofdis_run_batch_u8(c, da, db, n, width, height, p, dout, c->stream);
-  if (rc == OFDIS_OK) {
-    HIP_OK(hipStreamSynchronize(c->stream));
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (p->verbosity > 0) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", ms);
-    HIP_OK(hipMemcpy(flow_out, dout, out * sizeof(float), hipMemcpyDeviceToHost));
+  float *dout = nullptr, *dinit = nullptr;
+  int rc = OFDIS_OK;
+  auto step = [&](hipError_t e) {
+    if (e != hipSuccess && rc == OFDIS_OK) rc = e == hipErrorOutOfMemory ? OFDIS_ERR_OUT_OF_MEMORY : OFDIS_ERR_DEVICE;
+    return rc == OFDIS_OK;
+  };
+  if (step(hipMalloc(&da, in)) && step(hipMalloc(&db, in)) && step(hipMalloc(&dout, out * sizeof(float))) &&
+      (!init || step(hipMalloc(&dinit, out * sizeof(float)))) &&
+      step(hipMemcpyAsync(da, img_a, in, hipMemcpyHostToDevice, c->stream)) &&
+      step(hipMemcpyAsync(db, img_b, in, hipMemcpyHostToDevice, c->stream)) &&
+      (!init || step(hipMemcpyAsync(dinit, init, out * sizeof(float), hipMemcpyHostToDevice, c->stream)))) {
+    auto t0 = std::chrono::steady_clock::now();
+    rc = ofdis_run_batch_u8_init(c, da, db, dinit, n, width, height, p, dout, c->stream);
+    if (rc == OFDIS_OK && step(hipStreamSynchronize(c->stream))) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (p->verbosity > 0) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", ms);
+      step(hipMemcpy(flow_out, dout, out * sizeof(float), hipMemcpyDeviceToHost));
+    }
   }
   hipFree(da);
   hipFree(db);
   hipFree(dout);
+  hipFree(dinit);
   return rc;
 }
 

@@ -3,6 +3,7 @@
 //   run_OF_INT img1 img2 out.flo            operating point 2, coarsest scale chosen automatically
 //   run_OF_INT img1 img2 out.flo X          operating point X = 1..4
 //   run_OF_INT img1 img2 out.flo p1 .. p20  all 20 parameters explicitly (README.md:54-86)
+//   run_OF_INT img1 img2 out.flo p1 .. p20 1 init.flo   ... with an initial flow (run_dense.cpp:293-294)
 //
 // SELECTMODE (1 flow -> .flo, 2 depth -> .pfm) and SELECTCHANNEL (1 gray, 3 BGR) are compile-time, as in
 // the reference's CMakeLists.txt:36-61.  Images: PNG and Netpbm, decoded with cv::imread's semantics
@@ -39,8 +40,12 @@ static std::vector<uint8_t> load(const char *path, int &w, int &h) {
 
 int main(int argc, char **argv) {
   auto t0 = std::chrono::steady_clock::now();
-  if (argc != 4 && argc != 5 && argc != 24) {
-    std::fprintf(stderr, "usage: %s img1 img2 out [oppoint 1-4 | 20 parameters]\n", argv[0]);
+  // argv[24] / argv[25]: "hasinfile" and the initial-flow file, the reference's commented-out plumbing
+  // (run_dense.cpp:293-294): a .flo (OF) / float depth .flo (DE) of the input size
+  const bool hasinfile = argc == 26 && std::atoi(argv[24]) != 0;
+  if (argc != 4 && argc != 5 && argc != 24 && !(argc == 25 && std::atoi(argv[24]) == 0) && !hasinfile) {
+    std::fprintf(stderr, "usage: %s img1 img2 out [oppoint 1-4 | 20 parameters [hasinfile(0/1) [init.flo]]]\n",
+                 argv[0]);
     return 1;
   }
   int w = 0, h = 0, w2 = 0, h2 = 0;
@@ -70,8 +75,19 @@ int main(int argc, char **argv) {
     return 1;
   }
   const int nop = SELECTMODE == 1 ? 2 : 1;
-  std::vector<float> flow((size_t)w * h * nop);
-  rc = ofdis_run_batch_u8_host(ctx, a.data(), b.data(), 1, w, h, &p, flow.data());
+  std::vector<float> flow((size_t)w * h * nop), init;
+  if (hasinfile) {  // ReadFlowFile (run_dense.cpp:85-129) into a w x h x nop image
+    int iw = 0, ih = 0;
+    init.resize(flow.size());
+    if (ofdis_read_flo(argv[25], nullptr, &iw, &ih, nop) != OFDIS_OK || iw != w || ih != h ||
+        ofdis_read_flo(argv[25], init.data(), &iw, &ih, nop) != OFDIS_OK) {
+      std::fprintf(stderr, "cannot read %s (a %dx%d .flo file expected)\n", argv[25], w, h);
+      ofdis_context_destroy(ctx);
+      return 1;
+    }
+  }
+  rc = ofdis_run_batch_u8_init_host(ctx, a.data(), b.data(), hasinfile ? init.data() : nullptr, 1, w, h, &p,
+                                    flow.data());
   ofdis_context_destroy(ctx);
   if (rc != OFDIS_OK) {
     std::fprintf(stderr, "flow computation failed: %s\n", ofdis_status_string(rc));

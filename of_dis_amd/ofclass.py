@@ -153,13 +153,15 @@ class Context:
             pass
 
     def run_ptr(self, a_ptr: int, b_ptr: int, n: int, width: int, height: int, p: Params, out_ptr: int,
-                stream: int = 0) -> None:
-        """Device pointers in, device pointer out; asynchronous on `stream` (hipStream_t handle)."""
-        check(lib().ofdis_run_batch_u8(self._h, a_ptr, b_ptr, n, width, height, C.byref(p), out_ptr,
-                                       stream or None), "ofdis_run_batch_u8")
+                stream: int = 0, init_ptr: int = 0) -> None:
+        """Device pointers in, device pointer out; asynchronous on `stream` (hipStream_t handle).
+        init_ptr: optional device float [n, h, w, nop] initial flow (ofdis_run_batch_u8_init)."""
+        check(lib().ofdis_run_batch_u8_init(self._h, a_ptr, b_ptr, init_ptr or None, n, width, height, C.byref(p),
+                                            out_ptr, stream or None), "ofdis_run_batch_u8_init")
 
-    def run(self, a, b, p: Params, out=None):
-        """torch.uint8 CUDA tensors [n, h, w] or [n, h, w, noc] -> torch.float32 [n, h, w, nop]."""
+    def run(self, a, b, p: Params, out=None, init=None):
+        """torch.uint8 CUDA tensors [n, h, w] or [n, h, w, noc] -> torch.float32 [n, h, w, nop].
+        init: optional float32 CUDA tensor [n, h, w, nop], the initial flow at full resolution."""
         import torch
         if a.dim() == 3:
             a, b = a.unsqueeze(-1), b.unsqueeze(-1)
@@ -170,22 +172,32 @@ class Context:
         if out is None:
             out = torch.empty((n, h, w, p.nop), dtype=torch.float32, device=a.device)
         stream = torch.cuda.current_stream(a.device).cuda_stream
-        self.run_ptr(a.data_ptr(), b.data_ptr(), n, w, h, p, out.data_ptr(), stream)
+        if init is not None:
+            if tuple(init.shape) != (n, h, w, p.nop) or init.dtype != torch.float32 or not init.is_cuda:
+                raise ValueError("init must be a float32 CUDA tensor [n, h, w, nop]")
+            init = init.contiguous()
+        self.run_ptr(a.data_ptr(), b.data_ptr(), n, w, h, p, out.data_ptr(), stream,
+                     init.data_ptr() if init is not None else 0)
         if not stream:
             # torch's default stream is the legacy NULL stream, which the C-ABI reads as "the context's own
             # (non-blocking) stream": nothing would order later torch work after the flow, so wait here.
             torch.cuda.synchronize(a.device)
         return out
 
-    def run_host(self, a: np.ndarray, b: np.ndarray, p: Params) -> np.ndarray:
-        """numpy u8 [n,h,w,noc] (or a single [h,w,noc] pair) -> numpy float32 flow; synchronous."""
+    def run_host(self, a: np.ndarray, b: np.ndarray, p: Params, init: Optional[np.ndarray] = None) -> np.ndarray:
+        """numpy u8 [n,h,w,noc] (or a single [h,w,noc] pair) -> numpy float32 flow; synchronous.
+        init: optional initial flow at full resolution, [n,h,w,nop] (or [h,w,nop] for a single pair)."""
         single = a.ndim == 3
         a4 = np.ascontiguousarray(a[None] if single else a, np.uint8)
         b4 = np.ascontiguousarray(b[None] if single else b, np.uint8)
         n, h, w = a4.shape[:3]
         out = np.empty((n, h, w, p.nop), _f32)
-        check(lib().ofdis_run_batch_u8_host(self._h, a4.ctypes.data, b4.ctypes.data, n, w, h, C.byref(p),
-                                            out.ctypes.data), "ofdis_run_batch_u8_host")
+        i4 = None
+        if init is not None:
+            i4 = np.ascontiguousarray(init, _f32).reshape(n, h, w, p.nop)
+        check(lib().ofdis_run_batch_u8_init_host(self._h, a4.ctypes.data, b4.ctypes.data,
+                                                 None if i4 is None else i4.ctypes.data, n, w, h, C.byref(p),
+                                                 out.ctypes.data), "ofdis_run_batch_u8_init_host")
         return out[0] if single else out
 
     def pyramid_host(self, img: np.ndarray, p: Params, imgpadding: Optional[int] = None):

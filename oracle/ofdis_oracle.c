@@ -1220,11 +1220,40 @@ int ofo_upsample_crop(const float *flow_l, int wl, int hl, int nop, int scale_lo
 
 /* ------------------------------------------------------------------ whole pipeline (run_dense.cpp main) */
 
+/* The initial-flow input of run_dense.cpp:356-379 (commented out upstream, restated for the initflow
+ * boundary): the full-resolution flow is replicate-padded like the images (:299-312 with divisibility
+ * 2^(sc_f+1), :302), scaled by sc_fct = 2^-(sc_f+1) (float) and cv::resize'd by the same factor with
+ * INTER_AREA.  The factor is an integer, so OpenCV takes resizeAreaFast: per output value, the k x k block
+ * in row-major order, summed four at a time (sum += ((a + b) + c) + d, CV_ENABLE_UNROLLED), times 1/k^2. */
+void ofo_init_flow_area(const float *init, int width, int height, int nop, int padw, int padh, int sc_f,
+                        float *out) {
+  const int k = 1 << (sc_f + 1), area = k * k;
+  const int wo = (width + padw) / k, ho = (height + padh) / k, l = padw / 2, t = padh / 2;
+  const float sc = (float)pow(2.0, -sc_f - 1), scale = 1.f / (float)area;
+  for (int y = 0; y < ho; ++y)
+    for (int x = 0; x < wo; ++x)
+      for (int c = 0; c < nop; ++c) {
+#define IV(j) (init[((size_t)clampi(y * k + (j) / k - t, 0, height - 1) * width + \
+                     clampi(x * k + (j) % k - l, 0, width - 1)) * nop + c] * sc)
+        float sum = 0.0f;
+        int j = 0;
+        for (; j <= area - 4; j += 4) sum += IV(j) + IV(j + 1) + IV(j + 2) + IV(j + 3);
+        for (; j < area; ++j) sum += IV(j);
+#undef IV
+        out[((size_t)y * wo + x) * nop + c] = sum * scale;
+      }
+}
+
 int ofo_run_u8(const uint8_t *img_a, const uint8_t *img_b, int width, int height, const ofdis_params *p,
                float *flow_out, float *const *cap_dis, float *const *cap_tv) {
+  return ofo_run_u8_init(img_a, img_b, NULL, width, height, p, flow_out, cap_dis, cap_tv);
+}
+
+int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *init, int width, int height,
+                    const ofdis_params *p, float *flow_out, float *const *cap_dis, float *const *cap_tv) {
   const int noc = p->noc, nop = p->mode == OFDIS_MODE_OF ? 2 : 1, pad = p->p_samp_s;
   int padw, padh;
-  ofo_divisibility_pad(width, height, p->sc_f, &padw, &padh);
+  ofo_divisibility_pad(width, height, p->sc_f + (init ? 1 : 0), &padw, &padh);  /* run_dense.cpp:302 */
   const int Wp = width + padw, Hp = height + padh, l = padw / 2, t = padh / 2;
   uint8_t *pa = (uint8_t *)malloc((size_t)Wp * Hp * noc), *pb = (uint8_t *)malloc((size_t)Wp * Hp * noc);
   for (int y = 0; y < Hp; ++y)
@@ -1245,12 +1274,18 @@ int ofo_run_u8(const uint8_t *img_a, const uint8_t *img_b, int width, int height
   if (!rc) rc = ofo_build_pyramid(pb, Wp, Hp, noc, p->sc_f, p->sc_l, pad, pyr[3], pyr[4], pyr[5]);
   const int wl = Wp >> p->sc_l, hl = Hp >> p->sc_l;
   float *fl = (float *)malloc(sizeof(float) * (size_t)wl * hl * nop);
+  float *ini = NULL;
+  if (init) {
+    ini = (float *)malloc(sizeof(float) * (size_t)(Wp >> (p->sc_f + 1)) * (Hp >> (p->sc_f + 1)) * nop);
+    ofo_init_flow_area(init, width, height, nop, padw, padh, p->sc_f, ini);
+  }
   if (!rc)
     rc = ofo_oflow((const float *const *)pyr[0], (const float *const *)pyr[1], (const float *const *)pyr[2],
                    (const float *const *)pyr[3], (const float *const *)pyr[4], (const float *const *)pyr[5], pad, fl,
-                   NULL, Wp, Hp, p, cap_dis, cap_tv);
+                   ini, Wp, Hp, p, cap_dis, cap_tv);
   if (!rc) rc = ofo_upsample_crop(fl, wl, hl, nop, p->sc_l, padw, padh, width, height, flow_out);
   free(fl);
+  free(ini);
   for (int s = p->sc_l; s <= p->sc_f; ++s)
     for (int k = 0; k < 6; ++k) free(pyr[k][s]);
   free(pa); free(pb);

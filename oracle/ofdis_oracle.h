@@ -52,6 +52,12 @@ int ofo_upsample_crop(const float *flow_l, int wl, int hl, int nop, int scale_lo
 /* Whole pipeline for one frame pair of u8 images [h][w][noc]: output [h][w][nop]. */
 int ofo_run_u8(const uint8_t *img_a, const uint8_t *img_b, int width, int height, const ofdis_params *p,
                float *flow_out, float *const *cap_dis, float *const *cap_tv);
+/* Same with an optional full-resolution initial flow [h][w][nop] (run_dense.cpp:293-294, 302, 356-379:
+ * divisibility 2^(sc_f+1), replicate pad, x 2^-(sc_f+1), INTER_AREA down to the coarsest scale - 1). */
+int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *init, int width, int height,
+                    const ofdis_params *p, float *flow_out, float *const *cap_dis, float *const *cap_tv);
+void ofo_init_flow_area(const float *init, int width, int height, int nop, int padw, int padh, int sc_f,
+                        float *out);
 
 /* One VarRefClass run at scale `level` on padded interleaved level images; flow w*h*nop in place. */
 int ofo_refine_level(const float *im_ao, const float *im_bo, int w, int h, int imgpadding, int level,

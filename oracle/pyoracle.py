@@ -67,6 +67,8 @@ def lib():
         L.ofo_upsample_crop.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, _f32p]
         L.ofo_run_u8.argtypes = [_u8p, _u8p, C.c_int, C.c_int, C.POINTER(Params), _f32p, vp, vp]
+        L.ofo_run_u8_init.argtypes = [_u8p, _u8p, vp, C.c_int, C.c_int, C.POINTER(Params), _f32p, vp, vp]
+        L.ofo_init_flow_area.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _f32p]
         L.ofo_refine_level.argtypes = [_f32p, _f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Params), _f32p]
         L.ofo_image_warp.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, C.c_int, C.c_int]
         L.ofo_get_derivatives.argtypes = [_f32p, _f32p, C.c_int, C.c_int, C.c_int] + [_f32p] * 8
@@ -77,7 +79,7 @@ def lib():
         L.ofo_sor_coupled.argtypes = [_f32p] * 9 + [C.c_int, C.c_int, C.c_int, C.c_float]
         L.ofo_sor_point_de.argtypes = [_f32p] * 5 + [C.c_int, C.c_int, C.c_int, C.c_float]
         for f in ("ofo_params_oppoint", "ofo_build_pyramid", "ofo_oflow", "ofo_upsample_crop", "ofo_run_u8",
-                  "ofo_refine_level"):
+                  "ofo_run_u8_init", "ofo_refine_level"):
             getattr(L, f).restype = C.c_int
         _lib = L
     return _lib
@@ -140,19 +142,22 @@ def oflow(pyr_a, pyr_b, width, height, p: Params, imgpadding: int, initflow=None
     return (out, cap_d, cap_t) if capture else out
 
 
-def run_u8(a: np.ndarray, b: np.ndarray, p: Params, capture=False):
-    """Whole run_dense pipeline for one pair of u8 [h][w][noc] images -> flow [h][w][nop]."""
+def run_u8(a: np.ndarray, b: np.ndarray, p: Params, capture=False, init=None):
+    """Whole run_dense pipeline for one pair of u8 [h][w][noc] images -> flow [h][w][nop].
+    init: optional full-resolution initial flow [h][w][nop] (run_dense.cpp:293-294, 356-379)."""
     h, w = a.shape[:2]
     nop = nop_of(p)
     out = np.zeros((h, w, nop), np.float32)
     cap_d, cap_t = {}, {}
     if capture:
-        pw, ph = divisibility_pad(w, h, p.sc_f)
+        pw, ph = divisibility_pad(w, h, p.sc_f + (init is not None))
         for s in range(p.sc_l, p.sc_f + 1):
             cap_d[s] = np.zeros((((h + ph) >> s), ((w + pw) >> s), nop), np.float32)
             cap_t[s] = np.zeros_like(cap_d[s])
-    rc = lib().ofo_run_u8(np.ascontiguousarray(a, np.uint8), np.ascontiguousarray(b, np.uint8), w, h, C.byref(p), out,
-                          _ptr_array(cap_d) if capture else None, _ptr_array(cap_t) if capture else None)
+    ini = None if init is None else np.ascontiguousarray(init, np.float32).reshape(h, w, nop)
+    rc = lib().ofo_run_u8_init(np.ascontiguousarray(a, np.uint8), np.ascontiguousarray(b, np.uint8),
+                               None if ini is None else ini.ctypes.data, w, h, C.byref(p), out,
+                               _ptr_array(cap_d) if capture else None, _ptr_array(cap_t) if capture else None)
     if rc != 0:
         raise RuntimeError(f"ofo_run_u8 failed: {rc}")
     return (out, cap_d, cap_t) if capture else out
