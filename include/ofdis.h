@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define OFDIS_ABI_VERSION 1
+#define OFDIS_ABI_VERSION 2
 
 /* Status codes.  The reference has no error channel (it exit(1)s on OOM, FDF1.0.1/image.cpp:26-27,
  * and never validates parameters); every entry point here returns one of these instead. */
@@ -61,6 +61,12 @@ typedef struct ofdis_params {
   int tv_solverit;  /* SOR sweeps per TV iteration                                         */
   float tv_sor;     /* SOR relaxation omega                                                */
   int verbosity;    /* 0 silent, 1 total time, 2 per-scale TIME lines (oflow.cpp:297,336)  */
+  /* Reference build variants (compile-time there, runtime fields here; 0 = the default build): */
+  int omp_build;    /* USE_OPENMP build (CMakeLists.txt:4,17-23): optical-flow refinement runs
+                       sor_coupled_slow_but_readable, point SOR (refine_variational.cpp:202-203,
+                       solver.c:34-78), in its single-thread order (the multi-threaded build races rows) */
+  int gradmag;      /* SELECTCHANNEL 2 (run_dense.cpp:139-148, 194-197): the pyramid is built on each
+                       frame's Sobel gradient magnitude instead of its intensity (noc must be 1)          */
 } ofdis_params;
 
 /* ------------------------------------------------------------------ parameters */
@@ -78,7 +84,8 @@ int ofdis_params_oppoint(ofdis_params *p, int oppoint, int width_org, int mode, 
 int ofdis_params_from_strings(ofdis_params *p, int count, const char *const *values, int mode, int noc);
 
 /* Validation the reference never does: p even and >= 2, p*p*noc divisible by 4 (patch.cpp:230),
- * 0 <= sc_l <= sc_f, width/height divisible by 2^sc_f, costfct in {0,1,2}, noc in {1,3}. */
+ * 0 <= sc_l <= sc_f, width/height divisible by 2^sc_f, costfct in {0,1,2}, noc in {1,3}, gradmag only
+ * with noc = 1. */
 int ofdis_params_validate(const ofdis_params *p, int width, int height, int imgpadding);
 
 /* ------------------------------------------------------------------ library boundary */

@@ -46,8 +46,11 @@ class OFClass {
           const int noc_in, const int patnorm_in, const bool usetvref_in, const float tv_alpha_in,
           const float tv_gamma_in, const float tv_delta_in, const int tv_innerit_in, const int tv_solverit_in,
           const float tv_sor_in, const int verbosity_in) {
-    ofdis_params p;
+    ofdis_params p = {};
     p.mode = SELECTMODE;
+#ifdef _OPENMP
+    p.omp_build = 1;  // an OpenMP build of the reference refines with point SOR (refine_variational.cpp:202-203)
+#endif
     p.noc = noc_in;
     p.sc_f = sc_f_in;
     p.sc_l = sc_l_in;

@@ -43,6 +43,7 @@ class Params(C.Structure):
         ("patnorm", C.c_int), ("usetvref", C.c_int),
         ("tv_alpha", C.c_float), ("tv_gamma", C.c_float), ("tv_delta", C.c_float),
         ("tv_innerit", C.c_int), ("tv_solverit", C.c_int), ("tv_sor", C.c_float), ("verbosity", C.c_int),
+        ("omp_build", C.c_int), ("gradmag", C.c_int),
     ]
 
     def as_dict(self):

@@ -101,6 +101,7 @@ int ofdis_params_validate(const ofdis_params *p, int width, int height, int imgp
   if (!p) return OFDIS_ERR_INVALID_ARGUMENT;
   if (p->mode != OFDIS_MODE_OF && p->mode != OFDIS_MODE_DE) return OFDIS_ERR_INVALID_ARGUMENT;
   if (p->noc != 1 && p->noc != 3) return OFDIS_ERR_INVALID_ARGUMENT;
+  if (p->gradmag && p->noc != 1) return OFDIS_ERR_INVALID_ARGUMENT;  // SELECTCHANNEL 2 is single-channel
   if (p->p_samp_s < 2 || (p->p_samp_s & 1)) return OFDIS_ERR_INVALID_ARGUMENT;
   if ((p->p_samp_s * p->p_samp_s * p->noc) % 4) return OFDIS_ERR_INVALID_ARGUMENT;
   if (p->p_samp_s * p->p_samp_s * p->noc > 448) return OFDIS_ERR_UNSUPPORTED;  // 7 values per lane

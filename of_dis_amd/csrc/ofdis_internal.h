@@ -32,6 +32,15 @@ struct PyrBaseArgs {
   float *out;                    // unpadded level [2n][h][w][noc]
 };
 
+// SELECTCHANNEL 2 (run_dense.cpp:139-148): level 0 = Sobel gradient magnitude of the divisibility-padded
+// intensity frame, sqrt(dx*dx + dy*dy) (exact up to the correctly rounded sqrt: dx, dy are multiples of
+// 1/8 below 2^10, their squares and sum exact in fp32).
+struct PyrGradmagArgs {
+  const uint8_t *img_a, *img_b;  // [n][H0][W0]
+  int n, W0, H0, padl, padt, Wp, Hp;
+  float *out;                    // [2n][Hp][Wp]
+};
+
 struct PyrDownArgs {
   const float *src;  // [2n][2h][2w][noc]
   float *dst;        // [2n][h][w][noc]
@@ -91,6 +100,7 @@ struct TvArgs {
   int sor_generic;             // force the generic global-memory SOR wavefront (A/B testing)
   int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
   int sor_rows;                // sweep-per-wave SOR rows per lane: 0 auto, 1/2/4/8 forced (A/B testing)
+  int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
 };
 
 struct UpArgs {
@@ -111,6 +121,7 @@ struct InitArgs {
 
 void launch_init_area(const InitArgs &a, hipStream_t s);
 void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s);
+void launch_pyr_gradmag(const PyrGradmagArgs &a, hipStream_t s);
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s);
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s);
 void launch_patch(const PatchArgs &a, hipStream_t s);

@@ -153,6 +153,27 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i;
 }
 
+// Gradient-magnitude base level (oracle: ofo_build_pyramid_ex): Sobel ksize 3 x 1/8 with reflect-101 at the
+// padded frame's border, on the replicate-padded u8 frame; same expression trees as k_pyr_pad_grad.
+__global__ __launch_bounds__(256) void k_pyr_gradmag(PyrGradmagArgs a) {
+  const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y, f = blockIdx.z;
+  if (X >= a.Wp) return;
+  const long fs = (long)a.H0 * a.W0;
+  const uint8_t *src = f < a.n ? a.img_a + (long)f * fs : a.img_b + (long)(f - a.n) * fs;
+  const int xm = reflect101(X - 1, a.Wp), xp = reflect101(X + 1, a.Wp);
+  const int ym = reflect101(Y - 1, a.Hp), yp = reflect101(Y + 1, a.Hp);
+  auto px = [&](int xx, int yy) {  // replicate divisibility padding (run_dense.cpp:307-311)
+    return (float)src[(long)clampi(yy - a.padt, 0, a.H0 - 1) * a.W0 + clampi(xx - a.padl, 0, a.W0 - 1)];
+  };
+  const float tm = px(xp, ym) - px(xm, ym);
+  const float t0 = px(xp, Y) - px(xm, Y);
+  const float tp = px(xp, yp) - px(xm, yp);
+  const float sm = (px(xm, ym) + px(xp, ym)) * 0.125f + px(X, ym) * 0.25f;
+  const float sp = (px(xm, yp) + px(xp, yp)) * 0.125f + px(X, yp) * 0.25f;
+  const float dx = (tm + tp) * 0.125f + t0 * 0.25f, dy = sp - sm;
+  a.out[((long)f * a.Hp + Y) * a.Wp + X] = sqrtf(dx * dx + dy * dy);
+}
+
 __global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
   const int W = a.w + 2 * a.pad, H = a.h + 2 * a.pad;
   const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y, f = blockIdx.z;
@@ -1348,7 +1369,7 @@ __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
     // d = the sum of the four diffusivities (solver.c:122-128, border forms :131-190).  It depends on the
     // system only, so it is computed here, fully parallel, with the same expressions; every SOR sweep then
     // reads the inverse.  (w < 2 or h < 2 run the point-SOR fallback on the raw matrix, solver.c:34-78.)
-    if (w >= 2 && h >= 2) {
+    if (w >= 2 && h >= 2 && !a.sor_point) {
       const float hl = x > 0 ? sl + sc : 0.0f;  // h[x-1]
       const float vt = su + sc;                  // v[y-1] (y > 0)
       const float dpsis = y == 0 ? hl + (shv + svv) : (y < h - 1 ? (hl + shv) + (vt + svv) : hl + (shv + vt));
@@ -2224,6 +2245,9 @@ void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s) {
   }
   k_pyr_base<<<dim3(ceil_div(a.w, 256), a.h, 2 * a.n), 256, 0, s>>>(a);
 }
+void launch_pyr_gradmag(const PyrGradmagArgs &a, hipStream_t s) {
+  k_pyr_gradmag<<<dim3(ceil_div(a.Wp, 256), a.Hp, 2 * a.n), 256, 0, s>>>(a);
+}
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {
   k_pyr_down<<<dim3(ceil_div((long)a.w * a.noc, 256), a.h, a.n2), 256, 0, s>>>(a);
 }
@@ -2345,7 +2369,7 @@ static void sor_waves(const TvArgs &a, hipStream_t s) {
 }
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
-  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2);
+  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);  // point SOR (solver.c:34-78)
   const int R = sor_rows_per_lane(a.h, a.sor_rows), G = (a.h + 64 * R - 1) / (64 * R);
   const size_t lds = sizeof(float4) * a.solverit * 3 * (G * 64 * R + 2);
   if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 &&
@@ -2384,7 +2408,7 @@ static void tv_level_s(const TvArgs &a, int n_inner, hipStream_t s) {
     k_tv_level<S, MODE, 1024><<<a.n, threads, lds, s>>>(a, n_inner);
 }
 bool tv_level_fusable(const TvArgs &a) {
-  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2);
+  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);
   const int G = (a.h + 63) / 64;
   return !tiny && !a.sor_generic && a.sor_variant == 0 && a.solverit >= 2 && a.solverit <= 4 &&
          G * a.solverit <= 16;

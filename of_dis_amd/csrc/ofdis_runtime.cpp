@@ -37,6 +37,8 @@ struct Plan {
   size_t off_init = 0;  // initial flow at the coarsest scale - 1, [n][Hp >> (sc_f+1)][Wp >> (sc_f+1)][nop]
   bool init = false;    // an initial flow is given: divisibility 2^(sc_f+1) (run_dense.cpp:302)
   bool fb = false;      // usefbcon: backward grid, flow and refinement
+  bool gradmag = false; // SELECTCHANNEL 2: float level 0 (gradient magnitude) halved down to sc_l
+  size_t off_gm = 0;    // its scratch: [2n][Hp][Wp] + [2n][Hp/2][Wp/2] (ping-pong)
   size_t total = 0;
 };
 
@@ -245,6 +247,11 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad, bool init 
   for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, (size_t)skew_plane(g.w, g.h));
   P.tv_plane = max_sp;
   if (p->usetvref) off = align_up(off + sizeof(float) * (size_t)n * max_sp * (14 + 9 * (size_t)P.noc));
+  P.off_gm = off;
+  if (p->gradmag) {
+    P.gradmag = true;
+    off = align_up(off + sizeof(float) * 2 * (size_t)n * ((size_t)Wp * Hp + (size_t)(Wp / 2) * (Hp / 2)));
+  }
   P.off_init = off;
   if (init) {
     P.init = true;
@@ -437,6 +444,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_rows = c->opt_sor_rows;
+      tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       if (c->opt_tv_fused && tv_level_fusable(tv)) {
         timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
       } else {
@@ -506,7 +514,35 @@ int check_device(int device) {
 // Pyramid of the batch (run_dense.cpp:299-312,327-328,131-179) into the workspace.
 int run_pyramid(ofdis_context *c, char *ws, const Plan &P, const uint8_t *a, const uint8_t *b, hipStream_t s) {
   const int n2 = 2 * P.n;
-  {
+  if (P.gradmag) {  // SELECTCHANNEL 2 (run_dense.cpp:139-148): float level 0, then 2x2 means down to sc_l
+    float *lvl0 = (float *)(ws + P.off_lvl[0]);
+    float *bufA = (float *)(ws + P.off_gm), *bufB = bufA + (size_t)n2 * P.Wp * P.Hp;
+    PyrGradmagArgs g{};
+    g.img_a = a;
+    g.img_b = b;
+    g.n = P.n;
+    g.W0 = P.W0;
+    g.H0 = P.H0;
+    g.padl = P.padl;
+    g.padt = P.padt;
+    g.Wp = P.Wp;
+    g.Hp = P.Hp;
+    g.out = P.sc_l == 0 ? lvl0 : bufA;
+    timed(c, 0, s, [&] { launch_pyr_gradmag(g, s); });
+    const float *src = bufA;
+    int w = P.Wp, h = P.Hp;
+    for (int l = 1; l <= P.sc_l; ++l) {
+      PyrDownArgs pd{};
+      pd.src = src;
+      pd.dst = l == P.sc_l ? lvl0 : ((l & 1) ? bufB : bufA);
+      pd.n2 = n2;
+      pd.w = w /= 2;
+      pd.h = h /= 2;
+      pd.noc = 1;
+      timed(c, 1, s, [&] { launch_pyr_down(pd, s); });
+      src = pd.dst;
+    }
+  } else {
     PyrBaseArgs pb{};
     pb.img_a = a;
     pb.img_b = b;

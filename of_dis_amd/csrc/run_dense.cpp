@@ -22,14 +22,17 @@
 #ifndef SELECTCHANNEL
 #define SELECTCHANNEL 1
 #endif
+// SELECTCHANNEL 1: intensity, 2: gradient magnitude of the intensity image (run_dense.cpp:139-148,
+// 194-197), 3: BGR colour
+#define NOCHANNELS (SELECTCHANNEL == 3 ? 3 : 1)
 
 // cv::imread(path, CV_LOAD_IMAGE_GRAYSCALE / CV_LOAD_IMAGE_COLOR) (run_dense.cpp:202-206)
 static std::vector<uint8_t> load(const char *path, int &w, int &h) {
-  int rc = ofdis_read_image(path, nullptr, &w, &h, SELECTCHANNEL, 0);
+  int rc = ofdis_read_image(path, nullptr, &w, &h, NOCHANNELS, 0);
   std::vector<uint8_t> px;
   if (rc == OFDIS_OK) {
-    px.resize((size_t)w * h * SELECTCHANNEL);
-    rc = ofdis_read_image(path, px.data(), &w, &h, SELECTCHANNEL, px.size());
+    px.resize((size_t)w * h * NOCHANNELS);
+    rc = ofdis_read_image(path, px.data(), &w, &h, NOCHANNELS, px.size());
   }
   if (rc != OFDIS_OK) {
     std::fprintf(stderr, "cannot read %s (PNG or Netpbm expected): %s\n", path, ofdis_status_string(rc));
@@ -57,9 +60,13 @@ int main(int argc, char **argv) {
   ofdis_params p;
   int rc;
   if (argc <= 5)
-    rc = ofdis_params_oppoint(&p, argc == 5 ? std::atoi(argv[4]) : 2, w, SELECTMODE, SELECTCHANNEL);
+    rc = ofdis_params_oppoint(&p, argc == 5 ? std::atoi(argv[4]) : 2, w, SELECTMODE, NOCHANNELS);
   else
-    rc = ofdis_params_from_strings(&p, 20, (const char *const *)(argv + 4), SELECTMODE, SELECTCHANNEL);
+    rc = ofdis_params_from_strings(&p, 20, (const char *const *)(argv + 4), SELECTMODE, NOCHANNELS);
+  p.gradmag = SELECTCHANNEL == 2;
+#ifdef OFDIS_OMP_BUILD
+  p.omp_build = 1;  // the reference's USE_OPENMP build semantics (point SOR), in single-thread order
+#endif
   if (rc == OFDIS_OK) rc = ofdis_params_validate(&p, -1, -1, -1);
   if (rc != OFDIS_OK) {
     std::fprintf(stderr, "invalid parameters: %s\n", ofdis_status_string(rc));

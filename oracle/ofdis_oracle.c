@@ -170,10 +170,23 @@ static void pad_level(const float *L, int w, int h, int noc, int pad, int replic
 
 int ofo_build_pyramid(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
                       float **img_pyr, float **dx_pyr, float **dy_pyr) {
+  return ofo_build_pyramid_ex(img, width, height, noc, sc_f, sc_l, imgpadding, 0, img_pyr, dx_pyr, dy_pyr);
+}
+
+int ofo_build_pyramid_ex(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
+                         int gradmag, float **img_pyr, float **dx_pyr, float **dy_pyr) {
   int w = width, h = height;
   float *cur = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
   if (!cur) return OFDIS_ERR_OUT_OF_MEMORY;
   for (size_t i = 0; i < (size_t)w * h * noc; ++i) cur[i] = (float)img[i]; /* convertTo CV_32F (:327) */
+  if (gradmag) { /* SELECTCHANNEL 2 (:139-148): level 0 = sqrt(dx.mul(dx) + dy.mul(dy)), Sobel 3, 1/8 */
+    float *gx = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
+    float *gy = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
+    if (!gx || !gy) { free(gx); free(gy); free(cur); return OFDIS_ERR_OUT_OF_MEMORY; }
+    sobel_level(cur, w, h, noc, gx, gy);
+    for (size_t i = 0; i < (size_t)w * h * noc; ++i) cur[i] = sqrtf(gx[i] * gx[i] + gy[i] * gy[i]);
+    free(gx); free(gy);
+  }
   for (int s = 0; s <= sc_f; ++s) {
     if (s > 0) { /* cv::resize(.5, INTER_LINEAR) -> OpenCV area-fast 2x: mean of the 2x2 block */
       int nw = w / 2, nh = h / 2;
@@ -885,8 +898,9 @@ void ofo_compute_data_de(float *a11, float *b1, const float *mask, const float *
   }
 }
 
-/* sor_coupled_slow_but_readable (solver.c:34-78): point SOR, used upstream for tiny images. */
-static void sor_point_of(float *du, float *dv, const float *a11, const float *a12, const float *a22,
+/* sor_coupled_slow_but_readable (solver.c:34-78): point SOR, used upstream for tiny images and by the
+ * OpenMP build for every image (refine_variational.cpp:202-203; single-thread order). */
+void ofo_sor_point_of(float *du, float *dv, const float *a11, const float *a12, const float *a22,
                          const float *b1, const float *b2, const float *hh, const float *vv, int w, int hgt,
                          int iterations, float omega) {
   for (int it = 0; it < iterations; ++it)
@@ -909,7 +923,7 @@ static void sor_point_of(float *du, float *dv, const float *a11, const float *a1
 void ofo_sor_coupled(float *du, float *dv, float *a11, float *a12, float *a22, const float *b1, const float *b2,
                      const float *hh, const float *vv, int w, int hgt, int iterations, float omega) {
   if (w < 2 || hgt < 2 || iterations < 1) {
-    sor_point_of(du, dv, a11, a12, a22, b1, b2, hh, vv, w, hgt, iterations, omega);
+    ofo_sor_point_of(du, dv, a11, a12, a22, b1, b2, hh, vv, w, hgt, iterations, omega);
     return;
   }
   for (int it = 0; it < iterations; ++it)
@@ -1018,7 +1032,10 @@ static int var_refine(const cam_t *c, const opt_t *o, const ofdis_params *p, con
                        hgo3);
       ofo_sub_laplacian(b1, wx, sh, sv, w, h);
       ofo_sub_laplacian(b2, wy, sh, sv, w, h);
-      ofo_sor_coupled(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
+      if (p->omp_build) /* refine_variational.cpp:202-203 (#ifdef _OPENMP) */
+        ofo_sor_point_of(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
+      else
+        ofo_sor_coupled(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
       for (size_t i = 0; i < n; ++i) {
         uu[i] = wx[i] + du[i];
         vv[i] = wy[i] + dv[i];
@@ -1270,8 +1287,8 @@ int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *ini
     size_t n = (size_t)((Wp >> s) + 2 * pad) * ((Hp >> s) + 2 * pad) * noc;
     for (int k = 0; k < 6; ++k) pyr[k][s] = (float *)malloc(sizeof(float) * n);
   }
-  rc = ofo_build_pyramid(pa, Wp, Hp, noc, p->sc_f, p->sc_l, pad, pyr[0], pyr[1], pyr[2]);
-  if (!rc) rc = ofo_build_pyramid(pb, Wp, Hp, noc, p->sc_f, p->sc_l, pad, pyr[3], pyr[4], pyr[5]);
+  rc = ofo_build_pyramid_ex(pa, Wp, Hp, noc, p->sc_f, p->sc_l, pad, p->gradmag, pyr[0], pyr[1], pyr[2]);
+  if (!rc) rc = ofo_build_pyramid_ex(pb, Wp, Hp, noc, p->sc_f, p->sc_l, pad, p->gradmag, pyr[3], pyr[4], pyr[5]);
   const int wl = Wp >> p->sc_l, hl = Hp >> p->sc_l;
   float *fl = (float *)malloc(sizeof(float) * (size_t)wl * hl * nop);
   float *ini = NULL;

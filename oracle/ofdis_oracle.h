@@ -38,6 +38,10 @@ void ofo_divisibility_pad(int width, int height, int sc_f, int *padw, int *padh)
 int ofo_build_pyramid(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
                       float **img_pyr, float **dx_pyr, float **dy_pyr);
 
+/* Same; gradmag = SELECTCHANNEL 2 (run_dense.cpp:139-148): level 0 is the Sobel gradient magnitude. */
+int ofo_build_pyramid_ex(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
+                         int gradmag, float **img_pyr, float **dx_pyr, float **dy_pyr);
+
 /* OFC::OFClass (oflow.cpp:31-338).  Optional per-scale capture of the flow after aggregation
  * and after TV refinement (arrays indexed by scale, w_s*h_s*nop interleaved; may be NULL). */
 int ofo_oflow(const float *const *im_ao, const float *const *im_ao_dx, const float *const *im_ao_dy,
@@ -88,6 +92,9 @@ void ofo_compute_data_de(float *a11, float *b1, const float *mask, const float *
 /* sor_coupled (solver.c:83-433) incl. its small-image fallback (solver.c:34-78) */
 void ofo_sor_coupled(float *du, float *dv, float *a11, float *a12, float *a22, const float *b1, const float *b2,
                      const float *h, const float *v, int w, int hgt, int iterations, float omega);
+/* sor_coupled_slow_but_readable (solver.c:34-78), the OpenMP build's optical-flow SOR */
+void ofo_sor_point_of(float *du, float *dv, const float *a11, const float *a12, const float *a22, const float *b1,
+                      const float *b2, const float *h, const float *v, int w, int hgt, int iterations, float omega);
 /* sor_coupled_slow_but_readable_DE (solver.c:439-471) */
 void ofo_sor_point_de(float *du, const float *a11, const float *b1, const float *h, const float *v, int w,
                       int hgt, int iterations, float omega);

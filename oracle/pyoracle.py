@@ -31,6 +31,7 @@ class Params(C.Structure):
         ("patnorm", C.c_int), ("usetvref", C.c_int),
         ("tv_alpha", C.c_float), ("tv_gamma", C.c_float), ("tv_delta", C.c_float),
         ("tv_innerit", C.c_int), ("tv_solverit", C.c_int), ("tv_sor", C.c_float), ("verbosity", C.c_int),
+        ("omp_build", C.c_int), ("gradmag", C.c_int),
     ]
 
     def as_dict(self):
@@ -63,6 +64,7 @@ def lib():
         L.ofo_params_oppoint.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int, C.c_int]
         L.ofo_divisibility_pad.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.ofo_build_pyramid.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp]
+        L.ofo_build_pyramid_ex.argtypes = [_u8p] + [C.c_int] * 7 + [vp, vp, vp]
         L.ofo_oflow.argtypes = [vp] * 6 + [C.c_int, _f32p, vp, C.c_int, C.c_int, C.POINTER(Params), vp, vp]
         L.ofo_upsample_crop.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, _f32p]
@@ -78,7 +80,8 @@ def lib():
         L.ofo_compute_data_de.argtypes = [_f32p] * 12 + [C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
         L.ofo_sor_coupled.argtypes = [_f32p] * 9 + [C.c_int, C.c_int, C.c_int, C.c_float]
         L.ofo_sor_point_de.argtypes = [_f32p] * 5 + [C.c_int, C.c_int, C.c_int, C.c_float]
-        for f in ("ofo_params_oppoint", "ofo_build_pyramid", "ofo_oflow", "ofo_upsample_crop", "ofo_run_u8",
+        L.ofo_sor_point_of.argtypes = [_f32p] * 9 + [C.c_int, C.c_int, C.c_int, C.c_float]
+        for f in ("ofo_params_oppoint", "ofo_build_pyramid", "ofo_build_pyramid_ex", "ofo_oflow", "ofo_upsample_crop", "ofo_run_u8",
                   "ofo_run_u8_init", "ofo_refine_level"):
             getattr(L, f).restype = C.c_int
         _lib = L
@@ -112,10 +115,11 @@ def build_pyramid(img: np.ndarray, p: Params, imgpadding: int):
     for s in range(p.sc_l, p.sc_f + 1):
         shp = ((h >> s) + 2 * imgpadding, (w >> s) + 2 * imgpadding, noc)
         lev[s] = tuple(np.zeros(shp, np.float32) for _ in range(3))
-    rc = lib().ofo_build_pyramid(np.ascontiguousarray(img, dtype=np.uint8), w, h, noc, p.sc_f, p.sc_l, imgpadding,
-                                 _ptr_array({s: v[0] for s, v in lev.items()}),
-                                 _ptr_array({s: v[1] for s, v in lev.items()}),
-                                 _ptr_array({s: v[2] for s, v in lev.items()}))
+    rc = lib().ofo_build_pyramid_ex(np.ascontiguousarray(img, dtype=np.uint8), w, h, noc, p.sc_f, p.sc_l,
+                                    imgpadding, p.gradmag,
+                                    _ptr_array({s: v[0] for s, v in lev.items()}),
+                                    _ptr_array({s: v[1] for s, v in lev.items()}),
+                                    _ptr_array({s: v[2] for s, v in lev.items()}))
     assert rc == 0, rc
     return lev
 
@@ -241,6 +245,7 @@ def ref(noc: int = 1):
         L.compute_data_DE.argtypes = [vp] * 14 + [C.c_float] * 3
         L.sor_coupled.argtypes = [vp] * 9 + [C.c_int, C.c_float]
         L.sor_coupled_slow_but_readable_DE.argtypes = [vp] * 5 + [C.c_int, C.c_float]
+        L.sor_coupled_slow_but_readable.argtypes = [vp] * 9 + [C.c_int, C.c_float]
         _ref_libs[noc] = L
     return _ref_libs[noc]
 
@@ -288,8 +293,9 @@ def ref_refine_level(noc, mode, im1, im2, flow, level, p):
                            uu.ptr, vv.ptr, *[x.ptr for x in I], C.c_float(hdo3), C.c_float(0), C.c_float(hgo3))
             R.sub_laplacian(b1.ptr, wx.ptr, sh.ptr, sv.ptr)
             R.sub_laplacian(b2.ptr, wy.ptr, sh.ptr, sv.ptr)
-            R.sor_coupled(du.ptr, dv.ptr, a11.ptr, a12.ptr, a22.ptr, b1.ptr, b2.ptr, sh.ptr, sv.ptr,
-                          p["tv_solverit"], C.c_float(p["tv_sor"]))
+            sor = R.sor_coupled_slow_but_readable if p.get("omp_build") else R.sor_coupled  # :202-205
+            sor(du.ptr, dv.ptr, a11.ptr, a12.ptr, a22.ptr, b1.ptr, b2.ptr, sh.ptr, sv.ptr,
+                p["tv_solverit"], C.c_float(p["tv_sor"]))
             uu.buf[:] = wx.buf + du.buf
             vv.buf[:] = wy.buf + dv.buf
         else:

@@ -86,15 +86,43 @@ def make_sor():
                         iters=iters, omega=np.float32(omega), out_du=refs[0].get())
 
 
+def make_sor_point_of():
+    """sor_coupled_slow_but_readable (solver.c:34-78): the USE_OPENMP build's OF solver."""
+    w, h, iters, omega = 29, 21, 3, 1.6
+    rng = np.random.default_rng(78)
+    a11 = (np.abs(rnd(rng, h, w)) * 5 + 0.5).astype(np.float32)
+    a22 = (np.abs(rnd(rng, h, w)) * 5 + 0.5).astype(np.float32)
+    a12 = rnd(rng, h, w, scale=0.3)
+    b1, b2 = rnd(rng, h, w), rnd(rng, h, w)
+    hh = np.abs(rnd(rng, h, w)); hh[:, -1] = 0
+    vv = np.abs(rnd(rng, h, w)); vv[-1, :] = 0
+    du, dv = rnd(rng, h, w, scale=0.1), rnd(rng, h, w, scale=0.1)
+    ins = [du, dv, a11, a12, a22, b1, b2, hh, vv]
+    R = O.ref(1)
+    refs = []
+    for a in ins:
+        r = O.RefImage(w, h); r.set(a); refs.append(r)
+    R.sor_coupled_slow_but_readable(*[r.ptr for r in refs], iters, C.c_float(omega))
+    np.savez_compressed(os.path.join(HERE, "fdf_sor_point_of.npz"), du=du, dv=dv, a11=a11, a12=a12, a22=a22,
+                        b1=b1, b2=b2, h=hh, v=vv, iters=iters, omega=np.float32(omega), out_du=refs[0].get(),
+                        out_dv=refs[1].get())
+
+
 def pipe_cases():
     """(w, h, noc, mode, oppoint, overrides) -- small whole-pipeline regression vectors."""
     return [(160, 120, 1, 1, 2, {}), (173, 97, 1, 1, 2, {}), (96, 64, 3, 1, 3, {"costfct": 1}),
-            (120, 64, 1, 2, 4, {}), (128, 96, 1, 1, 2, {"usefbcon": 1})]
+            (120, 64, 1, 2, 4, {}), (128, 96, 1, 1, 2, {"usefbcon": 1})] + variant_pipe_cases()
+
+
+def variant_pipe_cases():
+    """Build variants: USE_OPENMP semantics (point SOR) and SELECTCHANNEL 2 (gradient-magnitude input)."""
+    return [(128, 96, 1, 1, 2, {"omp_build": 1}), (136, 88, 1, 1, 2, {"gradmag": 1})]
 
 
 def pipe_name(w, h, noc, mode, op, over=None):
-    fb = "_fb" if (over or {}).get("usefbcon") else ""
-    return os.path.join(HERE, f"pipe_m{mode}_c{noc}_op{op}_{w}x{h}{fb}.npz")
+    over = over or {}
+    tag = "".join(t for k, t in (("usefbcon", "_fb"), ("omp_build", "_omp"), ("gradmag", "_grad")) if over.get(k))
+    return os.path.join(HERE, f"pipe_m{mode}_c{noc}_op{op}_{w}x{h}{tag}.npz")
 
 
 def make_pipe(w, h, noc, mode, op, over):
@@ -115,6 +143,7 @@ def main():
     for c in refine_cases():
         make_refine(*c)
     make_sor()
+    make_sor_point_of()
     for c in pipe_cases():
         make_pipe(*c)
     print("golden vectors written to", HERE)

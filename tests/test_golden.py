@@ -54,6 +54,15 @@ def test_sor_coupled_matches_reference_vectors(oracle):
         assert np.array_equal(_bits(arrs[k]), _bits(g["out_" + name])), name
 
 
+def test_sor_point_of_matches_reference_vectors(oracle):
+    """The USE_OPENMP build's solver, sor_coupled_slow_but_readable (solver.c:34-78)."""
+    g = _load(os.path.join(GOLD, "fdf_sor_point_of.npz"))
+    h, w = g["du"].shape
+    arrs = [g[k].copy() for k in ("du", "dv", "a11", "a12", "a22", "b1", "b2", "h", "v")]
+    O.lib().ofo_sor_point_of(*arrs, w, h, int(g["iters"]), float(g["omega"]))
+    assert np.array_equal(_bits(arrs[0]), _bits(g["out_du"])) and np.array_equal(_bits(arrs[1]), _bits(g["out_dv"]))
+
+
 def test_sor_de_matches_reference_vectors(oracle):
     g = _load(os.path.join(GOLD, "fdf_sor_de.npz"))
     h, w = g["du"].shape
@@ -104,3 +113,21 @@ def test_oracle_known_answer(oracle, mode, op, noc):
     med = np.median(out[40:-40, 40:-40].reshape(-1, out.shape[-1]), 0)
     want = [6.5, 2.25] if mode == 1 else [-6.5]
     assert np.all(np.abs(med - want) < 0.25), med
+
+
+def test_oracle_gradmag_base_level(oracle):
+    """SELECTCHANNEL 2 (run_dense.cpp:139-148): the finest pyramid level is sqrt(dx^2 + dy^2) of the Sobel
+    (ksize 3, x 1/8, reflect-101) derivatives -- exact in fp32 up to the rounded sqrt, so an independent
+    numpy computation must agree bit for bit."""
+    import of_dis_amd as od
+    a, _ = od.synth_pair(64, 48, 1, 2, 1)
+    p = O.oppoint(2, 64, 1, 1)
+    p.sc_f, p.sc_l, p.gradmag = 1, 0, 1
+    lev = O.build_pyramid(a, p, 8)
+    f = a[..., 0].astype(np.float64)
+    fp = np.pad(f, 1, mode="reflect")  # numpy "reflect" == OpenCV BORDER_REFLECT_101
+    dx = (fp[:-2, 2:] - fp[:-2, :-2] + fp[2:, 2:] - fp[2:, :-2]) / 8 + (fp[1:-1, 2:] - fp[1:-1, :-2]) / 4
+    dy = (fp[2:, :-2] + fp[2:, 2:] - fp[:-2, :-2] - fp[:-2, 2:]) / 8 + (fp[2:, 1:-1] - fp[:-2, 1:-1]) / 4
+    want = np.sqrt((dx * dx + dy * dy).astype(np.float32))  # squares exact; fp32 sqrt correctly rounded
+    got = lev[0][0][8:-8, 8:-8, 0]
+    assert np.array_equal(_bits(got), _bits(want))

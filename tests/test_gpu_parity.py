@@ -57,6 +57,11 @@ CASES = [
     (240, 120, 1, 2, 4, {"usefbcon": 1, "max_iter": 16, "min_iter": 16}),  # ... depth (right camera clamp)
     (400, 300, 1, 1, 2, {"sc_l": 0, "sc_f": 2}),              # 300 rows: 5 row groups x 3 sweep waves
     (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows: register pipeline, 1024 threads
+    (160, 120, 1, 1, 2, {"omp_build": 1}),                    # USE_OPENMP build: point SOR (solver.c:34-78)
+    (192, 128, 3, 1, 3, {"omp_build": 1, "usefbcon": 1}),     # ... RGB, forward-backward
+    (173, 97, 1, 1, 2, {"gradmag": 1}),                       # SELECTCHANNEL 2: gradient-magnitude pyramid
+    (240, 120, 1, 2, 4, {"gradmag": 1, "max_iter": 16, "min_iter": 16}),  # ... depth
+    (160, 120, 1, 1, 2, {"gradmag": 1, "sc_l": 0, "sc_f": 2}),             # ... finest scale 0
 ]
 
 
@@ -114,12 +119,15 @@ def test_kernel_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op,
     assert_bitexact(got, ref, f"{key}={val}")
 
 
-@pytest.mark.parametrize("w,h,noc,op", [(160, 120, 1, 2), (173, 97, 1, 2), (192, 128, 3, 3), (1920, 1080, 1, 2),
-                                         (640, 480, 1, 2), (330, 250, 1, 2), (2000, 1000, 1, 2)])
-def test_pyramid_bitexact(oracle, od, ctx, w, h, noc, op):
+@pytest.mark.parametrize("w,h,noc,op,over", [(160, 120, 1, 2, {}), (173, 97, 1, 2, {}), (192, 128, 3, 3, {}),
+                                              (1920, 1080, 1, 2, {}), (640, 480, 1, 2, {}), (330, 250, 1, 2, {}),
+                                              (2000, 1000, 1, 2, {}), (173, 97, 1, 2, {"gradmag": 1}),
+                                              (640, 480, 1, 2, {"gradmag": 1}),
+                                              (96, 64, 1, 2, {"gradmag": 1, "sc_l": 0, "sc_f": 1})])
+def test_pyramid_bitexact(oracle, od, ctx, w, h, noc, op, over):
     O = oracle
     a, _ = od.synth_pair(w, h, noc, 1, 1)
-    p, q = _params(od, O, w, noc, 1, op, {})
+    p, q = _params(od, O, w, noc, 1, op, over)
     pw, ph = O.divisibility_pad(w, h, q.sc_f)
     padded = np.pad(a, ((ph // 2, ph - ph // 2), (pw // 2, pw - pw // 2), (0, 0)), mode="edge")
     want = O.build_pyramid(padded, q, q.p_samp_s)
@@ -216,8 +224,11 @@ def test_oflow_hpp_dropin_program(oracle, od, tmp_path):
     assert_bitexact(od.read_flo(str(out)), want, "OFC::OFClass drop-in program")
 
 
-@pytest.mark.parametrize("exe_name,noc,mode", [("run_OF_INT", 1, 1), ("run_OF_RGB", 3, 1), ("run_DE_INT", 1, 2)])
-def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode):
+@pytest.mark.parametrize("exe_name,noc,mode,over", [("run_OF_INT", 1, 1, {}), ("run_OF_RGB", 3, 1, {}),
+                                                     ("run_DE_INT", 1, 2, {}), ("run_OF_GRAD", 1, 1, {"gradmag": 1}),
+                                                     ("run_DE_GRAD", 1, 2, {"gradmag": 1}),
+                                                     ("run_OF_INT_OMP", 1, 1, {"omp_build": 1})])
+def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode, over):
     """The CLI reads colour PNGs with cv::imread's semantics (GRAYSCALE conversion for *_INT) and writes
     the oracle's flow (.flo) / depth (.pfm) for the decoded pixels, bit for bit."""
     import os
@@ -236,7 +247,10 @@ def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode):
     r = subprocess.run([exe, str(tmp_path / "a.png"), str(tmp_path / "b.png"), str(out), "2"], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    want = oracle.run_u8(a, b, oracle.oppoint(2, w, mode, noc))
+    q = oracle.oppoint(2, w, mode, noc)
+    for k, v in over.items():
+        setattr(q, k, v)
+    want = oracle.run_u8(a, b, q)
     if mode == 1:
         got = od.read_flo(str(out))
     else:

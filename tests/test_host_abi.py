@@ -44,7 +44,7 @@ def test_library_is_gfx950_code():
 
 def test_abi_version_and_status_strings():
     L = od.lib()
-    assert L.ofdis_abi_version() == 1
+    assert L.ofdis_abi_version() == 2
     for code in range(7):
         assert L.ofdis_status_string(code)
     assert b"unknown" in L.ofdis_status_string(99).lower()

@@ -162,6 +162,22 @@ def test_sor_coupled(oracle, w, h, iters):
         assert bits_equal(refs[k].get(), mine[k]), f"array {k}"
 
 
+@pytest.mark.parametrize("w,h", SIZES + [(1, 5), (6, 1)])
+def test_sor_point_of(oracle, w, h):
+    """sor_coupled_slow_but_readable (solver.c:34-78): the OpenMP build's OF solver, single-thread order."""
+    rng = np.random.default_rng(53 + w * 3 + h)
+    R = O.ref(1)
+    arrs = _sor_inputs(rng, h, w)
+    refs = []
+    for a in arrs:
+        r = O.RefImage(w, h); r.set(a); refs.append(r)
+    R.sor_coupled_slow_but_readable(*[r.ptr for r in refs], 3, C.c_float(1.6))
+    mine = [a.copy() for a in arrs]
+    O.lib().ofo_sor_point_of(*mine, w, h, 3, 1.6)
+    for k in (0, 1):
+        assert bits_equal(refs[k].get(), mine[k]), f"array {k}"
+
+
 @pytest.mark.parametrize("w,h", SIZES)
 def test_sor_point_de(oracle, w, h):
     rng = np.random.default_rng(41 + w)
@@ -176,12 +192,14 @@ def test_sor_point_de(oracle, w, h):
     assert bits_equal(refs[0].get(), mine)
 
 
-@pytest.mark.parametrize("mode,noc", [(1, 1), (1, 3), (2, 1), (2, 3)])
+@pytest.mark.parametrize("mode,noc,omp", [(1, 1, 0), (1, 3, 0), (2, 1, 0), (2, 3, 0), (1, 1, 1), (1, 3, 1)])
 @pytest.mark.parametrize("w,h,level", [(30, 17, 6), (41, 23, 2), (16, 12, 0)])
-def test_refine_level(oracle, mode, noc, w, h, level):
+def test_refine_level(oracle, mode, noc, omp, w, h, level):
+    """One VarRefClass level; omp = 1: the USE_OPENMP build's solver (refine_variational.cpp:202-203)."""
     rng = np.random.default_rng(100 + w + noc + mode)
     pad = 8
     p = O.oppoint(2, 1920, mode, noc)
+    p.omp_build = omp
     nop = 2 if mode == 1 else 1
     im1 = (rng.random((noc, h, w)) * 255).astype(np.float32)
     im2 = np.roll(im1, 1, axis=-1) + rnd(rng, noc, h, w, scale=2)
