@@ -101,6 +101,7 @@ struct TvArgs {
   int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
   int sor_rows;                // sweep-per-wave SOR rows per lane: 0 auto, 1/2/4/8 forced (A/B testing)
   int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
+  int sor_lean;                // sweep-per-wave SOR, one row per lane: lean form (SorLane) vs SorWave (A/B)
 };
 
 struct UpArgs {

@@ -1380,8 +1380,8 @@ __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
       A12 = A12 / (0.0f - det);
     }
     float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
-    C[0] = make_float4(A11, A12, A22, B1);
-    C[1] = make_float4(B2, shv, svv, 0.0f);
+    C[0] = make_float4(A11, A12, A12, A22);  // (a11, a12) and (a12, a22) pair up for packed fp32
+    C[1] = make_float4(B1, B2, shv, svv);
   } else {
     reinterpret_cast<float4 *>(a.coef)[idx] = make_float4(A11, B1, shv, svv);
   }
@@ -1411,9 +1411,9 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
   const long fo = (long)f * a.sp;
   float *du = a.du + fo, *dv = a.dv + fo;
   float4 *C = reinterpret_cast<float4 *>(a.coef) + fo * (MODE == 2 ? 1 : 2);
-  // AoS accessors: OF (a11, a12, a22, b1) (b2, sh, sv, -); DE (a11, b1, sh, sv)
-#define SH_(o) (MODE == 2 ? C[o].z : C[2 * (o) + 1].y)
-#define SV_(o) (MODE == 2 ? C[o].w : C[2 * (o) + 1].z)
+  // AoS accessors: OF (a11, a12, a12, a22) (b1, b2, sh, sv); DE (a11, b1, sh, sv)
+#define SH_(o) (MODE == 2 ? C[o].z : C[2 * (o) + 1].z)
+#define SV_(o) (MODE == 2 ? C[o].w : C[2 * (o) + 1].w)
   const float omega = a.omega;
   const int items = S * h;
   const int T = (w - 1) + (h - 1) + 2 * (S - 1) + 1;
@@ -1429,7 +1429,7 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
       if (MODE == 0) {
         const float4 c0 = C[2 * o];
         const float4 c1 = C[2 * o + 1];
-        const float b1 = c0.w, b2 = c1.x, hr = c1.y, vo = c1.z;
+        const float b1 = c1.x, b2 = c1.y, hr = c1.z, vo = c1.w;
         const float hl = x > 0 ? SH_(oL) : 0.0f;
         const float ur = x < w - 1 ? du[oR] : 0.0f, vr = x < w - 1 ? dv[oR] : 0.0f;
         float s1, s2;
@@ -1445,7 +1445,7 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
           s1 = (b1 + hr * ur) + vt * du[oU];
           s2 = (b2 + hr * vr) + vt * dv[oU];
         }
-        const float i11 = c0.x, i12 = c0.y, i22 = c0.z;  // inverse precomputed by k_tv_system
+        const float i11 = c0.x, i12 = c0.y, i22 = c0.w;  // inverse precomputed by k_tv_system
         float B1 = s1, B2 = s2;
         if (x > 0) {
           B1 = hl * du[oL] + s1;
@@ -1459,10 +1459,10 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
         float su = 0.0f, sv = 0.0f, sd = 0.0f;
         if (y > 0) { const float q = SV_(oU); su -= q * du[oU]; sv -= q * dv[oU]; sd += q; }
         if (x > 0) { const float q = SH_(oL); su -= q * du[oL]; sv -= q * dv[oL]; sd += q; }
-        if (y < h - 1) { su -= c1.z * du[oD]; sv -= c1.z * dv[oD]; sd += c1.z; }
-        if (x < w - 1) { su -= c1.y * du[oR]; sv -= c1.y * dv[oR]; sd += c1.y; }
-        const float A11 = c0.x + sd, A12 = c0.y, A22 = c0.z + sd;
-        const float B1 = c0.w - su, B2 = c1.x - sv;
+        if (y < h - 1) { su -= c1.w * du[oD]; sv -= c1.w * dv[oD]; sd += c1.w; }
+        if (x < w - 1) { su -= c1.z * du[oR]; sv -= c1.z * dv[oR]; sd += c1.z; }
+        const float A11 = c0.x + sd, A12 = c0.y, A22 = c0.w + sd;
+        const float B1 = c1.x - su, B2 = c1.y - sv;
         du[o] = (1.0f - omega) * du[o] + omega / A11 * (B1 - A12 * dv[o]);
         dv[o] = (1.0f - omega) * dv[o] + omega / A22 * (B2 - A12 * du[o]);
       } else {
@@ -1575,7 +1575,7 @@ struct SorPipe {
     // consume this step's prefetched values, then reuse the buffer for step t + 2
     float c11, c12 = 0, c22 = 0, cb1, cb2 = 0, csh, csv;
     if (MODE == 0) {
-      c11 = B.c0.x; c12 = B.c0.y; c22 = B.c0.z; cb1 = B.c0.w; cb2 = B.c1.x; csh = B.c1.y; csv = B.c1.z;
+      c11 = B.c0.x; c12 = B.c0.y; c22 = B.c0.w; cb1 = B.c1.x; cb2 = B.c1.y; csh = B.c1.z; csv = B.c1.w;
     } else {
       c11 = B.c0.x; cb1 = B.c0.y; csh = B.c0.z; csv = B.c0.w;
     }
@@ -1833,9 +1833,9 @@ struct SorWave {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (MODE == 0) {
-        i11[r] = opaque_mov(B[r].c0.x); i12[r] = opaque_mov(B[r].c0.y); i22[r] = opaque_mov(B[r].c0.z);
-        b1[r] = opaque_mov(B[r].c0.w); b2[r] = opaque_mov(B[r].c1.x); hr[r] = opaque_mov(B[r].c1.y);
-        vv[r] = opaque_mov(B[r].c1.z);
+        i11[r] = opaque_mov(B[r].c0.x); i12[r] = opaque_mov(B[r].c0.y); i22[r] = opaque_mov(B[r].c0.w);
+        b1[r] = opaque_mov(B[r].c1.x); b2[r] = opaque_mov(B[r].c1.y); hr[r] = opaque_mov(B[r].c1.z);
+        vv[r] = opaque_mov(B[r].c1.w);
       } else {
         i11[r] = opaque_mov(B[r].c0.x); b1[r] = opaque_mov(B[r].c0.y); hr[r] = opaque_mov(B[r].c0.z);
         vv[r] = opaque_mov(B[r].c0.w);
@@ -1931,6 +1931,221 @@ struct SorWave {
   }
 };
 
+// Skewed row of anti-diagonal d for a wave-uniform d (SALU only).  Diagonals outside the frame map to a row
+// inside the plane: every lane reading it is outside the frame (its value is never used), and with the
+// 64 dump slots after the rows even lanes beyond h stay inside the plane.
+// The layout is folded into two wave-uniform constants (branch-free SALU): lim = w (wrapped) or a value
+// above every d (unwrapped), rmax = the last row of the plane.
+__device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
+  const int dd = max(d, 0);
+  return min(dd >= lim ? dd - lim : dd, rmax);
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Lean form of the sweep-per-wave SOR (one row per lane), same schedule and arithmetic as SorWave:
+//  * addresses are a wave-uniform base (SALU: skewed row of the step's diagonal) plus a per-lane constant:
+//    no per-step vector address arithmetic; lanes outside the frame read real plane slots (sor_row) and
+//    only the stores are masked;
+//  * coefficients are multi-buffered (NB buffers, prefetch distance NB - 1 into the buffer of step t-1);
+//    sweep 0's right neighbour is the next step's own value (one load fewer);
+//  * the LDS rings hold (u, v) as float2 [row][slot] (24-B lane stride) and sv as float [row][slot]
+//    (12-B stride): conflict-free ds_read_b64 / ds_write_b64 / b32, slots a compile-time phase of the
+//    unrolled block -> immediate offsets.  (Loading the upper pixel's sv from the coefficients instead
+//    measured 40 % slower with 4 frames per CU: the per-sweep coefficient re-reads already load the
+//    vector memory path, the LDS much less);
+//  * (u, v) pairs run on packed fp32 (v_pk_mul_f32 / v_pk_add_f32: the same roundings as scalar, no FMA);
+//  * a wave whose rows are all outside the frame for a whole block only joins the block's barriers.
+template <int S, int MODE, bool FIRST, bool LAST, int NB>
+struct SorLane {
+  static constexpr int PD = NB - 1;                                    // prefetch distance (steps)
+  static constexpr int U = NB % 3 == 0 ? (NB < 6 ? 6 : NB) : 3 * NB;  // multiple of 3 (ring) and NB
+  static constexpr int CW = MODE == 0 ? 2 : 1;                         // float4s of coefficients per pixel
+  struct Ld {
+    float4 c0, c1;
+    f2v o, b;   // sweep 0: old (u, v) of the pixel and of the one below (the right one: next step's o)
+  };
+  Ld L0, L1, L2, L3, L4, L5;  // buffers as named members (no array: keeps them in registers)
+  template <int I>
+  __device__ __forceinline__ Ld &buf() {
+    static_assert(I < NB && NB <= 6, "buffer index");
+    if constexpr (I == 0) return L0;
+    else if constexpr (I == 1) return L1;
+    else if constexpr (I == 2) return L2;
+    else if constexpr (I == 3) return L3;
+    else if constexpr (I == 4) return L4;
+    else return L5;
+  }
+  f2v pp;      // own (u, v) of step t-1 (left neighbour)
+  float phr;   // own sh of step t-1 (left neighbour's sh)
+  const float4 *C;
+  const float *du_r, *dv_r;
+  float *du, *dv;
+  f2v *ring_s;        // [NR][3] this sweep, lane base = entry y + 1 (entry 0 = row -1 stays zero)
+  const f2v *ring_p;  // [NR][3] previous sweep
+  float *sv_s;        // [NR][3] this sweep's sv (row y's sv at entry y + 1)
+  int w, h, y, s, lim, rmax, hplane;
+  bool border, notop;
+  float omega;
+
+  __device__ __forceinline__ void load(int t, Ld &B) {
+    const int d = t - 2 * s;
+    const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
+    const float4 *cp = C + (size_t)r0 * CW;
+    B.c0 = cp[(unsigned)y * CW];
+    if (MODE == 0) B.c1 = cp[(unsigned)y * CW + 1];
+    if (FIRST) {
+      const unsigned r1 = (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane;
+      const float *u0 = du_r + r0, *u1 = du_r + r1;
+      float ov = 0.0f, bv = 0.0f;
+      if (MODE == 0) {
+        const float *v0 = dv_r + r0, *v1 = dv_r + r1;
+        ov = v0[(unsigned)y];
+        bv = v1[(unsigned)y + 1];
+      }
+      B.o = f2v{u0[(unsigned)y], ov};
+      B.b = f2v{u1[(unsigned)y + 1], bv};
+    }
+  }
+
+  template <int Q>
+  __device__ __forceinline__ void step(const int t) {
+    constexpr int m0 = Q % 3, m1 = (Q + 2) % 3, m2 = (Q + 1) % 3;  // ring slots of steps t, t-1, t-2
+    Ld &B = buf<Q % NB>();
+    const Ld &Bn = buf<(Q + 1) % NB>();
+    load(t + PD, buf<(Q + PD) % NB>());  // beyond the last step too: sor_row keeps every address in the plane
+    const int d = t - 2 * s;
+    const int xp = d - y;
+    const bool hasl = xp > 0, hasr = xp < w - 1;
+    f2v o, r, bt;
+    if (FIRST) {
+      o = B.o; r = Bn.o; bt = B.b;
+    } else {
+      o = ring_p[m2]; r = ring_p[m1]; bt = ring_p[3 + m1];
+    }
+    const f2v tp = ring_s[m1 - 3];  // row y - 1 at step t-1
+    const float tsv = sv_s[m1 - 3];  // sv of row y - 1 (entry 0: zero)
+    f2v nw;
+    float vv;
+    if (MODE == 0) {
+      const float hr = B.c1.z;
+      vv = B.c1.w;
+      const f2v bb = f2v{B.c1.x, B.c1.y};
+      const f2v rr = hasr ? r : f2v{0.0f, 0.0f};
+      const f2v X = hr * rr, Y = tsv * tp, Z = vv * bt;
+      // solver.c's three border expression trees (see sor_rhs), lane-constant operand selects
+      const f2v l = X + (border ? bb : Y);
+      const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Y) : Z);
+      const f2v sr = l + rg;
+      const f2v Bv = hasl ? phr * pp + sr : sr;
+      const f2v m_1 = f2v{B.c0.x, B.c0.y} * Bv.x, m_2 = f2v{B.c0.z, B.c0.w} * Bv.y;  // (i11,i12), (i12,i22)
+      nw = o + omega * ((m_1 + m_2) - o);
+      phr = hr;
+    } else {
+      const float a11 = B.c0.x, b1 = B.c0.y, hr = B.c0.z;
+      vv = B.c0.w;
+      const bool has_top = !notop, has_bot = !(border && has_top);
+      const float tu = tp.x, ur = hasr ? r.x : 0.0f, hl = phr;
+      float su = 0.0f, sd = 0.0f;
+      su = has_top ? su - tsv * tu : su;   sd = has_top ? sd + tsv : sd;
+      su = hasl ? su - hl * pp.x : su;     sd = hasl ? sd + hl : sd;
+      su = has_bot ? su - vv * bt.x : su;  sd = has_bot ? sd + vv : sd;
+      su = hasr ? su - hr * ur : su;       sd = hasr ? sd + hr : sd;
+      const float A = a11 + sd, Bq = b1 - su;
+      nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
+      phr = hr;
+    }
+    ring_s[m0] = nw;
+    sv_s[m0] = vv;
+    if (LAST) {
+      if ((unsigned)xp < (unsigned)w && y < h) {
+        const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
+        du[r0 + (unsigned)y] = nw.x;
+        if (MODE == 0) dv[r0 + (unsigned)y] = nw.y;
+      }
+    }
+    pp = nw;
+    __syncthreads();
+  }
+
+  template <int J>
+  __device__ __forceinline__ void prologue(const int t) {
+    load(t + J, buf<J>());
+    if constexpr (J + 1 < PD) prologue<J + 1>(t);
+  }
+  template <int J>
+  __device__ __forceinline__ void block(const int t) {
+    step<J>(t + J);
+    if constexpr (J + 1 < U) block<J + 1>(t);
+  }
+
+  // Steps [0, T), T a multiple of U.  The wave's rows y0..ymax are inside the frame for diagonals
+  // d = t - 2s in [y0, ymax + w - 1]; blocks wholly outside that range only join the barriers.
+  __device__ __forceinline__ void run(int T, int y0, int ymax) {
+    pp = f2v{0.0f, 0.0f};
+    phr = 0.0f;
+    const int ta = max(0, (y0 + 2 * s) / U * U);
+    const int tb = min(T, (ymax + w - 1 + 2 * s) / U * U + U);
+    for (int t = 0; t < ta; ++t) __syncthreads();
+    prologue<0>(ta);
+    for (int t = ta; t < tb; t += U) block<0>(t);
+    for (int t = tb; t < T; ++t) __syncthreads();
+  }
+};
+
+// LDS of the lean SOR: S (u, v) rings of NR = 64 G + 2 entries x 3 slots of float2, then S sv rings.
+__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h) {
+  return sizeof(float) * 3 * 3 * (size_t)S * (((h + 63) / 64) * 64 + 2);
+}
+
+// One frame's SOR call, lean form (R = 1): 64 * G * S threads.
+template <int S, int MODE, int NB>
+__device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
+  const int G = (a.h + 63) / 64;
+  const int NR = G * 64 + 2;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int g = wid / S, s = wid - g * S;
+  float *svr = reinterpret_cast<float *>(ring + S * 3 * NR);
+  for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) {
+    ring[i] = f2v{0.f, 0.f};
+    svr[i] = 0.0f;
+  }
+  __syncthreads();
+  const long fo = (long)frame * a.sp;
+  constexpr int U = SorLane<S, MODE, true, false, NB>::U;
+  const int T = ((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1 + U - 1) / U * U;
+  const int y0 = g * 64, ymax = min(y0 + 63, a.h - 1);
+  auto setup = [&](auto &st) {
+    st.C = reinterpret_cast<const float4 *>(a.coef) + fo * (MODE == 0 ? 2 : 1);
+    st.du_r = a.du + fo;
+    st.dv_r = a.dv + fo;
+    st.du = a.du + fo;
+    st.dv = a.dv + fo;
+    const int y = y0 + lane;
+    st.ring_s = ring + (s * NR + y + 1) * 3;
+    st.ring_p = ring + ((s > 0 ? s - 1 : 0) * NR + y + 1) * 3;
+    st.sv_s = svr + (s * NR + y + 1) * 3;
+    st.w = a.w; st.h = a.h; st.y = y; st.s = s;
+    st.lim = a.wrap ? a.w : 1 << 30;
+    st.rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
+    st.hplane = a.h;
+    st.notop = y == 0;
+    st.border = y == 0 || y >= a.h - 1;
+    st.omega = a.omega;
+    st.run(T, y0, ymax);
+  };
+  if (s == 0) {
+    SorLane<S, MODE, true, S == 1, NB> st;
+    setup(st);
+  } else if (s == S - 1) {
+    SorLane<S, MODE, false, true, NB> st;
+    setup(st);
+  } else {
+    SorLane<S, MODE, false, false, NB> st;
+    setup(st);
+  }
+}
+
 // Rows per lane of the sweep-per-wave SOR.  One row per lane and more waves measured faster than 2 or 4
 // rows per lane and fewer waves (1080p op2: 0.76 vs 0.91 ms per step), so 1 is the default; `forced`
 // (option "sor_rows") selects 2 or 4 for A/B runs.
@@ -1981,6 +2196,12 @@ template <int S, int MODE, int R, int MAXT>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_waves(TvArgs a) {
   extern __shared__ float4 ring[];  // [S][3][NR]
   sor_waves_frame<S, MODE, R>(a, blockIdx.x, ring);
+}
+
+template <int S, int MODE, int NB, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
+  extern __shared__ f2v ring_uv[];  // [S][NR][3]
+  sor_lanes_frame<S, MODE, NB>(a, blockIdx.x, ring_uv);
 }
 
 __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
@@ -2349,6 +2570,20 @@ template <int S, int R, int MAXT>
 static void sor_waves_r(const TvArgs &a, hipStream_t s) {
   const int G = (a.h + 64 * R - 1) / (64 * R);
   const size_t lds = sizeof(float4) * S * 3 * (G * 64 * R + 2);
+  if (R == 1 && a.sor_lean) {
+    const int pd = a.sor_lean;  // prefetch distance: 2, 3 or 5 steps (3, 4 or 6 buffers)
+    const size_t lds = sor_lanes_lds(S, a.h);
+    if (a.nop == 2) {
+      if (pd == 5) k_tv_sor_lanes<S, 0, 6, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+      else if (pd == 3) k_tv_sor_lanes<S, 0, 4, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+      else k_tv_sor_lanes<S, 0, 3, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+    } else {
+      if (pd == 5) k_tv_sor_lanes<S, 2, 6, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+      else if (pd == 3) k_tv_sor_lanes<S, 2, 4, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+      else k_tv_sor_lanes<S, 2, 3, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+    }
+    return;
+  }
   if (a.nop == 2)
     k_tv_sor_waves<S, 0, R, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
   else

@@ -81,6 +81,8 @@ struct ofdis_context {
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
+  int opt_sor_lean = 2;        // sweep-per-wave SOR, one row per lane: lean SorLane form with this prefetch
+                               // distance (2, 3, 5 steps); 0: SorWave (A/B)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
@@ -444,6 +446,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_rows = c->opt_sor_rows;
+      tv.sor_lean = c->opt_sor_lean;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       if (c->opt_tv_fused && tv_level_fusable(tv)) {
         timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
@@ -992,6 +995,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   }
   if (std::strcmp(key, "sor_rows") == 0 && (value == 0 || value == 1 || value == 2 || value == 4)) {
     c->opt_sor_rows = value;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "sor_lean") == 0 && (value == 0 || value == 2 || value == 3 || value == 5)) {
+    c->opt_sor_lean = value;
     return OFDIS_OK;
   }
   if (std::strcmp(key, "wave_per_patch") == 0) {
