@@ -102,6 +102,7 @@ struct TvArgs {
   int sor_rows;                // sweep-per-wave SOR rows per lane: 0 auto, 1/2/4/8 forced (A/B testing)
   int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
   int sor_lean;                // sweep-per-wave SOR, one row per lane: lean form (SorLane) vs SorWave (A/B)
+  int sys_fused;               // system + SOR in one launch (k_tv_sys_sor) where it applies
 };
 
 struct UpArgs {
@@ -133,6 +134,8 @@ void launch_tv_deriv2(const TvArgs &a, hipStream_t s);
 void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
+bool tv_sys_sor_fusable(const TvArgs &a);
+void launch_tv_sys_sor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
 // Whole refinement level in one launch per frame (k_tv_level); only when tv_level_fusable(a).
 bool tv_level_fusable(const TvArgs &a);

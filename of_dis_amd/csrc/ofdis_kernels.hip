@@ -1318,36 +1318,23 @@ __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, b
 // All of a pixel's inputs are gathered first with unconditional loads (border neighbours clamped to the
 // pixel itself and discarded by selects afterwards): one memory round trip per pixel instead of one per
 // data-dependent branch.  Same arithmetic, same order as before.
+// The system of one pixel from its gathered inputs (s, wx, wy of the pixel and its 4-neighbourhood in the
+// order centre, left, right, up, down; mask; du, dv; the derivative images).  Neighbours that do not exist
+// (hasl ... hasd false) may hold any value: every use of them is behind a select.  OF: c0 = (a11, a12,
+// a12, a22) (the inverse sor_coupled's first sweep computes, see below), c1 = (b1, b2, sh, sv); DE: c0 =
+// (a11, b1, sh, sv).
 template <int NOP, int NOC>
-__device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
-  const long idx = fr * a.sp + kk;
-  int x, y;
-  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
+__device__ __forceinline__ void sys_compute(const TvArgs &a, int x, int y, const float (&S5)[5], const float (&X5)[5],
+                                            const float (&Y5)[5], float m, float u, float v, const float (&lIx)[NOC],
+                                            const float (&lIy)[NOC], const float (&lIz)[NOC], const float (&lIxx)[NOC],
+                                            const float (&lIxy)[NOC], const float (&lIyy)[NOC],
+                                            const float (&lIxz)[NOC], const float (&lIyz)[NOC], float4 &c0,
+                                            float4 &c1) {
   const int w = a.w, h = a.h;
   const bool hasl = x >= 1, hasr = x <= w - 2, hasu = y >= 1, hasd = y <= h - 2;
-  const unsigned f0 = (unsigned)(fr * a.sp), ui = (unsigned)idx;
-  const unsigned il = hasl ? f0 + (unsigned)skw(x - 1, y, h, w, a.wrap) : ui;
-  const unsigned ir = hasr ? f0 + (unsigned)skw(x + 1, y, h, w, a.wrap) : ui;
-  const unsigned iu = hasu ? f0 + (unsigned)skw(x, y - 1, h, w, a.wrap) : ui;
-  const unsigned id = hasd ? f0 + (unsigned)skw(x, y + 1, h, w, a.wrap) : ui;
-  // ---- gather
-  const float *S = a.s, *WX = a.wxs, *WY = a.wys;
-  const float sc = ldu(S, ui), sl = ldu(S, il), sr = ldu(S, ir), su = ldu(S, iu), sd = ldu(S, id);
-  const float xc = ldu(WX, ui), xl = ldu(WX, il), xr = ldu(WX, ir), xu = ldu(WX, iu), xd = ldu(WX, id);
-  float yc = 0.0f, yl = 0.0f, yr = 0.0f, yu = 0.0f, yd = 0.0f;
-  if (NOP == 2) {
-    yc = ldu(WY, ui); yl = ldu(WY, il); yr = ldu(WY, ir); yu = ldu(WY, iu); yd = ldu(WY, id);
-  }
-  const float m = ldu(a.mask, ui), u = ldu(a.du, ui), v = NOP == 2 ? ldu(a.dv, ui) : 0.0f;
-  const unsigned q = (unsigned)(fr * NOC * a.sp + kk);
-  float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
-#pragma unroll
-  for (int c = 0; c < NOC; ++c) {
-    const unsigned o = q + (unsigned)(c * a.sp);
-    lIx[c] = ldu(a.Ix, o); lIy[c] = ldu(a.Iy, o); lIz[c] = ldu(a.Iz, o); lIxx[c] = ldu(a.Ixx, o);
-    lIxy[c] = ldu(a.Ixy, o); lIyy[c] = ldu(a.Iyy, o); lIxz[c] = ldu(a.Ixz, o); lIyz[c] = ldu(a.Iyz, o);
-  }
-  // ---- compute
+  const float sc = S5[0], sl = S5[1], sr = S5[2], su = S5[3], sd = S5[4];
+  const float xc = X5[0], xl = X5[1], xr = X5[2], xu = X5[3], xd = X5[4];
+  const float yc = Y5[0], yl = Y5[1], yr = Y5[2], yu = Y5[3], yd = Y5[4];
   const float shv = x < w - 1 ? sc + sr : 0.0f;  // h[x] = s[x] + s[x+1]
   const float svv = y < h - 1 ? sc + sd : 0.0f;  // v[y] = s[y] + s[y+1]
   float A11, A12 = 0.0f, A22 = 0.0f, B1, B2 = 0.0f;
@@ -1379,11 +1366,58 @@ __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
       A22 = M22 / det;
       A12 = A12 / (0.0f - det);
     }
-    float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
-    C[0] = make_float4(A11, A12, A12, A22);  // (a11, a12) and (a12, a22) pair up for packed fp32
-    C[1] = make_float4(B1, B2, shv, svv);
+    c0 = make_float4(A11, A12, A12, A22);  // (a11, a12) and (a12, a22) pair up for packed fp32
+    c1 = make_float4(B1, B2, shv, svv);
   } else {
-    reinterpret_cast<float4 *>(a.coef)[idx] = make_float4(A11, B1, shv, svv);
+    c0 = make_float4(A11, B1, shv, svv);
+    c1 = c0;
+  }
+}
+
+// One TV inner iteration's system (refine_variational.cpp:195-199): diffusivities from s
+// (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
+// All of a pixel's inputs are gathered first with unconditional loads (border neighbours clamped to the
+// pixel itself and discarded by selects afterwards): one memory round trip per pixel instead of one per
+// data-dependent branch.
+template <int NOP, int NOC>
+__device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
+  const long idx = fr * a.sp + kk;
+  int x, y;
+  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
+  const int w = a.w, h = a.h;
+  const bool hasl = x >= 1, hasr = x <= w - 2, hasu = y >= 1, hasd = y <= h - 2;
+  const unsigned f0 = (unsigned)(fr * a.sp), ui = (unsigned)idx;
+  const unsigned il = hasl ? f0 + (unsigned)skw(x - 1, y, h, w, a.wrap) : ui;
+  const unsigned ir = hasr ? f0 + (unsigned)skw(x + 1, y, h, w, a.wrap) : ui;
+  const unsigned iu = hasu ? f0 + (unsigned)skw(x, y - 1, h, w, a.wrap) : ui;
+  const unsigned id = hasd ? f0 + (unsigned)skw(x, y + 1, h, w, a.wrap) : ui;
+  // ---- gather
+  const unsigned i5[5] = {ui, il, ir, iu, id};
+  float S5[5], X5[5], Y5[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    S5[k] = ldu(a.s, i5[k]);
+    X5[k] = ldu(a.wxs, i5[k]);
+    Y5[k] = NOP == 2 ? ldu(a.wys, i5[k]) : 0.0f;
+  }
+  const float m = ldu(a.mask, ui), u = ldu(a.du, ui), v = NOP == 2 ? ldu(a.dv, ui) : 0.0f;
+  const unsigned q = (unsigned)(fr * NOC * a.sp + kk);
+  float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
+#pragma unroll
+  for (int c = 0; c < NOC; ++c) {
+    const unsigned o = q + (unsigned)(c * a.sp);
+    lIx[c] = ldu(a.Ix, o); lIy[c] = ldu(a.Iy, o); lIz[c] = ldu(a.Iz, o); lIxx[c] = ldu(a.Ixx, o);
+    lIxy[c] = ldu(a.Ixy, o); lIyy[c] = ldu(a.Iyy, o); lIxz[c] = ldu(a.Ixz, o); lIyz[c] = ldu(a.Iyz, o);
+  }
+  // ---- compute
+  float4 c0, c1;
+  sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, u, v, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz, lIyz, c0, c1);
+  if (NOP == 2) {
+    float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
+    C[0] = c0;
+    C[1] = c1;
+  } else {
+    reinterpret_cast<float4 *>(a.coef)[idx] = c0;
   }
 }
 
@@ -2146,6 +2180,284 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
   }
 }
 
+// ---------------------------------------------------------------------------------- fused system + SOR
+// One TV inner iteration's system AND its exact-order SOR in one launch, one workgroup per frame
+// (refine_variational.cpp:195-208): per row group g, one producer wave computes the system of diagonal t
+// at step t (sys_compute: the same function k_tv_system uses, hence the same bits) into an LDS ring of
+// coefficients, and S sweep waves run the SorLane schedule one step behind it (sweep s on diagonal
+// t - 1 - 2 s), reading their coefficients from that ring.  The coefficients never leave the CU: the 64
+// B/pixel of coefficient writes and re-reads of the two-kernel form, and one launch per iteration, are
+// gone.  Ring depth 6 covers a diagonal's life from its producer step to the last sweep's read (S <= 3);
+// G <= 2 row groups (h <= 128) keep every LDS offset a compile-time constant.
+
+// Producer: gathers one pixel's system inputs two steps ahead (3 buffers) with wave-uniform row bases.
+template <int MODE>
+struct SysProducer {
+  static constexpr int NOP = MODE == 0 ? 2 : 1;
+  struct In {
+    float s5[5], x5[5], y5[5];
+    float m, u, v;
+    float d[8];  // Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz
+  };
+  In P0, P1, P2;
+  template <int I>
+  __device__ __forceinline__ In &buf() {
+    if constexpr (I == 0) return P0;
+    else if constexpr (I == 1) return P1;
+    else return P2;
+  }
+  const float *S, *WX, *WY, *M, *DU, *DV, *D[8];
+  int y, yu, h, lim, rmax;
+
+  __device__ __forceinline__ void load(int e, In &B) {
+    const unsigned rc = (unsigned)sor_row2(e, lim, rmax) * (unsigned)h;
+    const unsigned rl = (unsigned)sor_row2(e - 1, lim, rmax) * (unsigned)h;
+    const unsigned rr = (unsigned)sor_row2(e + 1, lim, rmax) * (unsigned)h;
+    const unsigned i5[5] = {rc + (unsigned)y, rl + (unsigned)y, rr + (unsigned)y, rl + (unsigned)yu,
+                            rr + (unsigned)y + 1};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      B.s5[k] = S[i5[k]];
+      B.x5[k] = WX[i5[k]];
+      B.y5[k] = NOP == 2 ? WY[i5[k]] : 0.0f;
+    }
+    B.m = M[i5[0]];
+    B.u = DU[i5[0]];
+    B.v = NOP == 2 ? DV[i5[0]] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) B.d[k] = D[k][i5[0]];
+  }
+  __device__ __forceinline__ void compute(const TvArgs &a, int e, const In &B, float4 &c0, float4 &c1) {
+    const float lIx[1] = {B.d[0]}, lIy[1] = {B.d[1]}, lIz[1] = {B.d[2]}, lIxx[1] = {B.d[3]};
+    const float lIxy[1] = {B.d[4]}, lIyy[1] = {B.d[5]}, lIxz[1] = {B.d[6]}, lIyz[1] = {B.d[7]};
+    sys_compute<NOP, 1>(a, e - y, y, B.s5, B.x5, B.y5, B.m, B.u, B.v, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz,
+                        lIyz, c0, c1);
+  }
+};
+
+template <int S, int MODE, int G>
+struct SysSor {
+  static constexpr int NR = 64 * G + 2;  // ring entries: row y at y + 1, rows -1 and 64 G are halos
+  static constexpr int U = 6;
+  struct Ring {
+    float4 c[6][2][NR];  // coefficients of diagonal d in slot d mod 6: c0, c1
+    f2v uv[S][NR][3];    // sweep results (u, v), slot = step mod 3
+    float sv[NR][3];     // sweep 2's own sv, slot = step mod 3: the coefficient slot of the diagonal above
+                         // (d - 1) is refilled by the producer in the very step sweep 2 would read it
+  };
+};
+
+template <int S, int MODE, int G, int SI>
+struct SysSorLane {
+  static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
+  static constexpr int NR = SysSor<S, MODE, G>::NR;
+  using Ring = typename SysSor<S, MODE, G>::Ring;
+  struct Ld {
+    f2v o, b;  // sweep 0: old (u, v) of the pixel and of the one below (the right one: next step's o)
+  };
+  Ld L0, L1, L2;
+  template <int I>
+  __device__ __forceinline__ Ld &buf() {
+    if constexpr (I == 0) return L0;
+    else if constexpr (I == 1) return L1;
+    else return L2;
+  }
+  f2v pp;
+  float phr;
+  const float *du_r, *dv_r;
+  float *du, *dv;
+  Ring *R;
+  int e;  // ring entry of this lane's row
+  int w, h, y, lim, rmax;
+  bool border, notop;
+  float omega;
+
+  __device__ __forceinline__ void load(int t, Ld &B) {
+    if (!FIRST) return;
+    const int d = t - 1;
+    const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)h;
+    const unsigned r1 = (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)h;
+    float ov = 0.0f, bv = 0.0f;
+    if (MODE == 0) {
+      ov = dv_r[r0 + (unsigned)y];
+      bv = dv_r[r1 + (unsigned)y + 1];
+    }
+    B.o = f2v{du_r[r0 + (unsigned)y], ov};
+    B.b = f2v{du_r[r1 + (unsigned)y + 1], bv};
+  }
+
+  template <int J>
+  __device__ __forceinline__ void step(const int t) {
+    constexpr int m0 = J % 3, m1 = (J + 2) % 3, m2 = (J + 1) % 3;  // (u, v) ring slots of steps t, t-1, t-2
+    constexpr int cs = ((J - 1 - 2 * SI) % 6 + 6) % 6;            // coefficient slot of this diagonal
+    constexpr int ct = (cs + 5) % 6;                               // ... of the diagonal before
+    Ld &B = buf<J % 3>();
+    const Ld &Bn = buf<(J + 1) % 3>();
+    load(t + 2, buf<(J + 2) % 3>());
+    const int d = t - 1 - 2 * SI;
+    const int xp = d - y;
+    const bool hasl = xp > 0, hasr = xp < w - 1;
+    const float4 c0 = R->c[cs][0][e], c1 = R->c[cs][1][e];
+    f2v o, r, bt;
+    if (FIRST) {
+      o = B.o; r = Bn.o; bt = B.b;
+    } else {
+      o = R->uv[SI - 1][e][m2]; r = R->uv[SI - 1][e][m1]; bt = R->uv[SI - 1][e + 1][m1];
+    }
+    const f2v tp = R->uv[SI][e - 1][m1];  // row y - 1 at step t-1 (entry 0: zero)
+    f2v nw;
+    float vv;
+    if (MODE == 0) {
+      const float tsv = SI >= 2 ? R->sv[e - 1][m1] : R->c[ct][1][e - 1].w;  // sv of (x, y - 1)
+      const float hr = c1.z;
+      vv = c1.w;
+      const f2v bb = f2v{c1.x, c1.y};
+      const f2v rr = hasr ? r : f2v{0.0f, 0.0f};
+      const f2v X = hr * rr, Y = tsv * tp, Z = vv * bt;
+      const f2v l = X + (border ? bb : Y);
+      const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Y) : Z);
+      const f2v sr = l + rg;
+      const f2v Bv = hasl ? phr * pp + sr : sr;
+      const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;
+      nw = o + omega * ((m_1 + m_2) - o);
+      phr = hr;
+    } else {
+      const float tsv = SI >= 2 ? R->sv[e - 1][m1] : R->c[ct][0][e - 1].w;
+      const float a11 = c0.x, b1 = c0.y, hr = c0.z;
+      vv = c0.w;
+      const bool has_top = !notop, has_bot = !(border && has_top);
+      const float tu = tp.x, ur = hasr ? r.x : 0.0f, hl = phr;
+      float su = 0.0f, sd = 0.0f;
+      su = has_top ? su - tsv * tu : su;   sd = has_top ? sd + tsv : sd;
+      su = hasl ? su - hl * pp.x : su;     sd = hasl ? sd + hl : sd;
+      su = has_bot ? su - vv * bt.x : su;  sd = has_bot ? sd + vv : sd;
+      su = hasr ? su - hr * ur : su;       sd = hasr ? sd + hr : sd;
+      const float A = a11 + sd, Bq = b1 - su;
+      nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
+      phr = hr;
+    }
+    R->uv[SI][e][m0] = nw;
+    if (SI >= 2) R->sv[e][m0] = vv;
+    if (LAST) {
+      if ((unsigned)xp < (unsigned)w && y < h) {
+        const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)h;
+        du[r0 + (unsigned)y] = nw.x;
+        if (MODE == 0) dv[r0 + (unsigned)y] = nw.y;
+      }
+    }
+    pp = nw;
+    __syncthreads();
+  }
+  template <int J>
+  __device__ __forceinline__ void block(const int t) {
+    step<J>(t + J);
+    if constexpr (J + 1 < 6) block<J + 1>(t);
+  }
+  // active diagonals [y0, ymax + w - 1] -> steps [y0 + 1 + 2 SI, ymax + w + 2 SI]
+  __device__ __forceinline__ void run(int T, int y0, int ymax) {
+    pp = f2v{0.0f, 0.0f};
+    phr = 0.0f;
+    const int ta = (y0 + 1 + 2 * SI) / 6 * 6;
+    const int tb = min(T, (ymax + w + 2 * SI) / 6 * 6 + 6);
+    for (int t = 0; t < ta; ++t) __syncthreads();
+    load(ta, L0);
+    load(ta + 1, L1);
+    for (int t = ta; t < tb; t += 6) block<0>(t);
+    for (int t = tb; t < T; ++t) __syncthreads();
+  }
+};
+
+template <int S, int MODE, int G>
+struct SysProdLane {
+  using Ring = typename SysSor<S, MODE, G>::Ring;
+  SysProducer<MODE> P;
+  Ring *R;
+  int e;
+  template <int J>
+  __device__ __forceinline__ void step(const TvArgs &a, const int t) {
+    auto &B = P.template buf<J % 3>();
+    float4 c0, c1;
+    P.compute(a, t, B, c0, c1);
+    P.load(t + 2, P.template buf<(J + 2) % 3>());
+    R->c[J][0][e] = c0;
+    R->c[J][1][e] = c1;
+    __syncthreads();
+  }
+  template <int J>
+  __device__ __forceinline__ void block(const TvArgs &a, const int t) {
+    step<J>(a, t + J);
+    if constexpr (J + 1 < 6) block<J + 1>(a, t);
+  }
+  // active diagonals [y0, ymax + w - 1] (diagonal t at step t)
+  __device__ __forceinline__ void run(const TvArgs &a, int T, int y0, int ymax) {
+    const int ta = y0 / 6 * 6;
+    const int tb = min(T, (ymax + a.w - 1) / 6 * 6 + 6);
+    for (int t = 0; t < ta; ++t) __syncthreads();
+    P.load(ta, P.P0);
+    P.load(ta + 1, P.P1);
+    for (int t = ta; t < tb; t += 6) block<0>(a, t);
+    for (int t = tb; t < T; ++t) __syncthreads();
+  }
+};
+
+template <int S, int MODE, int G>
+__global__ __launch_bounds__(64 * G * (S + 1)) void k_tv_sys_sor(TvArgs a) {
+  using Ring = typename SysSor<S, MODE, G>::Ring;
+  __shared__ Ring ring;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int g = wid / (S + 1), role = wid - g * (S + 1);
+  {
+    float *z = reinterpret_cast<float *>(&ring);
+    for (int i = threadIdx.x; i < (int)(sizeof(Ring) / 4); i += blockDim.x) z[i] = 0.0f;
+  }
+  __syncthreads();
+  const int frame = blockIdx.x;
+  const long fo = (long)frame * a.sp;
+  const int T = ((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 2 + 5) / 6 * 6;  // + 1: sweeps run a step behind
+  const int y0 = g * 64, ymax = min(y0 + 63, a.h - 1);
+  const int y = y0 + lane;
+  const int lim = a.wrap ? a.w : 1 << 30, rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
+  if (role == S) {
+    SysProdLane<S, MODE, G> pr;
+    pr.R = &ring;
+    pr.e = y + 1;
+    SysProducer<MODE> &P = pr.P;
+    P.S = a.s + fo; P.WX = a.wxs + fo; P.WY = a.wys + fo; P.M = a.mask + fo; P.DU = a.du + fo; P.DV = a.dv + fo;
+    P.D[0] = a.Ix + fo; P.D[1] = a.Iy + fo; P.D[2] = a.Iz + fo; P.D[3] = a.Ixx + fo;
+    P.D[4] = a.Ixy + fo; P.D[5] = a.Iyy + fo; P.D[6] = a.Ixz + fo; P.D[7] = a.Iyz + fo;
+    P.y = y; P.yu = y > 0 ? y - 1 : 0; P.h = a.h; P.lim = lim; P.rmax = rmax;
+    pr.run(a, T, y0, ymax);
+    return;
+  }
+  auto sweep = [&](auto &st) {
+    st.du_r = a.du + fo; st.dv_r = a.dv + fo; st.du = a.du + fo; st.dv = a.dv + fo;
+    st.R = &ring; st.e = y + 1;
+    st.w = a.w; st.h = a.h; st.y = y; st.lim = lim; st.rmax = rmax;
+    st.notop = y == 0;
+    st.border = y == 0 || y >= a.h - 1;
+    st.omega = a.omega;
+    st.run(T, y0, ymax);
+  };
+  if (role == 0) {
+    SysSorLane<S, MODE, G, 0> st;
+    sweep(st);
+  } else if (role == 1) {
+    SysSorLane<S, MODE, G, (S > 1 ? 1 : 0)> st;
+    sweep(st);
+  } else {
+    SysSorLane<S, MODE, G, (S > 2 ? 2 : 0)> st;
+    sweep(st);
+  }
+}
+
+template <int S, int MODE>
+static void sys_sor_s(const TvArgs &a, hipStream_t s) {
+  if (a.h <= 64)
+    k_tv_sys_sor<S, MODE, 1><<<a.n, 64 * (S + 1), 0, s>>>(a);
+  else
+    k_tv_sys_sor<S, MODE, 2><<<a.n, 128 * (S + 1), 0, s>>>(a);
+}
+
 // Rows per lane of the sweep-per-wave SOR.  One row per lane and more waves measured faster than 2 or 4
 // rows per lane and fewer waves (1080p op2: 0.76 vs 0.91 ms per step), so 1 is the default; `forced`
 // (option "sor_rows") selects 2 or 4 for A/B runs.
@@ -2629,6 +2941,19 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
     k_tv_sor<1><<<a.n, 256, 0, s>>>(a);
   else
     k_tv_sor<0><<<a.n, 256, 0, s>>>(a);
+}
+bool tv_sys_sor_fusable(const TvArgs &a) {
+  return a.sys_fused && a.noc == 1 && (a.solverit == 2 || a.solverit == 3) && a.w >= 2 && a.h >= 2 &&
+         a.h <= 128 && !a.sor_point && !a.sor_generic && a.sor_variant == 0;
+}
+void launch_tv_sys_sor(const TvArgs &a, hipStream_t s) {
+  if (a.nop == 2) {
+    if (a.solverit == 2) sys_sor_s<2, 0>(a, s);
+    else sys_sor_s<3, 0>(a, s);
+  } else {
+    if (a.solverit == 2) sys_sor_s<2, 2>(a, s);
+    else sys_sor_s<3, 2>(a, s);
+  }
 }
 template <int S, int MODE>
 static void tv_level_s(const TvArgs &a, int n_inner, hipStream_t s) {

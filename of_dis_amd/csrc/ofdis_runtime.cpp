@@ -26,7 +26,8 @@ using namespace ofdis;
 namespace {
 
 const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_level"};
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_level",
+                                    "tv_sys_sor"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -81,6 +82,8 @@ struct ofdis_context {
   int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
+  int opt_sys_fused = 0;       // 1: system + SOR in one launch where it applies (k_tv_sys_sor; A/B: the
+                               // producer wave's per-step system latency lengthens the wavefront step ~3x)
   int opt_sor_lean = 2;        // sweep-per-wave SOR, one row per lane: lean SorLane form with this prefetch
                                // distance (2, 3, 5 steps); 0: SorWave (A/B)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
@@ -447,6 +450,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_rows = c->opt_sor_rows;
       tv.sor_lean = c->opt_sor_lean;
+      tv.sys_fused = c->opt_sys_fused;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       if (c->opt_tv_fused && tv_level_fusable(tv)) {
         timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
@@ -458,11 +462,16 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
         });
         for (int it = 0; it < n_inner; ++it) {
           tv.first_iter = it == 0;
-          timed(c, 7, s, [&] {
-            launch_tv_smooth(tv, s);
-            launch_tv_system(tv, s);
-          });
-          timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
+          if (tv_sys_sor_fusable(tv)) {
+            timed(c, 7, s, [&] { launch_tv_smooth(tv, s); });
+            timed(c, 12, s, [&] { launch_tv_sys_sor(tv, s); });
+          } else {
+            timed(c, 7, s, [&] {
+              launch_tv_smooth(tv, s);
+              launch_tv_system(tv, s);
+            });
+            timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
+          }
         }
         timed(c, 9, s, [&] { launch_tv_final(tv, s); });
       }
@@ -1001,6 +1010,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     c->opt_sor_lean = value;
     return OFDIS_OK;
   }
+  if (std::strcmp(key, "sys_fused") == 0) {
+    c->opt_sys_fused = value != 0;
+    return OFDIS_OK;
+  }
   if (std::strcmp(key, "wave_per_patch") == 0) {
     c->opt_wave_per_patch = value != 0;
     return OFDIS_OK;
@@ -1087,6 +1100,10 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
       b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
       b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
     }
+    // the fused system + SOR launch: the system's inputs and the SOR's du / dv traffic (coefficients stay
+    // in LDS); the smoothness weights are tv_system's
+    if (k == "tv_sys_sor")
+      b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * 2 * nop);
     if (p->usetvref) {
       if (k == "tv_prep") b += px * 4.0 * (4 * noc + 1 + 3 * nop);
       if (k == "tv_deriv") b += px * 4.0 * noc * (2 + 4 + 2 + 3);

@@ -58,6 +58,8 @@ CASES = [
     (400, 300, 1, 1, 2, {"sc_l": 0, "sc_f": 2}),              # 300 rows: 5 row groups x 3 sweep waves
     (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows: register pipeline, 1024 threads
     (160, 120, 1, 1, 2, {"omp_build": 1}),                    # USE_OPENMP build: point SOR (solver.c:34-78)
+    (240, 200, 1, 1, 2, {"sc_l": 1, "sc_f": 2, "tv_solverit": 2}),  # fused system + SOR: 2 sweeps, 2 row groups
+    (248, 232, 1, 2, 2, {"sc_l": 1, "sc_f": 2}),              # ... depth, 116 rows (2 row groups)
     (192, 128, 3, 1, 3, {"omp_build": 1, "usefbcon": 1}),     # ... RGB, forward-backward
     (173, 97, 1, 1, 2, {"gradmag": 1}),                       # SELECTCHANNEL 2: gradient-magnitude pyramid
     (240, 120, 1, 2, 4, {"gradmag": 1, "max_iter": 16, "min_iter": 16}),  # ... depth
@@ -100,6 +102,9 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("wave_per_patch", 1, 0),  # one wave per DIS patch instead of eight lanes
     ("sor_rows", 1, 0),        # sweep-per-wave SOR with one row per lane
     ("sor_rows", 4, 0),        # ... four rows per lane
+    ("sys_fused", 1, 0),       # system and SOR in one launch (producer wave + LDS coefficient ring)
+    ("sor_lean", 0, 2),        # ... with the SorWave sweep-per-wave SOR
+    ("sor_lean", 5, 2),        # ... with the lean SOR, prefetch distance 5
 ]
 
 

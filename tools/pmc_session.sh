@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${1:-pmc}
-B=${BENCH_BATCH:-512}
+B=${BENCH_BATCH:-1024}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
