@@ -45,8 +45,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frame pairs per GPU per step (0 = the config's)")
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--streams", type=int, default=1, help="HIP streams the batch's chunks round-robin over")
-    ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = whole batch in one chunk)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="HIP streams the batch's chunks round-robin over (0 = the library's auto: 2 from 512 pairs)")
+    ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = the batch split over the streams)")
     ap.add_argument("--tv-fused", type=int, default=-1, help="1/0: force the fused TV level kernel on/off")
     ap.add_argument("--option", action="append", default=[], help="context option key=value (A/B runs)")
     ap.add_argument("--host-io", action="store_true",
@@ -60,10 +61,11 @@ def config_tag(cfg, B):
     return f"{cfg[1]}x{cfg[2]}:op{cfg[5]}:b{B}" + ("" if cfg[3] == 1 else ":rgb")
 
 
-def kernel_roofline(od, p, W, H, B, cfg, steps, kernels, name):
+def kernel_roofline(od, p, W, H, B, per_launch, cfg, steps, kernels, name):
     """HBM roofline of one kernel: algorithmic bytes per launch (SURVEY §8(d) byte model x the frames one
     launch processes) / its average launch time (HIP events on the launch stream); traffic = HBM bytes per
-    launch from the rocprofv3 PMC passes (profiles/traffic.json, tools/pmc_traffic.py) when recorded."""
+    launch from the rocprofv3 PMC passes (profiles/traffic.json, tools/pmc_traffic.py, keyed by the pairs
+    per launch) when recorded."""
     k = kernels[name]
     bytes_frame = od.algorithmic_bytes(p, W, H, name)
     launches_per_step = k["launches"] / steps
@@ -73,7 +75,7 @@ def kernel_roofline(od, p, W, H, B, cfg, steps, kernels, name):
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
         try:
-            ent = json.load(open(tf)).get(f"{name}:{config_tag(cfg, B)}")
+            ent = json.load(open(tf)).get(f"{name}:{config_tag(cfg, per_launch)}")
             traffic = None if ent is None else round(ent["bytes_per_launch"])
         except Exception:
             traffic = None
@@ -118,6 +120,9 @@ def main():
     ctx = od.Context(dev.index)
     ctx.set_option("streams", args.streams)
     ctx.set_option("chunk", args.chunk)
+    # the library's chunking (ofdis_runtime.cpp stream_count): streams 0 = 2 from 512 pairs, else 1
+    streams_eff = args.streams or (2 if B >= 512 else 1)
+    chunk_eff = min(B, args.chunk or -(-B // streams_eff))
     if args.tv_fused >= 0:
         ctx.set_option("tv_fused", args.tv_fused)
     for kv in args.option:
@@ -165,7 +170,9 @@ def main():
     roofline = None
     roofline_sor = None
     if not args.no_kernel_timing:
+        # the same launches (chunk_eff pairs each), serialised on one stream: each kernel timed alone
         ctx.set_option("streams", 1)
+        ctx.set_option("chunk", chunk_eff)
         ctx.enable_kernel_timing(True)
         for _ in range(args.steps):
             step()
@@ -176,10 +183,11 @@ def main():
                 kernels[k] = {"total_ms": ms, "launches": cnt, "avg_us": ms / cnt * 1e3}
         ctx.enable_kernel_timing(False)
         ctx.set_option("streams", args.streams)
+        ctx.set_option("chunk", args.chunk)
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-        roofline = kernel_roofline(od, p, W, H, B, cfg, args.steps, kernels, dom)
+        roofline = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, dom)
         if dom != "tv_sor" and "tv_sor" in kernels:  # the north-star kernel, reported beside the dominant one
-            roofline_sor = kernel_roofline(od, p, W, H, B, cfg, args.steps, kernels, "tv_sor")
+            roofline_sor = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, "tv_sor")
 
     # ---- host-buffer entry point (PCIe-inclusive; never the headline value)
     host_io = None
@@ -235,7 +243,7 @@ def main():
             "config": {"workload": f"{binary} {W}x{H} op-point {op}" + (f" ({explicit})" if explicit else "")
                                    + f", {B} pairs/GPU/step", "name": args.config,
                        "width": W, "height": H, "channels": noc, "oppoint": op, "batch_per_gpu": B,
-                       "streams": args.streams, "chunk": args.chunk, "tv_fused": args.tv_fused,
+                       "streams": streams_eff, "pairs_per_launch": chunk_eff, "tv_fused": args.tv_fused,
                        "options": args.option,
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,

@@ -103,6 +103,7 @@ struct TvArgs {
   int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
   int sor_lean;                // sweep-per-wave SOR, one row per lane: lean form (SorLane) vs SorWave (A/B)
   int sys_fused;               // system + SOR in one launch (k_tv_sys_sor) where it applies
+  int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3)
 };
 
 struct UpArgs {

@@ -1990,8 +1990,14 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 //    vector memory path, the LDS much less);
 //  * (u, v) pairs run on packed fp32 (v_pk_mul_f32 / v_pk_add_f32: the same roundings as scalar, no FMA);
 //  * a wave whose rows are all outside the frame for a whole block only joins the block's barriers.
-template <int S, int MODE, bool FIRST, bool LAST, int NB>
+// SI: sweep index.  CRN > 0: coefficient ring of CRN entries per slot -- sweep 0 loads each pixel's
+// coefficients once and passes them to the later sweeps through LDS (slot = diagonal mod 6: a diagonal
+// lives from sweep 0's step to sweep S-1's, 2 (S - 1) + 1 <= 6 steps for S <= 3), which also supplies the
+// upper pixel's sv; CRN = 0: every sweep loads its own coefficients and keeps an sv ring.
+template <int S, int MODE, int SI, int NB, int CRN>
 struct SorLane {
+  static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
+  static_assert(CRN == 0 || S <= 3, "coefficient ring depth 6 needs S <= 3");
   static constexpr int PD = NB - 1;                                    // prefetch distance (steps)
   static constexpr int U = NB % 3 == 0 ? (NB < 6 ? 6 : NB) : 3 * NB;  // multiple of 3 (ring) and NB
   static constexpr int CW = MODE == 0 ? 2 : 1;                         // float4s of coefficients per pixel
@@ -2017,7 +2023,8 @@ struct SorLane {
   float *du, *dv;
   f2v *ring_s;        // [NR][3] this sweep, lane base = entry y + 1 (entry 0 = row -1 stays zero)
   const f2v *ring_p;  // [NR][3] previous sweep
-  float *sv_s;        // [NR][3] this sweep's sv (row y's sv at entry y + 1)
+  float *sv_s;        // [NR][3] this sweep's sv (row y's sv at entry y + 1) (CRN = 0)
+  float4 *cr;         // [6][CW][CRN] coefficient ring, lane base = entry y + 1 (CRN > 0)
   int w, h, y, s, lim, rmax, hplane;
   bool border, notop;
   float omega;
@@ -2025,9 +2032,11 @@ struct SorLane {
   __device__ __forceinline__ void load(int t, Ld &B) {
     const int d = t - 2 * s;
     const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
-    const float4 *cp = C + (size_t)r0 * CW;
-    B.c0 = cp[(unsigned)y * CW];
-    if (MODE == 0) B.c1 = cp[(unsigned)y * CW + 1];
+    if (FIRST || CRN == 0) {
+      const float4 *cp = C + (size_t)r0 * CW;
+      B.c0 = cp[(unsigned)y * CW];
+      if (MODE == 0) B.c1 = cp[(unsigned)y * CW + 1];
+    }
     if (FIRST) {
       const unsigned r1 = (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane;
       const float *u0 = du_r + r0, *u1 = du_r + r1;
@@ -2058,13 +2067,32 @@ struct SorLane {
       o = ring_p[m2]; r = ring_p[m1]; bt = ring_p[3 + m1];
     }
     const f2v tp = ring_s[m1 - 3];  // row y - 1 at step t-1
-    const float tsv = sv_s[m1 - 3];  // sv of row y - 1 (entry 0: zero)
+    // coefficients of this pixel and sv of the one above (entry 0, row -1, stays zero)
+    constexpr int cs = ((Q - 2 * SI) % 6 + 6) % 6, ct = (cs + 5) % 6;  // slots of diagonals d, d - 1
+    float4 c0, c1;
+    float tsv;
+    if (CRN > 0) {
+      if (FIRST) {
+        c0 = B.c0;
+        c1 = MODE == 0 ? B.c1 : B.c0;
+        cr[cs * CW * CRN] = c0;
+        if (MODE == 0) cr[(cs * CW + 1) * CRN] = c1;
+      } else {
+        c0 = cr[cs * CW * CRN];
+        c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN] : c0;
+      }
+      tsv = cr[(ct * CW + CW - 1) * CRN - 1].w;
+    } else {
+      c0 = B.c0;
+      c1 = MODE == 0 ? B.c1 : B.c0;
+      tsv = sv_s[m1 - 3];
+    }
     f2v nw;
     float vv;
     if (MODE == 0) {
-      const float hr = B.c1.z;
-      vv = B.c1.w;
-      const f2v bb = f2v{B.c1.x, B.c1.y};
+      const float hr = c1.z;
+      vv = c1.w;
+      const f2v bb = f2v{c1.x, c1.y};
       const f2v rr = hasr ? r : f2v{0.0f, 0.0f};
       const f2v X = hr * rr, Y = tsv * tp, Z = vv * bt;
       // solver.c's three border expression trees (see sor_rhs), lane-constant operand selects
@@ -2072,12 +2100,12 @@ struct SorLane {
       const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Y) : Z);
       const f2v sr = l + rg;
       const f2v Bv = hasl ? phr * pp + sr : sr;
-      const f2v m_1 = f2v{B.c0.x, B.c0.y} * Bv.x, m_2 = f2v{B.c0.z, B.c0.w} * Bv.y;  // (i11,i12), (i12,i22)
+      const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;  // (i11,i12), (i12,i22)
       nw = o + omega * ((m_1 + m_2) - o);
       phr = hr;
     } else {
-      const float a11 = B.c0.x, b1 = B.c0.y, hr = B.c0.z;
-      vv = B.c0.w;
+      const float a11 = c0.x, b1 = c0.y, hr = c0.z;
+      vv = c0.w;
       const bool has_top = !notop, has_bot = !(border && has_top);
       const float tu = tp.x, ur = hasr ? r.x : 0.0f, hl = phr;
       float su = 0.0f, sd = 0.0f;
@@ -2090,7 +2118,7 @@ struct SorLane {
       phr = hr;
     }
     ring_s[m0] = nw;
-    sv_s[m0] = vv;
+    if (CRN == 0) sv_s[m0] = vv;
     if (LAST) {
       if ((unsigned)xp < (unsigned)w && y < h) {
         const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
@@ -2118,8 +2146,8 @@ struct SorLane {
   __device__ __forceinline__ void run(int T, int y0, int ymax) {
     pp = f2v{0.0f, 0.0f};
     phr = 0.0f;
-    const int ta = max(0, (y0 + 2 * s) / U * U);
-    const int tb = min(T, (ymax + w - 1 + 2 * s) / U * U + U);
+    const int ta = max(0, (y0 + 2 * SI) / U * U);
+    const int tb = min(T, (ymax + w - 1 + 2 * SI) / U * U + U);
     for (int t = 0; t < ta; ++t) __syncthreads();
     prologue<0>(ta);
     for (int t = ta; t < tb; t += U) block<0>(t);
@@ -2127,26 +2155,37 @@ struct SorLane {
   }
 };
 
-// LDS of the lean SOR: S (u, v) rings of NR = 64 G + 2 entries x 3 slots of float2, then S sv rings.
-__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h) {
-  return sizeof(float) * 3 * 3 * (size_t)S * (((h + 63) / 64) * 64 + 2);
+// Entries per slot of the coefficient ring: the most rows a workgroup of MAXT threads holds, + 2 halos
+// (a compile-time constant, so every ring offset is an immediate); 0 = no coefficient ring (S > 3).
+__host__ __device__ constexpr int sor_crn(int S, int MAXT) { return S <= 3 ? 64 * (MAXT / (64 * S)) + 2 : 0; }
+
+// LDS of the lean SOR: S (u, v) rings of NR = 64 G + 2 entries x 3 slots of float2, then S sv rings
+// (CRN = 0) or the [6][CW][CRN] coefficient ring (16-byte aligned).
+__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw) {
+  const size_t uv = sizeof(float) * 2 * 3 * (size_t)S * (((h + 63) / 64) * 64 + 2);
+  if (crn == 0) return uv + sizeof(float) * 3 * (size_t)S * (((h + 63) / 64) * 64 + 2);
+  return (uv + 15) / 16 * 16 + sizeof(float4) * 6 * cw * (size_t)crn;
 }
 
 // One frame's SOR call, lean form (R = 1): 64 * G * S threads.
-template <int S, int MODE, int NB>
+template <int S, int MODE, int NB, int CRN>
 __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
+  constexpr int CW = MODE == 0 ? 2 : 1;
   const int G = (a.h + 63) / 64;
   const int NR = G * 64 + 2;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = wid / S, s = wid - g * S;
   float *svr = reinterpret_cast<float *>(ring + S * 3 * NR);
+  float4 *crr = reinterpret_cast<float4 *>(reinterpret_cast<char *>(ring) + (sizeof(f2v) * S * 3 * NR + 15) / 16 * 16);
   for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) {
     ring[i] = f2v{0.f, 0.f};
-    svr[i] = 0.0f;
+    if (CRN == 0) svr[i] = 0.0f;
   }
+  if (CRN > 0)
+    for (int i = threadIdx.x; i < 6 * CW * CRN; i += blockDim.x) crr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   const long fo = (long)frame * a.sp;
-  constexpr int U = SorLane<S, MODE, true, false, NB>::U;
+  constexpr int U = SorLane<S, MODE, 0, NB, CRN>::U;
   const int T = ((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1 + U - 1) / U * U;
   const int y0 = g * 64, ymax = min(y0 + 63, a.h - 1);
   auto setup = [&](auto &st) {
@@ -2159,7 +2198,8 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.ring_s = ring + (s * NR + y + 1) * 3;
     st.ring_p = ring + ((s > 0 ? s - 1 : 0) * NR + y + 1) * 3;
     st.sv_s = svr + (s * NR + y + 1) * 3;
-    st.w = a.w; st.h = a.h; st.y = y; st.s = s;
+    st.cr = crr + y + 1;
+    st.w = a.w; st.h = a.h; st.y = y; st.s = s;  // s == SI
     st.lim = a.wrap ? a.w : 1 << 30;
     st.rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
     st.hplane = a.h;
@@ -2169,13 +2209,16 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.run(T, y0, ymax);
   };
   if (s == 0) {
-    SorLane<S, MODE, true, S == 1, NB> st;
+    SorLane<S, MODE, 0, NB, CRN> st;
     setup(st);
-  } else if (s == S - 1) {
-    SorLane<S, MODE, false, true, NB> st;
+  } else if (s == 1) {
+    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN> st;
+    setup(st);
+  } else if (s == 2) {
+    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN> st;
     setup(st);
   } else {
-    SorLane<S, MODE, false, false, NB> st;
+    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN> st;
     setup(st);
   }
 }
@@ -2510,10 +2553,10 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_waves(TvArgs a) {
   sor_waves_frame<S, MODE, R>(a, blockIdx.x, ring);
 }
 
-template <int S, int MODE, int NB, int MAXT>
+template <int S, int MODE, int NB, int MAXT, bool CRING>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
-  extern __shared__ f2v ring_uv[];  // [S][NR][3]
-  sor_lanes_frame<S, MODE, NB>(a, blockIdx.x, ring_uv);
+  extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
+  sor_lanes_frame<S, MODE, NB, CRING ? sor_crn(S, MAXT) : 0>(a, blockIdx.x, ring_uv);
 }
 
 __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
@@ -2884,15 +2927,21 @@ static void sor_waves_r(const TvArgs &a, hipStream_t s) {
   const size_t lds = sizeof(float4) * S * 3 * (G * 64 * R + 2);
   if (R == 1 && a.sor_lean) {
     const int pd = a.sor_lean;  // prefetch distance: 2, 3 or 5 steps (3, 4 or 6 buffers)
-    const size_t lds = sor_lanes_lds(S, a.h);
-    if (a.nop == 2) {
-      if (pd == 5) k_tv_sor_lanes<S, 0, 6, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
-      else if (pd == 3) k_tv_sor_lanes<S, 0, 4, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
-      else k_tv_sor_lanes<S, 0, 3, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+    constexpr int crn = sor_crn(S, MAXT);
+    const bool cring = crn > 0 && a.sor_cring;
+    const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, a.nop == 2 ? 2 : 1);
+    const int th = 64 * G * S;
+    if (cring) {
+      if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
+      else k_tv_sor_lanes<S, 2, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
+    } else if (a.nop == 2) {
+      if (pd == 5) k_tv_sor_lanes<S, 0, 6, MAXT, false><<<a.n, th, lds, s>>>(a);
+      else if (pd == 3) k_tv_sor_lanes<S, 0, 4, MAXT, false><<<a.n, th, lds, s>>>(a);
+      else k_tv_sor_lanes<S, 0, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
     } else {
-      if (pd == 5) k_tv_sor_lanes<S, 2, 6, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
-      else if (pd == 3) k_tv_sor_lanes<S, 2, 4, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
-      else k_tv_sor_lanes<S, 2, 3, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
+      if (pd == 5) k_tv_sor_lanes<S, 2, 6, MAXT, false><<<a.n, th, lds, s>>>(a);
+      else if (pd == 3) k_tv_sor_lanes<S, 2, 4, MAXT, false><<<a.n, th, lds, s>>>(a);
+      else k_tv_sor_lanes<S, 2, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
     }
     return;
   }

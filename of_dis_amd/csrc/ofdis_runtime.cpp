@@ -84,12 +84,15 @@ struct ofdis_context {
   int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
   int opt_sys_fused = 0;       // 1: system + SOR in one launch where it applies (k_tv_sys_sor; A/B: the
                                // producer wave's per-step system latency lengthens the wavefront step ~3x)
+  int opt_sor_cring = 1;       // lean SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_sor_lean = 2;        // sweep-per-wave SOR, one row per lane: lean SorLane form with this prefetch
                                // distance (2, 3, 5 steps); 0: SorWave (A/B)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
-  // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels
-  int opt_streams = 1, opt_chunk = 0;
+  // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
+  // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
+  // chains on two streams), else 1; chunk 0 = the batch split evenly over the streams.
+  int opt_streams = 0, opt_chunk = 0;
   int opt_pipeline = 0;              // two-stream pipeline: streaming stages beside the DIS + TV chain
   std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
@@ -451,6 +454,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_rows = c->opt_sor_rows;
       tv.sor_lean = c->opt_sor_lean;
       tv.sys_fused = c->opt_sys_fused;
+      tv.sor_cring = c->opt_sor_cring;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       if (c->opt_tv_fused && tv_level_fusable(tv)) {
         timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
@@ -727,12 +731,14 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
   return OFDIS_OK;
 }
 
+int stream_count(const ofdis_context *c, int n) { return c->opt_streams > 0 ? c->opt_streams : (n >= 512 ? 2 : 1); }
+
 // Chunks round-robin over opt_streams streams, each chunk's whole pipeline on one stream ("streams").
 int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
                     const uint8_t *img_b, const float *init, float *flow_out, int n, int width, int height,
                     int chunk) {
   const int nchunks = (n + chunk - 1) / chunk;
-  const int k = std::min(c->opt_streams, nchunks);
+  const int k = std::min(stream_count(c, n), nchunks);
   Plan PC = batch_plan(p, chunk, width, height, init != nullptr);
   int rc = ensure_lanes(c, k, PC.total);
   if (rc) return rc;
@@ -840,11 +846,12 @@ int ofdis_run_batch_u8_init(ofdis_context *c, const uint8_t *img_a, const uint8_
   rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
   if (rc) return rc;
   const bool capturing = !c->cap_dis.empty() || !c->cap_tv.empty();
-  const int chunk = c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : n;
+  const int nstreams = stream_count(c, n);
+  const int chunk = c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : (n + nstreams - 1) / nstreams;
   const int nchunks = (n + chunk - 1) / chunk;
   // pipelined: the streaming stages of neighbouring chunks overlap the DIS + TV chain of the current one
   const bool pipelined = c->opt_pipeline && nchunks > 1 && !capturing && !c->timing;
-  if (!pipelined && (c->opt_streams > 1 && nchunks > 1 && !capturing))
+  if (!pipelined && nchunks > 1 && !capturing)  // chunks over nstreams streams (1: serialised)
     return run_round_robin(c, s, p, img_a, img_b, init, flow_out, n, width, height, chunk);
   if (!pipelined) {
     rc = ensure_ws(c, P.total);
@@ -1010,6 +1017,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     c->opt_sor_lean = value;
     return OFDIS_OK;
   }
+  if (std::strcmp(key, "sor_cring") == 0) {
+    c->opt_sor_cring = value != 0;
+    return OFDIS_OK;
+  }
   if (std::strcmp(key, "sys_fused") == 0) {
     c->opt_sys_fused = value != 0;
     return OFDIS_OK;
@@ -1034,7 +1045,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     c->opt_sor_pipe = value != 0;
     return OFDIS_OK;
   }
-  if (std::strcmp(key, "streams") == 0 && value >= 1 && value <= 16) {
+  if (std::strcmp(key, "streams") == 0 && value >= 0 && value <= 16) {
     c->opt_streams = value;
     return OFDIS_OK;
   }

@@ -104,7 +104,8 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_rows", 4, 0),        # ... four rows per lane
     ("sys_fused", 1, 0),       # system and SOR in one launch (producer wave + LDS coefficient ring)
     ("sor_lean", 0, 2),        # ... with the SorWave sweep-per-wave SOR
-    ("sor_lean", 5, 2),        # ... with the lean SOR, prefetch distance 5
+    ("sor_lean", 5, 2),        # ... with the lean SOR, prefetch distance 5 (per-sweep coefficient loads)
+    ("sor_cring", 0, 1),       # lean SOR without the LDS coefficient ring
 ]
 
 

@@ -5,6 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${1:-pmc}
 B=${BENCH_BATCH:-1024}
+C=$(( B >= 512 ? (B + 1) / 2 : B ))  # pairs per launch: bench.py / the library split >= 512 pairs over 2 streams
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
@@ -15,4 +16,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $c rc=$rc"; tail -n 3 "$OUT/$c.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
-python tools/pmc_traffic.py "$OUT/FETCH_SIZE" "$OUT/WRITE_SIZE" "1920x1080:op2:b$B" "$OUT/traffic.json"
+python tools/pmc_traffic.py "$OUT/FETCH_SIZE" "$OUT/WRITE_SIZE" "1920x1080:op2:b$C" "$OUT/traffic.json"
