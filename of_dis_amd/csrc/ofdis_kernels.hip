@@ -1265,28 +1265,11 @@ __device__ __forceinline__ void data_de(int noc, long plane, float u, float m, c
 
 // uu / vv of the current inner iteration (refine_variational.cpp:189-190,209-222,305-320)
 
-// compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
+// s of one pixel from (wx, du, wy, dv) of the pixel and its clamped 4-neighbourhood (centre, left, right,
+// up, down): the arithmetic of compute_smoothness (opticalflow_aux.c:138-160) on uu = wx + du.
 template <int NOP>
-__device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, bool first) {
-  const long f0 = fr * a.sp, idx = f0 + kk;
-  int x, y;
-  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
-  const int w = a.w, h = a.h;
-  const int wr = a.wrap;
-  const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h, w, wr), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h, w, wr);
-  const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h, w, wr), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h, w, wr);
-  const unsigned k5[5] = {(unsigned)idx, (unsigned)kl, (unsigned)kr, (unsigned)ku, (unsigned)kd};
-  // gather everything first (one memory round trip), then uu = wx (first iteration) or wx + du
-  float wx5[5], du5[5], wy5[5], dv5[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    wx5[i] = ldu(a.wxs, k5[i]);
-    du5[i] = ldu(a.du, k5[i]);
-    if (NOP == 2) {
-      wy5[i] = ldu(a.wys, k5[i]);
-      dv5[i] = ldu(a.dv, k5[i]);
-    }
-  }
+__device__ __forceinline__ float smooth_compute(const TvArgs &a, bool first, const float (&wx5)[5],
+                                             const float (&du5)[5], const float (&wy5)[5], const float (&dv5)[5]) {
   float uu5[5], vv5[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -1310,14 +1293,34 @@ __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, b
     vy = vx;
   }
   const float eps = 0.001f * 0.001f;
-  a.s[idx] = a.quarter_alpha / sqrtf(eps + ((ux * ux + uy * uy) + (vx * vx + vy * vy)));
+  return a.quarter_alpha / sqrtf(eps + ((ux * ux + uy * uy) + (vx * vx + vy * vy)));
 }
 
-// One TV inner iteration's system (refine_variational.cpp:195-199): diffusivities from s
-// (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
-// All of a pixel's inputs are gathered first with unconditional loads (border neighbours clamped to the
-// pixel itself and discarded by selects afterwards): one memory round trip per pixel instead of one per
-// data-dependent branch.  Same arithmetic, same order as before.
+// compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
+template <int NOP>
+__device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, bool first) {
+  const long f0 = fr * a.sp, idx = f0 + kk;
+  int x, y;
+  if (!skew_xy(kk, a.w, a.h, a.wrap, x, y)) return;
+  const int w = a.w, h = a.h;
+  const int wr = a.wrap;
+  const long kl = f0 + skw(x > 0 ? x - 1 : 0, y, h, w, wr), kr = f0 + skw(x < w - 1 ? x + 1 : w - 1, y, h, w, wr);
+  const long ku = f0 + skw(x, y > 0 ? y - 1 : 0, h, w, wr), kd = f0 + skw(x, y < h - 1 ? y + 1 : h - 1, h, w, wr);
+  const unsigned k5[5] = {(unsigned)idx, (unsigned)kl, (unsigned)kr, (unsigned)ku, (unsigned)kd};
+  // gather everything first (one memory round trip), then uu = wx (first iteration) or wx + du
+  float wx5[5], du5[5], wy5[5], dv5[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    wx5[i] = ldu(a.wxs, k5[i]);
+    du5[i] = ldu(a.du, k5[i]);
+    if (NOP == 2) {
+      wy5[i] = ldu(a.wys, k5[i]);
+      dv5[i] = ldu(a.dv, k5[i]);
+    }
+  }
+  a.s[idx] = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
+}
+
 // The system of one pixel from its gathered inputs (s, wx, wy of the pixel and its 4-neighbourhood in the
 // order centre, left, right, up, down; mask; du, dv; the derivative images).  Neighbours that do not exist
 // (hasl ... hasd false) may hold any value: every use of them is behind a select.  OF: c0 = (a11, a12,
