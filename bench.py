@@ -171,6 +171,8 @@ def main():
     roofline_sor = None
     if not args.no_kernel_timing:
         # the same launches (chunk_eff pairs each), serialised on one stream: each kernel timed alone
+        # (HIP events bracketing launches of two concurrent streams do not measure the kernels: they
+        # measured 2x rocprofv3's kernel durations)
         ctx.set_option("streams", 1)
         ctx.set_option("chunk", chunk_eff)
         ctx.enable_kernel_timing(True)
