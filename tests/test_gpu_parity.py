@@ -193,7 +193,7 @@ def test_batch_equals_singles(od, ctx):
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
     ctx.set_option("graph", 1)
-    ctx.set_option("streams", 1)
+    ctx.set_option("streams", 0)
     ctx.set_option("chunk", 0)
     ctx.set_option("pipeline", 0)
     for f in range(n):
@@ -265,3 +265,32 @@ def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode, over):
         assert raw.startswith(head)
         got = -np.frombuffer(raw[len(head):], np.float32).reshape(h, w)[::-1][..., None]
     assert_bitexact(got, want, f"{exe_name} on PNG inputs")
+
+
+def test_auto_two_streams_bitexact(oracle, od, ctx):
+    """From 512 pairs the library splits the batch over two streams by default (ofdis_runtime.cpp
+    stream_count): every frame equals the one-stream whole-batch result, and frames of both chunks equal
+    the oracle."""
+    import torch
+    w, h, n, nd = 96, 64, 520, 4
+    pairs = [od.synth_pair(w, h, 1, f, 1) for f in range(nd)]
+    a = torch.from_numpy(np.stack([pairs[i % nd][0] for i in range(n)])).cuda()
+    b = torch.from_numpy(np.stack([pairs[i % nd][1] for i in range(n)])).cuda()
+    p = od.oppoint(2, w, 1, 1)
+    ctx.set_option("streams", 0)
+    ctx.set_option("chunk", 0)
+    auto = ctx.run(a, b, p)
+    torch.cuda.synchronize()
+    auto = auto.cpu().numpy()
+    ctx.set_option("streams", 1)
+    try:
+        one = ctx.run(a, b, p)
+        torch.cuda.synchronize()
+        one = one.cpu().numpy()
+    finally:
+        ctx.set_option("streams", 0)
+    assert_bitexact(auto, one, "two-stream chunks vs one stream")
+    q = oracle.oppoint(2, w, 1, 1)
+    for f in (0, 259, 260, 519):  # first / last frame of each 260-pair chunk
+        ref = oracle.run_u8(pairs[f % nd][0], pairs[f % nd][1], q)
+        assert_bitexact(auto[f], ref, f"frame {f}")
