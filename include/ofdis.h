@@ -157,12 +157,21 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        today: one workgroup per frame leaves the data-parallel phases latency-bound);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (same bits; A/B);
  *   "sor_rows" (0, 1, 2, 4): rows per lane of the sweep-per-wave SOR (0 = automatic; same bits);
+ *   "sor_lean" (0, 2, 3, 5; default 2): the one-row-per-lane SOR in its lean form (k_tv_sor_lanes) with
+ *                        this coefficient prefetch distance in steps; 0 = the earlier SorWave form;
+ *   "sor_cring" (0/1, default 1): in the lean SOR, sweep 0 loads each pixel's coefficients once and hands
+ *                        them to the later sweeps through LDS (solverit <= 3);
+ *   "sys_fused" (0/1, default 0): system and SOR of an inner iteration in one launch (a producer wave
+ *                        per row group computes the system into an LDS ring; same bits; slower today);
+ *   "sor_pipe", "sor_generic" (0/1): force the register-pipeline / generic global-memory SOR (A/B);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
  *   "graph" (0/1, default 1): replay a single-stream batch as one captured HIP graph while its pointers,
  *                        sizes and parameters repeat (re-captured when they change; same bits);
- *   "streams" (1-16, default 1) and "chunk" (frames, default 0 = whole batch): a batch is cut into
- *                        chunks that run round-robin on that many HIP streams with separate workspaces,
- *                        overlapping one chunk's latency-bound wavefront with another's streaming kernels;
+ *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1) and "chunk" (frames, default 0 =
+ *                        the batch split evenly over the streams): a batch is cut into chunks that run
+ *                        round-robin on that many HIP streams with separate workspaces, overlapping one
+ *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
+ *                        several chunks: the chunks run one after the other);
  *   "pipeline" (0/1, default 0): with "chunk" > 0, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
