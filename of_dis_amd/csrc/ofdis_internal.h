@@ -104,6 +104,7 @@ struct TvArgs {
   int sor_lean;                // sweep-per-wave SOR, one row per lane: lean form (SorLane) vs SorWave (A/B)
   int sys_fused;               // system + SOR in one launch (k_tv_sys_sor) where it applies
   int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3)
+  int smsys;                   // smoothness + system in one launch (k_tv_smsys)
 };
 
 struct UpArgs {
@@ -134,6 +135,8 @@ void launch_tv_deriv1(const TvArgs &a, hipStream_t s);
 void launch_tv_deriv2(const TvArgs &a, hipStream_t s);
 void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
+bool tv_smsys_ok(const TvArgs &a);
+void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
 bool tv_sys_sor_fusable(const TvArgs &a);
 void launch_tv_sys_sor(const TvArgs &a, hipStream_t s);

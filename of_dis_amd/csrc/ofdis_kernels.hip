@@ -1435,6 +1435,118 @@ __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
   if (kk < a.sp) tv_system_px<NOP, NOC>(a, blockIdx.y, kk);
 }
 
+// ---- smoothness + system in one launch (compute_smoothness + the system of refine_variational.cpp:195-199)
+// A workgroup takes RB consecutive rows of one frame's skewed plane.  In both layouts the 4-neighbours of a
+// row-r pixel lie in rows r - 1 (left: same column, up: column - 1) and r + 1 (right: same column, down:
+// column + 1), modulo w when folded.  Phase 0 stages (wx, wy, du, dv) of rows r0-2 .. r0+RB+1 in LDS,
+// phase 1 computes s of rows r0-1 .. r0+RB into LDS (smooth_compute, tv_smooth_px's replicate border),
+// phase 2 the system of rows r0 .. r0+RB-1 (sys_compute).  s never goes to memory and (wx, wy, du, dv)
+// are read once (plus the halo) instead of by two kernels: same functions, same bits.  blockIdx.x is the
+// frame, so the row blocks of a frame (which share halo rows) land on one XCD.
+__host__ __device__ __forceinline__ int smsys_rows(int w, int h, int wrap) { return wrap ? w : w + h - 1; }
+__host__ __device__ __forceinline__ int smsys_rb(int h) { return h >= 1024 ? 1 : (1024 / h > 16 ? 16 : 1024 / h); }
+__host__ __device__ __forceinline__ size_t smsys_lds(int h) {
+  const int rb = smsys_rb(h);
+  return (size_t)(rb + 4) * h * 16 + (size_t)(rb + 2) * h * 4;
+}
+
+template <int NOP, int NOC>
+__global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
+  extern __shared__ float4 st[];  // [(RB + 4) * h] (wx, wy, du, dv), then float s[(RB + 2) * h]
+  const int w = a.w, h = a.h, rb = smsys_rb(h), rows = smsys_rows(w, h, a.wrap);
+  float *sl = reinterpret_cast<float *>(st + (rb + 4) * h);
+  const int f = blockIdx.x, r0 = blockIdx.y * rb;
+  const long f0 = (long)f * a.sp;
+  const bool first = a.first_iter != 0;
+  // plane row of a staged / s row index (r0 - 2 + i); -1 when it does not exist (unfolded layout)
+  auto prow = [&](int r) { return a.wrap ? (r < 0 ? r + w : (r >= w ? r - w : r)) : (r < 0 || r >= rows ? -1 : r); };
+  // ---- phase 0: stage
+  for (int i = threadIdx.x; i < (rb + 4) * h; i += blockDim.x) {
+    const int ri = i / h, y = i - ri * h;
+    const int r = prow(r0 - 2 + ri);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= 0) {
+      const long o = f0 + (long)r * h + y;
+      v.x = a.wxs[o];
+      v.z = a.du[o];
+      if (NOP == 2) {
+        v.y = a.wys[o];
+        v.w = a.dv[o];
+      }
+    }
+    st[i] = v;
+  }
+  __syncthreads();
+  // ---- phase 1: s of rows r0 - 1 .. r0 + rb
+  auto pix = [&](int r, int y, int &x) {  // plane (row, column) -> pixel x; false outside the level
+    if (r < 0) return false;
+    x = r - y;
+    if (a.wrap) {
+      if (x < 0) x += w;
+      return true;
+    }
+    return x >= 0 && x < w;
+  };
+  for (int i = threadIdx.x; i < (rb + 2) * h; i += blockDim.x) {
+    const int ri = i / h, y = i - ri * h;  // s row ri <-> staged row ri + 1
+    const int r = prow(r0 - 1 + ri);
+    int x;
+    float sv = 0.0f;
+    if (pix(r, y, x)) {
+      const int c = (ri + 1) * h + y;
+      const int cl = x > 0 ? c - h : c, cr = x < w - 1 ? c + h : c;
+      const int cu = y > 0 ? c - h - 1 : c, cd = y < h - 1 ? c + h + 1 : c;
+      const float4 q0 = st[c], q1 = st[cl], q2 = st[cr], q3 = st[cu], q4 = st[cd];
+      const float wx5[5] = {q0.x, q1.x, q2.x, q3.x, q4.x}, du5[5] = {q0.z, q1.z, q2.z, q3.z, q4.z};
+      const float wy5[5] = {q0.y, q1.y, q2.y, q3.y, q4.y}, dv5[5] = {q0.w, q1.w, q2.w, q3.w, q4.w};
+      sv = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
+    }
+    sl[i] = sv;
+  }
+  __syncthreads();
+  // ---- phase 2: the system of rows r0 .. r0 + rb - 1
+  for (int i = threadIdx.x; i < rb * h; i += blockDim.x) {
+    const int ri = i / h, y = i - ri * h;
+    const int rr = r0 + ri;
+    if (rr >= rows) break;
+    int x;
+    if (!pix(rr, y, x)) continue;
+    const int c = (ri + 1) * h + y, cs = c + h;  // s index (row ri + 1), staged index (row ri + 2)
+    const int yu = y > 0 ? -1 : 0, yd = y < h - 1 ? 1 : 0;  // clamped columns; absent neighbours are discarded
+    const int s5[5] = {c, c - h, c + h, c - h + yu, c + h + yd};
+    const int t5[5] = {cs, cs - h, cs + h, cs - h + yu, cs + h + yd};
+    float S5[5], X5[5], Y5[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      S5[k] = sl[s5[k]];
+      const float4 q = st[t5[k]];
+      X5[k] = q.x;
+      Y5[k] = NOP == 2 ? q.y : 0.0f;
+    }
+    const float4 qc = st[cs];
+    const long idx = f0 + (long)rr * h + y;
+    const float m = a.mask[idx];
+    const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)rr * h + y);
+    float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
+#pragma unroll
+    for (int ch = 0; ch < NOC; ++ch) {
+      const unsigned o = qd + (unsigned)(ch * a.sp);
+      lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
+      lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
+    }
+    float4 c0, c1;
+    sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, qc.z, NOP == 2 ? qc.w : 0.0f, lIx, lIy, lIz, lIxx, lIxy, lIyy,
+                          lIxz, lIyz, c0, c1);
+    if (NOP == 2) {
+      float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
+      C[0] = c0;
+      C[1] = c1;
+    } else {
+      reinterpret_cast<float4 *>(a.coef)[idx] = c0;
+    }
+  }
+}
+
 // Generic exact-order SOR (any size / sweep count): one workgroup per frame, in-place skewed arrays in
 // global memory, one barrier per wavefront step.  Pixel (x, y) of sweep s runs at step t = x + y + 2 s:
 // its left/top neighbours of the same sweep ran at t-1, its right/bottom neighbours of the previous
@@ -2888,6 +3000,22 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
     k_tv_smooth<2><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
   else
     k_tv_smooth<1><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
+}
+bool tv_smsys_ok(const TvArgs &a) { return a.smsys && smsys_lds(a.h) <= 64 * 1024; }
+void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
+  const dim3 grid(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), smsys_rb(a.h)));
+  const size_t lds = smsys_lds(a.h);
+  if (a.nop == 2) {
+    if (a.noc == 1)
+      k_tv_smsys<2, 1><<<grid, 256, lds, s>>>(a);
+    else
+      k_tv_smsys<2, 3><<<grid, 256, lds, s>>>(a);
+  } else {
+    if (a.noc == 1)
+      k_tv_smsys<1, 1><<<grid, 256, lds, s>>>(a);
+    else
+      k_tv_smsys<1, 3><<<grid, 256, lds, s>>>(a);
+  }
 }
 void launch_tv_system(const TvArgs &a, hipStream_t s) {
   const dim3 grid(ceil_div(a.sp, 256), a.n);

@@ -84,6 +84,7 @@ struct ofdis_context {
   int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
   int opt_sys_fused = 0;       // 1: system + SOR in one launch where it applies (k_tv_sys_sor; A/B: the
                                // producer wave's per-step system latency lengthens the wavefront step ~3x)
+  int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   int opt_sor_cring = 1;       // lean SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_sor_lean = 2;        // sweep-per-wave SOR, one row per lane: lean SorLane form with this prefetch
                                // distance (2, 3, 5 steps); 0: SorWave (A/B)
@@ -455,6 +456,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_lean = c->opt_sor_lean;
       tv.sys_fused = c->opt_sys_fused;
       tv.sor_cring = c->opt_sor_cring;
+      tv.smsys = c->opt_smsys;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       if (c->opt_tv_fused && tv_level_fusable(tv)) {
         timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
@@ -471,8 +473,12 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
             timed(c, 12, s, [&] { launch_tv_sys_sor(tv, s); });
           } else {
             timed(c, 7, s, [&] {
-              launch_tv_smooth(tv, s);
-              launch_tv_system(tv, s);
+              if (tv_smsys_ok(tv)) {
+                launch_tv_smsys(tv, s);
+              } else {
+                launch_tv_smooth(tv, s);
+                launch_tv_system(tv, s);
+              }
             });
             timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
           }
@@ -1015,6 +1021,10 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   }
   if (std::strcmp(key, "sor_lean") == 0 && (value == 0 || value == 2 || value == 3 || value == 5)) {
     c->opt_sor_lean = value;
+    return OFDIS_OK;
+  }
+  if (std::strcmp(key, "smsys") == 0) {
+    c->opt_smsys = value != 0;
     return OFDIS_OK;
   }
   if (std::strcmp(key, "sor_cring") == 0) {

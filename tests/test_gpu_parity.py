@@ -106,6 +106,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_lean", 0, 2),        # ... with the SorWave sweep-per-wave SOR
     ("sor_lean", 5, 2),        # ... with the lean SOR, prefetch distance 5 (per-sweep coefficient loads)
     ("sor_cring", 0, 1),       # lean SOR without the LDS coefficient ring
+    ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
 ]
 
 
