@@ -959,12 +959,17 @@ __device__ __forceinline__ void tv_prep_px(const TvArgs &a, int x, int y, int f)
 // is read / written by rows, the skewed side by anti-diagonal segments of the tile (16 consecutive floats),
 // so neither side scatters 4-byte accesses over 64 cache lines per instruction.  Row pitch 66: the
 // diagonal-order accesses (row yy, column dd - yy) hit 16 different banks.
-constexpr int kTileW = 64, kTileH = 16, kTileP = 66, kTileD = kTileW + kTileH - 1;
+// TH: tile height.  A diagonal's run inside a 64 x TH tile is min(64, TH) pixels long, so the skewed side
+// moves TH-float segments (TH = 16: 64-byte half lines, 2-3x the algorithmic bytes on the bus; taller
+// tiles cut that).  NP = 3 + 2 noc planes.
+constexpr int kTileW = 64, kTileP = 66;
+template <int NP, int TH>
 __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
-  __shared__ float sm[9][kTileH][kTileP];  // mask, wx, wy, t[noc], dt[noc]
-  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH, f = blockIdx.z;
-  const int tx = threadIdx.x & 63, np = 3 + 2 * a.noc;
-  for (int yl = threadIdx.x >> 6; yl < kTileH; yl += 4) {
+  __shared__ float sm[NP][TH][kTileP];  // mask, wx, wy, t[noc], dt[noc]
+  constexpr int TD = kTileW + TH - 1;
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
+  const int tx = threadIdx.x & 63, np = NP;
+  for (int yl = threadIdx.x >> 6; yl < TH; yl += 4) {
     const int x = x0 + tx, y = y0 + yl;
     if (x < a.w && y < a.h) {
       float v[9];
@@ -973,8 +978,8 @@ __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kTileD * kTileH; i += 256) {
-    const int yy = i & (kTileH - 1), dd = i / kTileH, xl = dd - yy;
+  for (int i = threadIdx.x; i < TD * TH; i += 256) {
+    const int yy = i & (TH - 1), dd = i / TH, xl = dd - yy;
     const int x = x0 + xl, y = y0 + yy;
     if (xl < 0 || xl >= kTileW || x >= a.w || y >= a.h) continue;
     float v[9];
@@ -2688,11 +2693,13 @@ __device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f
   }
 }
 
+template <int TH>
 __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
-  __shared__ float sm[2][kTileH][kTileP];
-  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH, f = blockIdx.z;
-  for (int i = threadIdx.x; i < kTileD * kTileH; i += 256) {  // skewed side: diagonal segments
-    const int yy = i & (kTileH - 1), dd = i / kTileH, xl = dd - yy;
+  __shared__ float sm[2][TH][kTileP];
+  constexpr int TD = kTileW + TH - 1;
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
+  for (int i = threadIdx.x; i < TD * TH; i += 256) {  // skewed side: diagonal segments
+    const int yy = i & (TH - 1), dd = i / TH, xl = dd - yy;
     const int x = x0 + xl, y = y0 + yy;
     if (xl < 0 || xl >= kTileW || x >= a.w || y >= a.h) continue;
     const long fk = (long)f * a.sp + skw(x, y, a.h, a.w, a.wrap);
@@ -2708,7 +2715,7 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
   const int tx = threadIdx.x & 63, x = x0 + tx;
   const long plane = (long)a.w * a.h;
   float *WX = a.flow + (long)f * a.nop * plane;
-  for (int yl = threadIdx.x >> 6; yl < kTileH; yl += 4) {  // row-major side: rows
+  for (int yl = threadIdx.x >> 6; yl < TH; yl += 4) {  // row-major side: rows
     const int y = y0 + yl;
     if (x >= a.w || y >= a.h) continue;
     const long o = (long)y * a.w + x;
@@ -2987,7 +2994,10 @@ void launch_aggregate(const AggArgs &a, hipStream_t s) {
   k_aggregate<<<dim3(ceil_div(a.g.w, 64), ceil_div(a.g.h, 16), a.n), 256, 0, s>>>(a);
 }
 void launch_tv_prep(const TvArgs &a, hipStream_t s) {
-  k_tv_prep<<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, kTileH), a.n), 256, 0, s>>>(a);
+  if (a.noc == 1)
+    k_tv_prep<5, 32><<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, 32), a.n), 256, 0, s>>>(a);
+  else
+    k_tv_prep<9, 16><<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, 16), a.n), 256, 0, s>>>(a);
 }
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
   k_tv_deriv1<<<dim3(ceil_div(a.sp, 256), a.n * a.noc), 256, 0, s>>>(a);
@@ -3164,7 +3174,7 @@ void launch_tv_level(const TvArgs &a, int n_inner, hipStream_t s) {
   }
 }
 void launch_tv_final(const TvArgs &a, hipStream_t s) {
-  k_tv_final<<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, kTileH), a.n), 256, 0, s>>>(a);
+  k_tv_final<32><<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, 32), a.n), 256, 0, s>>>(a);
 }
 // OpenCV resizeAreaFast for the initial flow (oracle: ofo_init_flow_area): one thread per output value,
 // the k x k block in row-major order, sum += ((a + b) + c) + d four at a time, then x 1/k^2.  The chain is
