@@ -4,16 +4,24 @@
 Default workload (BASELINE configs[1], "B"): run_OF_INT 1920x1080 grayscale, operating point 2 (patch 8,
 overlap 0.4, TV on), batches of synthetic frame pairs resident in HBM.  One step = the whole hot path
 (pad + pyramid + DIS + aggregation + TV + upsample + crop) over one batch of `--batch` pairs per GPU.
-`--config A|C|D|E` runs the other BASELINE configs (640x480 op2; 1080p RGB op3 with the L1 cost; B at
-32 pairs per GPU = 256 over 8 GPUs; 4K stereo depth op4 with 10 TV outer iterations).
-N > 1: one process per GPU (torch.distributed.run); frames are sharded, no data-path collective; the
-only collectives are the barrier and the max-over-ranks of the elapsed time (RCCL, control traffic).
+`--config A|C|C2|D|E` runs the other BASELINE configs (640x480 op2; 1080p RGB op3 with the L1 cost / as
+op-point 3 defines it (L2); B at 32 pairs per GPU = 256 over 8 GPUs; 4K stereo depth op4 with 10 TV outer
+iterations).
+
+Multi-GPU: `--gpus N` (N > 1) without a torch.distributed environment re-launches this script as N ranks
+(`python -m torch.distributed.run --nproc-per-node N`, a child process -- this parent never touches a GPU)
+and exits with its status.  Each rank owns a contiguous shard of frames (no data-path collective); the
+control collectives are a broadcast of rank 0's parameters, the barrier + max-over-ranks of the timed
+region, and a sum of counters (frames, parity, kernel time) -- RCCL on GPU.  `--dry-run` runs the same
+rank logic on gloo without a GPU (CPU test of the launcher and the shard bookkeeping).
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,10 +38,13 @@ CONFIGS = {
     "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 1024),
     # op-point 3 as the config text states it ("finer scale, L1 cost"): op3 values with costfct = 1
     "C": ("run_OF_RGB", 1920, 1080, 3, 1, 3, "6 2 16 16 0.05 0.95 0 12 0.75 0 1 1 1 10 10 5 1 3 1.6 2", 64),
+    # op-point 3 as run_dense.cpp:248-253 defines it (costfct 0, L2); SURVEY §8(d): report both
+    "C2": ("run_OF_RGB", 1920, 1080, 3, 1, 3, None, 64),
     "D": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 32),
     # op-point 4 values with tv_innerit = 10
     "E": ("run_DE_INT", 3840, 2160, 1, 2, 4, "7 2 128 128 0.05 0.95 0 12 0.75 0 1 0 1 10 10 5 10 3 1.6 2", 256),
 }
+METRIC = "MPix/s (and frames/sec) 1080p op-point-2; avg EPE vs CPU ref"
 
 
 def parse():
@@ -44,21 +55,37 @@ def parse():
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="frame pairs per GPU per step (0 = the config's)")
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bounded CPU-baseline sample per leg (1 core, all cores; 0 = skip)")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams the batch's chunks round-robin over (0 = the library's auto: 2 from 512 pairs)")
     ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = the batch split over the streams)")
-    ap.add_argument("--tv-fused", type=int, default=-1, help="1/0: force the fused TV level kernel on/off")
     ap.add_argument("--option", action="append", default=[], help="context option key=value (A/B runs)")
     ap.add_argument("--host-io", action="store_true",
                     help="also time the host-buffer entry point (PCIe-inclusive rate, reported separately)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip the single-pair latency leg")
+    ap.add_argument("--dry-run", action="store_true", help="rank/shard bookkeeping on gloo, no GPU (CPU test)")
     return ap.parse_args()
+
+
+def relaunch_as_ranks(args) -> int:
+    """`--gpus N` outside a torch.distributed environment: run N ranks as a child torchrun job."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def config_tag(cfg, B):
     """Workload key of profiles/traffic.json (tools/pmc_traffic.py)."""
-    return f"{cfg[1]}x{cfg[2]}:op{cfg[5]}:b{B}" + ("" if cfg[3] == 1 else ":rgb")
+    return f"{cfg[1]}x{cfg[2]}:op{cfg[5]}:b{B}" + ("" if cfg[3] == 1 else ":rgb") + (
+        ":l1" if cfg[6] and cfg[3] == 3 else "")
 
 
 def kernel_roofline(od, p, W, H, B, per_launch, cfg, steps, kernels, name):
@@ -92,14 +119,131 @@ def params_of(mod, cfg):
     return mod.oppoint(op, W, mode, noc)
 
 
+def oracle_params(O, p):
+    q = O.Params()
+    for k, v in p.as_dict().items():
+        setattr(q, k, v)
+    return q
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores() -> int:
+    """The host cores this process may use: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
+    GPU pool) capped by the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, share) if share > 0 else aff)
+
+
+def cpu_baseline(O, q, pairs, W, H, seconds, binary, cfg_name):
+    """The oracle port (oracle/ofdis_oracle.c, -O3 -msse4.1 -ffp-contract=off; the reference's default
+    build semantics: lexicographic block SOR, no OpenMP) timed over whole pairs (pad + pyramid + OFClass
+    + upsample, the reference's verbosity-2 timer scope): one core, then one single-threaded worker per
+    host core, frame-parallel (ctypes releases the GIL inside the oracle)."""
+    from concurrent.futures import ThreadPoolExecutor
+    nd = len(pairs)
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        O.run_u8(pairs[done % nd][0], pairs[done % nd][1], q)
+        done += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    t1 = time.perf_counter() - t0
+    cores = host_cores()
+    done_all = 0
+    t_all = 0.0
+    if cores > 1:
+        deadline = time.perf_counter() + seconds
+
+        def worker(k):
+            n = 0
+            while True:
+                O.run_u8(pairs[(k + n) % nd][0], pairs[(k + n) % nd][1], q)
+                n += 1
+                if time.perf_counter() > deadline:
+                    return n
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            done_all = sum(ex.map(worker, range(cores)))
+        t_all = time.perf_counter() - t0
+    fair = None
+    ff = os.path.join(ROOT, "profiles", "cpu_fairness.json")
+    if os.path.exists(ff):
+        try:
+            fair = json.load(open(ff))
+        except Exception:
+            fair = None
+    out = {"value": round(W * H * done / t1 / 1e6, 3), "unit": "MPix/s", "cores": 1, "kind": "port",
+           "frames_per_sec": round(done / t1, 3),
+           "sample": f"{done} synthetic {W}x{H} {binary} pairs (config {cfg_name}), oracle/ofdis_oracle.c -O3 "
+                     f"-msse4.1, 1 thread (pad+pyramid+OFClass+upsample), {t1:.1f} s",
+           "cores_all": cores, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "fairness_vs_reference": fair}
+    if done_all:
+        out["value_all_cores"] = round(W * H * done_all / t_all / 1e6, 3)
+        out["frames_per_sec_all_cores"] = round(done_all / t_all, 3)
+        out["sample_all_cores"] = f"{done_all} pairs over {cores} worker threads, {t_all:.1f} s"
+    return out
+
+
+def dry_run(args, cfg):
+    """The rank logic without a GPU: gloo, shard bookkeeping, the control collectives."""
+    import torch.distributed as dist
+    from of_dis_amd import distributed as odd
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = args.batch or cfg[7]
+    shard = odd.shard_range(B * world, rank, world)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = odd.max_over_ranks(elapsed)
+        frames = odd.sum_over_ranks([shard[1] - shard[0]])[0]
+        shards = odd.all_gather_objects(list(shard))
+    else:
+        frames, shards = shard[1] - shard[0], [list(shard)]
+    if rank == 0:
+        if world != args.gpus:
+            raise SystemExit(f"world size {world} != --gpus {args.gpus}")
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": args.steps,
+                          "config": {"name": args.config, "batch_per_gpu": B}, "shards": shards,
+                          "frames": int(frames), "elapsed_max_s": elapsed}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_as_ranks(args))
+    cfg = CONFIGS[args.config]
+    if args.dry_run:
+        return dry_run(args, cfg)
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -111,11 +255,12 @@ def main():
     import of_dis_amd as od
     from of_dis_amd import distributed as odd
 
-    cfg = CONFIGS[args.config]
     binary, W, H, noc, mode, op, explicit, default_batch = cfg
     B = args.batch or default_batch
     p = params_of(od, cfg)
     p.verbosity = 0
+    if world > 1:  # one configuration for every shard
+        odd.broadcast_params(p, dev)
     nop = p.nop
     ctx = od.Context(dev.index)
     ctx.set_option("streams", args.streams)
@@ -123,21 +268,22 @@ def main():
     # the library's chunking (ofdis_runtime.cpp stream_count): streams 0 = 2 from 512 pairs, else 1
     streams_eff = args.streams or (2 if B >= 512 else 1)
     chunk_eff = min(B, args.chunk or -(-B // streams_eff))
-    if args.tv_fused >= 0:
-        ctx.set_option("tv_fused", args.tv_fused)
     for kv in args.option:
         k, v = kv.split("=")
         ctx.set_option(k, int(v))
 
-    # synthetic inputs, resident in HBM before timing: distinct pairs per rank, tiled over the batch
+    # synthetic inputs, resident in HBM before timing: this rank's shard of frames, distinct pairs tiled
     first = odd.shard_range(B * world, rank, world)[0]
     nd = max(1, min(args.distinct, B))
     pairs = [od.synth_pair(W, H, noc, first + k, mode) for k in range(nd)]
     a = torch.empty((B, H, W, noc), dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
-    for i in range(B):
-        a[i].copy_(torch.from_numpy(pairs[i % nd][0]))
-        b[i].copy_(torch.from_numpy(pairs[i % nd][1]))
+    for i in range(nd):
+        a[i].copy_(torch.from_numpy(pairs[i][0]))
+        b[i].copy_(torch.from_numpy(pairs[i][1]))
+    for i in range(nd, B):
+        a[i].copy_(a[i % nd])
+        b[i].copy_(b[i % nd])
     out = torch.empty((B, H, W, nop), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -159,6 +305,8 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     elapsed = odd.max_over_ranks(elapsed, dev) if world > 1 else elapsed
+    # the timed pass's output of the distinct pairs, for the parity check below
+    timed_out = out[:nd].cpu().numpy()
 
     frames = B * world * args.steps
     mpix = W * H * frames / elapsed / 1e6
@@ -179,10 +327,17 @@ def main():
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize(dev)
-        for k in od.kernel_names():
+        names = [k for k in od.kernel_names()]
+        raw = []
+        for k in names:
             ms, cnt = ctx.kernel_time(k)
+            raw += [ms, cnt]
+        if world > 1:  # whole-job device time per kernel (every rank ran the same launches)
+            raw = odd.sum_over_ranks(raw, dev)
+        for i, k in enumerate(names):
+            ms, cnt = raw[2 * i], int(raw[2 * i + 1])
             if cnt:
-                kernels[k] = {"total_ms": ms, "launches": cnt, "avg_us": ms / cnt * 1e3}
+                kernels[k] = {"total_ms": ms / world, "launches": cnt // world, "avg_us": ms / cnt * 1e3}
         ctx.enable_kernel_timing(False)
         ctx.set_option("streams", args.streams)
         ctx.set_option("chunk", args.chunk)
@@ -190,6 +345,11 @@ def main():
         roofline = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, dom)
         if dom != "tv_sor" and "tv_sor" in kernels:  # the north-star kernel, reported beside the dominant one
             roofline_sor = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, "tv_sor")
+
+    # ---- single-pair latency (the drop-in CLI's case: one pair per call), device-resident and host buffers
+    latency = None
+    if rank == 0 and world == 1 and not args.no_latency:
+        latency = pair_latency(od, ctx, p, pairs[0], dev, torch)
 
     # ---- host-buffer entry point (PCIe-inclusive; never the headline value)
     host_io = None
@@ -205,58 +365,97 @@ def main():
         host_io = {"value": round(W * H * B * reps / th / 1e6, 2), "unit": "MPix/s",
                    "what": "ofdis_run_batch_u8_host: u8 frames H2D + whole path + f32 flow D2H, pageable host memory"}
 
-    # ---- CPU baseline (rank 0, N=1 only): the oracle port, single thread, bounded sample
+    # ---- parity of the timed pass vs the CPU oracle (every rank: its shard's first frames), and the CPU
+    # baseline (rank 0, N = 1 only): the oracle port on this host's cores, bounded samples
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    sums = [0.0, 0.0, 0.0, 0.0]  # compared frames, sum of avg EPE, max avg EPE, bit-exact frames
+    if args.cpu_seconds > 0:
         from oracle import pyoracle as O
-        q = params_of(O, cfg) if hasattr(O, "params_from_strings") or not explicit else None
-        if q is None:  # the oracle's mirror of ofdis_params: same fields, same meaning
-            q = O.Params()
-            for k, v in p.as_dict().items():
-                setattr(q, k, v)
-        done, t0c, max_epe, bitexact = 0, time.perf_counter(), 0.0, 0
-        gpu_out = out.cpu().numpy()
-        while True:
-            k = done % nd
+        q = oracle_params(O, p)
+        ncmp = nd if world == 1 else 1
+        for k in range(ncmp):
             ref = O.run_u8(pairs[k][0], pairs[k][1], q)
-            done += 1
-            if done <= nd:  # compare against the GPU output of the same pair
-                g = gpu_out[k]
-                epe = float(np.sqrt(((g - ref) ** 2).sum(-1)).mean())
-                max_epe = max(max_epe, epe)
-                bitexact += int(np.array_equal(g.view(np.uint32), ref.view(np.uint32)))
-            if time.perf_counter() - t0c > args.cpu_seconds:
-                break
-        tc = time.perf_counter() - t0c
-        cpu = {"value": round(W * H * done / tc / 1e6, 3), "unit": "MPix/s", "cores": 1, "kind": "port",
-               "frames_per_sec": round(done / tc, 3),
-               "sample": f"{done} synthetic {W}x{H} {binary} pairs (config {args.config}), oracle/ofdis_oracle.c "
-                         f"single thread (pad+pyramid+OFClass+upsample), {tc:.1f} s"}
-        parity = {"avg_epe_vs_cpu_ref_max": max_epe, "bitexact_frames": bitexact, "compared_frames": min(done, nd)}
+            g = timed_out[k]
+            epe = float(np.sqrt(((g.astype(np.float64) - ref) ** 2).sum(-1)).mean())
+            sums[0] += 1
+            sums[1] += epe
+            sums[2] = max(sums[2], epe)
+            sums[3] += int(np.array_equal(g.view(np.uint32), ref.view(np.uint32)))
+        if rank == 0 and world == 1:
+            cpu = cpu_baseline(O, q, pairs, W, H, args.cpu_seconds, binary, args.config)
+    if world > 1:
+        tot = odd.sum_over_ranks([sums[0], sums[1], sums[3]], dev)
+        sums = [tot[0], tot[1], odd.max_over_ranks(sums[2], dev), tot[2]]
+    if sums[0]:
+        parity = {"avg_epe_vs_cpu_ref": sums[1] / sums[0], "avg_epe_vs_cpu_ref_max": sums[2],
+                  "bitexact_frames": int(sums[3]), "compared_frames": int(sums[0]), "checked": "timed pass output"}
 
     if rank == 0:
         line = {
-            "metric": "MPix/s (and frames/sec) 1080p op-point-2; avg EPE vs CPU ref",
+            "metric": METRIC,
             "value": round(mpix, 2), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "frames_per_sec": round(frames / elapsed, 2),
+            "per_gpu_mpix_s": round(mpix / world, 2),
             "config": {"workload": f"{binary} {W}x{H} op-point {op}" + (f" ({explicit})" if explicit else "")
                                    + f", {B} pairs/GPU/step", "name": args.config,
                        "width": W, "height": H, "channels": noc, "oppoint": op, "batch_per_gpu": B,
-                       "streams": streams_eff, "pairs_per_launch": chunk_eff, "tv_fused": args.tv_fused,
+                       "streams": streams_eff, "pairs_per_launch": chunk_eff,
                        "options": args.option,
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,
-            "host_io": host_io, "kernels": kernels,
+            "latency": latency, "host_io": host_io, "kernels": kernels,
         }
         if cpu:
             line["speedup_vs_cpu_1core"] = round(mpix / cpu["value"], 1)
+            if cpu.get("value_all_cores"):
+                line["speedup_vs_cpu_all_cores"] = round(mpix / cpu["value_all_cores"], 1)
         print(json.dumps(line))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pair_latency(od, ctx, p, pair, dev, torch, reps=20):
+    """One pair per call (run_dense.cpp's case): device-resident (u8 in HBM, flow out in HBM, synchronised
+    per call) and through host buffers (ofdis_run_batch_u8_host: H2D + path + D2H), plus the per-kernel
+    breakdown of one device-resident pair."""
+    H, W, noc = pair[0].shape
+    a = torch.from_numpy(pair[0][None]).to(dev)
+    b = torch.from_numpy(pair[1][None]).to(dev)
+    o = torch.empty((1, H, W, p.nop), dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ctx.set_option("streams", 1)
+    ctx.set_option("chunk", 0)
+    for _ in range(3):
+        ctx.run_ptr(a.data_ptr(), b.data_ptr(), 1, W, H, p, o.data_ptr(), s)
+    torch.cuda.synchronize(dev)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.run_ptr(a.data_ptr(), b.data_ptr(), 1, W, H, p, o.data_ptr(), s)
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    th = []
+    for _ in range(max(3, reps // 4)):
+        t0 = time.perf_counter()
+        ctx.run_host(pair[0], pair[1], p)
+        th.append(time.perf_counter() - t0)
+    ctx.enable_kernel_timing(True)
+    ctx.run_ptr(a.data_ptr(), b.data_ptr(), 1, W, H, p, o.data_ptr(), s)
+    torch.cuda.synchronize(dev)
+    brk = {}
+    for k in od.kernel_names():
+        ms, cnt = ctx.kernel_time(k)
+        if cnt:
+            brk[k] = {"ms": round(ms, 4), "launches": cnt}
+    ctx.enable_kernel_timing(False)
+    ctx.set_option("streams", 0)
+    return {"pairs_per_call": 1, "device_ms_median": round(float(np.median(ts)) * 1e3, 3),
+            "device_ms_min": round(min(ts) * 1e3, 3), "host_ms_median": round(float(np.median(th)) * 1e3, 3),
+            "kernels_one_pair": brk}
 
 
 if __name__ == "__main__":

@@ -116,7 +116,11 @@ void ofdis_context_destroy(ofdis_context *ctx);
  * OFClass (:392-401) -> x 2^sc_l + INTER_LINEAR upsample + crop (:407-415).
  * img_a/img_b: device u8 [n][height][width][noc] (BGR order when noc = 3).
  * flow_out: device float [n][height][width][nop] (nop = 2 OF, 1 DE).
- * stream: hipStream_t (NULL = the context's own stream).  Asynchronous w.r.t. the host.
+ * stream: hipStream_t, or NULL for the legacy default stream (torch's default): the call is then ordered
+ * after the work already queued there and that stream's later work after the call.  Asynchronous w.r.t. the
+ * host.  All calls on one context share its workspaces: a call waits for the previous call of the context
+ * whatever stream either was issued on.  A batch is split into launches of at most
+ * ofdis_max_frames_per_launch() frames.
  */
 int ofdis_run_batch_u8(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
                        int height, const ofdis_params *p, float *flow_out, void *stream);
@@ -147,37 +151,32 @@ int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int
  * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL). */
 int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, float *const *tv_flow, int nscales);
 
-/* Tuning / A-B switches:
- *   "sor_generic" (0/1): force the generic global-memory SOR wavefront instead of the register-pipelined
- *                        one (both are exact-order; used by the parity tests);
- *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline instead of the default
- *                        sweep-per-wave SOR (same bits; A/B and parity tests);
- *   "tv_fused" (0/1, default 0): run each refinement level as one launch per frame (k_tv_level) when the
- *                        level fits one workgroup, instead of one launch per phase (same bits; slower
- *                        today: one workgroup per frame leaves the data-parallel phases latency-bound);
- *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (same bits; A/B);
- *   "sor_rows" (0, 1, 2, 4): rows per lane of the sweep-per-wave SOR (0 = automatic; same bits);
- *   "sor_lean" (0, 2, 3, 5; default 2): the one-row-per-lane SOR in its lean form (k_tv_sor_lanes) with
- *                        this coefficient prefetch distance in steps; 0 = the earlier SorWave form;
- *   "sor_cring" (0/1, default 1): in the lean SOR, sweep 0 loads each pixel's coefficients once and hands
- *                        them to the later sweeps through LDS (solverit <= 3);
- *   "sys_fused" (0/1, default 0): system and SOR of an inner iteration in one launch (a producer wave
- *                        per row group computes the system into an LDS ring; same bits; slower today);
- *   "sor_pipe", "sor_generic" (0/1): force the register-pipeline / generic global-memory SOR (A/B);
+/* Tuning / A-B switches (all exact: results never depend on them):
+ *   "sor_generic" (0/1): force the generic global-memory SOR wavefront;
+ *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline (the default for tall levels)
+ *                        instead of the sweep-per-wave SOR;
+ *   "sor_cring" (0/1, default 1): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
+ *                        hands them to the later sweeps through LDS (solverit <= 3);
+ *   "smsys" (0/1, default 1): smoothness and system of a TV iteration in one launch;
+ *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch;
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
- *   "graph" (0/1, default 1): replay a single-stream batch as one captured HIP graph while its pointers,
- *                        sizes and parameters repeat (re-captured when they change; same bits);
+ *   "graph" (0/1, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
+ *                        parameters repeat (re-captured when they change);
  *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1) and "chunk" (frames, default 0 =
  *                        the batch split evenly over the streams): a batch is cut into chunks that run
  *                        round-robin on that many HIP streams with separate workspaces, overlapping one
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
- *   "pipeline" (0/1, default 0): with "chunk" > 0, a two-stream software pipeline instead: one stream runs
+ *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
- * Setting any option drops the captured graph.  Results never depend on these settings (frames are
- * independent). */
+ * Setting any option drops the captured graph.  Unknown keys and out-of-range values return
+ * OFDIS_ERR_INVALID_ARGUMENT. */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);
+
+/* Largest number of frame pairs one launch of the refinement kernels takes at this size (their plane groups
+ * are addressed with 32-bit offsets: frames * noc * plane < 2^30 floats); larger batches are chunked. */
+int ofdis_max_frames_per_launch(const ofdis_params *p, int width, int height, int *frames);
 
 /* HIP-event timing of individual kernels on the launch stream (used by bench.py for the roofline). */
 int ofdis_context_enable_kernel_timing(ofdis_context *ctx, int enable);

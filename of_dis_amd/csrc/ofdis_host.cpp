@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "../../include/ofdis.h"
@@ -258,25 +260,40 @@ int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, i
   const double ang = (0.5 * std::sin(0.7 * frame)) * 3.141592653589793 / 180.0;
   const double zoom = 1.0 + 0.01 * std::cos(1.3 * frame);
   const double ca = std::cos(ang) * zoom, sn = std::sin(ang) * zoom;
-  for (int y = 0; y < height; ++y)
-    for (int x = 0; x < width; ++x) {
-      double bx, by;
-      if (mode == OFDIS_MODE_DE) {
-        bx = x + 6.5;  // b(x) = a(x + 6.5): disparity -6.5
-        by = y;
-      } else {
-        // inverse of p -> R (p - c) + c + t
-        const double qx = x - cx - 6.5, qy = y - cy - 2.25;
-        const double det = ca * ca + sn * sn;
-        bx = (ca * qx + sn * qy) / det + cx;
-        by = (-sn * qx + ca * qy) / det + cy;
+  const size_t n = (size_t)width * height * noc;
+  // the noise streams are sequential (one splitmix64 sequence per frame, pixel-major order) ...
+  std::vector<double> na(n), nb(n);
+  for (size_t o = 0; o < n; ++o) {
+    na[o] = 2.0 * gauss(sa);
+    nb[o] = 2.0 * gauss(sb);
+  }
+  // ... the texture is evaluated row-parallel (same values: every pixel's expression is unchanged)
+  auto rows = [&](int y0, int y1) {
+    for (int y = y0; y < y1; ++y)
+      for (int x = 0; x < width; ++x) {
+        double bx, by;
+        if (mode == OFDIS_MODE_DE) {
+          bx = x + 6.5;  // b(x) = a(x + 6.5): disparity -6.5
+          by = y;
+        } else {
+          // inverse of p -> R (p - c) + c + t
+          const double qx = x - cx - 6.5, qy = y - cy - 2.25;
+          const double det = ca * ca + sn * sn;
+          bx = (ca * qx + sn * qy) / det + cx;
+          by = (-sn * qx + ca * qy) / det + cy;
+        }
+        for (int c = 0; c < noc; ++c) {
+          const size_t o = ((size_t)y * width + x) * noc + c;
+          img_a[o] = to_u8(texture(x, y, c) + na[o]);
+          img_b[o] = to_u8(texture(bx, by, c) + nb[o]);
+        }
       }
-      for (int c = 0; c < noc; ++c) {
-        const size_t o = ((size_t)y * width + x) * noc + c;
-        img_a[o] = to_u8(texture(x, y, c) + 2.0 * gauss(sa));
-        img_b[o] = to_u8(texture(bx, by, c) + 2.0 * gauss(sb));
-      }
-    }
+  };
+  const int nt = std::max(1, std::min({16, (int)std::thread::hardware_concurrency(), height / 32}));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(rows, (int)((long)height * t / nt), (int)((long)height * (t + 1) / nt));
+  rows(0, (int)((long)height / nt));
+  for (auto &t : th) t.join();
   return OFDIS_OK;
 }
 

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../include/ofdis.h"
@@ -103,6 +104,8 @@ inline unsigned sample(const uint8_t *row, size_t s, int depth) {
   }
 }
 
+constexpr uint64_t kMaxImagePixels = 1ull << 30;
+
 int decode_png(const std::vector<uint8_t> &f, int want, Image &img) {
   static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
   if (f.size() < 8 || std::memcmp(f.data(), sig, 8) != 0) return OFDIS_ERR_IO;
@@ -143,6 +146,8 @@ int decode_png(const std::vector<uint8_t> &f, int want, Image &img) {
     pos += 12 + len;
   }
   if (!seen_ihdr || !seen_iend || W == 0 || H == 0 || W > (1u << 24) || H > (1u << 24)) return OFDIS_ERR_IO;
+  // OpenCV's CV_IO_MAX_IMAGE_PIXELS (2^30): refuse before sizing any buffer from the header alone
+  if ((uint64_t)W * H > kMaxImagePixels) return OFDIS_ERR_IO;
   int nch;
   switch (ctype) {
     case 0: nch = 1; if (depth != 1 && depth != 2 && depth != 4 && depth != 8 && depth != 16) return OFDIS_ERR_IO; break;
@@ -300,6 +305,7 @@ int decode_pnm(const std::vector<uint8_t> &f, int want, Image &img) {
   const int w = cur.token(), h = cur.token();
   const int maxv = bitmap ? 1 : cur.token();
   if (w <= 0 || h <= 0 || maxv <= 0 || (maxv > 255 && maxv != 65535)) return OFDIS_ERR_IO;
+  if ((uint64_t)w * h > kMaxImagePixels) return OFDIS_ERR_IO;
   const size_t n = (size_t)w * h * nch;
   std::vector<unsigned> v(n);
   if (ascii) {
@@ -358,23 +364,29 @@ extern "C" {
 
 int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height, int want_noc, size_t capacity) {
   if (!path || !width || !height || (want_noc != 1 && want_noc != 3)) return OFDIS_ERR_INVALID_ARGUMENT;
-  std::vector<uint8_t> f;
-  if (!read_file(path, f)) return OFDIS_ERR_IO;
-  Image img;
-  int rc;
-  if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G')
-    rc = decode_png(f, want_noc, img);
-  else if (f.size() >= 2 && f[0] == 'P' && f[1] >= '1' && f[1] <= '6')
-    rc = decode_pnm(f, want_noc, img);
-  else
-    rc = OFDIS_ERR_UNSUPPORTED;
-  if (rc) return rc;
-  *width = img.w;
-  *height = img.h;
-  if (!pixels) return OFDIS_OK;
-  if (capacity < img.px.size()) return OFDIS_ERR_INVALID_ARGUMENT;
-  std::memcpy(pixels, img.px.data(), img.px.size());
-  return OFDIS_OK;
+  try {  // no C++ exception may cross the C-ABI: a failed allocation becomes a status code
+    std::vector<uint8_t> f;
+    if (!read_file(path, f)) return OFDIS_ERR_IO;
+    Image img;
+    int rc;
+    if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G')
+      rc = decode_png(f, want_noc, img);
+    else if (f.size() >= 2 && f[0] == 'P' && f[1] >= '1' && f[1] <= '6')
+      rc = decode_pnm(f, want_noc, img);
+    else
+      rc = OFDIS_ERR_UNSUPPORTED;
+    if (rc) return rc;
+    *width = img.w;
+    *height = img.h;
+    if (!pixels) return OFDIS_OK;
+    if (capacity < img.px.size()) return OFDIS_ERR_INVALID_ARGUMENT;
+    std::memcpy(pixels, img.px.data(), img.px.size());
+    return OFDIS_OK;
+  } catch (const std::bad_alloc &) {
+    return OFDIS_ERR_OUT_OF_MEMORY;
+  } catch (...) {
+    return OFDIS_ERR_IO;
+  }
 }
 
 }  // extern "C"

@@ -65,6 +65,8 @@ struct PatchArgs {
   float dp_thresh_sq, dr_thresh, res_thresh, outlierthresh;
   int camlr;
   int wave_per_patch;                         // 1: force the one-wave-per-patch kernel (A/B testing)
+  int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
+                                              // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;
 };
 
@@ -99,10 +101,7 @@ struct TvArgs {
   int camlr;
   int sor_generic;             // force the generic global-memory SOR wavefront (A/B testing)
   int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
-  int sor_rows;                // sweep-per-wave SOR rows per lane: 0 auto, 1/2/4/8 forced (A/B testing)
   int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
-  int sor_lean;                // sweep-per-wave SOR, one row per lane: lean form (SorLane) vs SorWave (A/B)
-  int sys_fused;               // system + SOR in one launch (k_tv_sys_sor) where it applies
   int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3)
   int smsys;                   // smoothness + system in one launch (k_tv_smsys)
 };
@@ -138,12 +137,7 @@ void launch_tv_system(const TvArgs &a, hipStream_t s);
 bool tv_smsys_ok(const TvArgs &a);
 void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
-bool tv_sys_sor_fusable(const TvArgs &a);
-void launch_tv_sys_sor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
-// Whole refinement level in one launch per frame (k_tv_level); only when tv_level_fusable(a).
-bool tv_level_fusable(const TvArgs &a);
-void launch_tv_level(const TvArgs &a, int n_inner, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);
 
 }  // namespace ofdis

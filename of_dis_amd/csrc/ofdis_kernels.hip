@@ -452,6 +452,10 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  if (a.stage == 1) {  // timing diagnostic "pconst": construction only; one store keeps the work alive
+    if (lane == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[JM - 1];
+    return;
+  }
   // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
   float pin0 = 0.0f, pin1 = 0.0f;
   if (a.prev) {
@@ -459,6 +463,10 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
     const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
     pin0 = pv[0] * 2;
     if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  if (a.stage == 2) {  // "pconst + pinit": construction and initialisation
+    if (lane == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[JM - 1] + pin0 + pin1;
+    return;
   }
   // ---- OptimizeStart (patch.cpp:117-154)
   float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
@@ -623,6 +631,10 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  if (a.stage == 1) {  // timing diagnostic "pconst": construction only; one store keeps the work alive
+    if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1];
+    return;
+  }
   // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
   float pin0 = 0.0f, pin1 = 0.0f;
   if (a.prev) {
@@ -630,6 +642,10 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
     const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
     pin0 = pv[0] * 2;
     if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  if (a.stage == 2) {  // "pconst + pinit": construction and initialisation
+    if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1] + pin0 + pin1;
+    return;
   }
   const float *Bimg = a.img_b + f * fs;
   const long rowstep = (long)W * noc;
@@ -948,11 +964,6 @@ __device__ __forceinline__ void tv_prep_store(const TvArgs &a, int x, int y, int
     a.t[q] = v[3 + ch];
     a.dt[q] = v[3 + a.noc + ch];
   }
-}
-__device__ __forceinline__ void tv_prep_px(const TvArgs &a, int x, int y, int f) {
-  float v[9];
-  tv_prep_values(a, x, y, f, v);
-  tv_prep_store(a, x, y, f, v);
 }
 
 // Row-major <-> skewed conversions run on 64 x 16 pixel tiles transposed through LDS: the row-major side
@@ -1645,12 +1656,6 @@ __device__ __forceinline__ float dpp_from_next_lane(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
 }
 
-// A register move the compiler cannot look through (see SorWave::step): an identity DPP quad permutation,
-// an ordinary VALU op for the wait-count pass (it waits only for its own operand).
-__device__ __forceinline__ float opaque_mov(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xE4, 0xF, 0xF, true));
-}
-
 // Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later (register ring).
 struct SorPix {
   float i11, i12, i22, b1, b2, hl, hr, vv, vt;
@@ -1918,173 +1923,6 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_pipe(TvArgs a) {
   for (int t = 0; t < TU; t += P::U) st.template steps<0>(t);
 }
 
-// Sweep-per-wave exact-order SOR.  Same wavefront as SorPipe (pixel (x, y) of sweep s at step
-// t = x + y + 2 s), but the S sweeps run on S different waves of the workgroup: wave (g, s) owns rows
-// 64 g .. 64 g + 63 of sweep s.  Per step every wave computes ONE pixel per lane and publishes
-// (u, v, sv) in an LDS ring of depth 3 (steps t, t-1, t-2); the wave of sweep s+1 reads its own / right /
-// bottom "old" values there, every wave reads its top neighbour there (lane y-1 of any row group), and its
-// left neighbour is its own result of step t-1.  Sweep 0 reads the old values from global memory (the
-// values of the previous SOR call, never yet overwritten: the last sweep writes pixel (x, y) at step
-// x + y + 2 (S-1) > every read of it).  One barrier per step.  Splitting the sweeps over waves shortens
-// the per-step critical path S-fold and fills S times more SIMDs.  Arithmetic and order as SorPipe:
-// bit-identical.  MODE 0: OF block SOR (2x2 inverse precomputed), 2: DE point SOR.
-template <int S, int MODE, bool FIRST, bool LAST, int R>
-struct SorWave {
-  struct Ld {
-    float4 c0, c1;
-    float ou, ov, ru, rv, bu, bv;
-  };
-  Ld L[2][R];
-  float pu[R], pv[R], phr[R], pvv[R];  // own results / sh / sv of step t-1 (left and, for r > 0, top)
-  const float4 *C;
-  float *du, *dv;
-  float4 *ring_s;              // [3][NR] this sweep's results (entry y + 1 for row y)
-  const float4 *ring_p;        // [3][NR] previous sweep's results (s >= 1)
-  int w, h, y0, s, NR, wrap;   // rows y0 .. y0 + R - 1
-  unsigned dump;
-  float omega;
-
-  __device__ __forceinline__ void load(int t, Ld (&B)[R]) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int y = y0 + r;
-      const int x = t - y - 2 * s;
-      const bool in = y < h && x >= 0 && x < w;
-      const unsigned here = (unsigned)(skrow(t - 2 * s, w, wrap) * h + y);
-      const unsigned next = (unsigned)(skrow(t - 2 * s + 1, w, wrap) * h + y);  // diagonal + 1
-      const unsigned o = in ? here : dump;
-      if (MODE == 0) {
-        B[r].c0 = C[2 * o];
-        B[r].c1 = C[2 * o + 1];
-      } else {
-        B[r].c0 = C[o];
-      }
-      if (FIRST) {
-        B[r].ou = du[o];
-        const unsigned orr = in && x + 1 < w ? next : dump;
-        B[r].ru = du[orr];
-        const unsigned ob = in && y < h - 1 ? next + 1 : dump;
-        B[r].bu = du[ob];
-        if (MODE == 0) {
-          B[r].ov = dv[o];
-          B[r].rv = dv[orr];
-          B[r].bv = dv[ob];
-        }
-      }
-    }
-  }
-
-  template <int Q, bool PREF>
-  __device__ __forceinline__ void step(const int t) {
-    Ld (&B)[R] = L[Q];
-    const int m1 = (t + 2) % 3, m2 = (t + 1) % 3, m0 = t % 3;  // ring slots of steps t-1, t-2, t
-    float i11[R], i12[R], i22[R], b1[R], b2[R], hr[R], vv[R];
-    float ou[R], ov[R], ru[R], rv[R], bu[R], bv[R];
-    // The prefetched values are moved out of the load buffers by opaque register moves before the next
-    // prefetch is issued into them: the buffers' old and new values then never overlap, so the register
-    // allocator keeps each buffer in the same registers across the loop back-edge and the loads stay in
-    // flight there (a back-edge copy would have to wait for them).
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (MODE == 0) {
-        i11[r] = opaque_mov(B[r].c0.x); i12[r] = opaque_mov(B[r].c0.y); i22[r] = opaque_mov(B[r].c0.w);
-        b1[r] = opaque_mov(B[r].c1.x); b2[r] = opaque_mov(B[r].c1.y); hr[r] = opaque_mov(B[r].c1.z);
-        vv[r] = opaque_mov(B[r].c1.w);
-      } else {
-        i11[r] = opaque_mov(B[r].c0.x); b1[r] = opaque_mov(B[r].c0.y); hr[r] = opaque_mov(B[r].c0.z);
-        vv[r] = opaque_mov(B[r].c0.w);
-        i12[r] = i22[r] = b2[r] = 0.0f;
-      }
-      if (FIRST) {
-        ou[r] = opaque_mov(B[r].ou); ru[r] = opaque_mov(B[r].ru); bu[r] = opaque_mov(B[r].bu);
-        ov[r] = MODE == 0 ? opaque_mov(B[r].ov) : 0.0f; rv[r] = MODE == 0 ? opaque_mov(B[r].rv) : 0.0f;
-        bv[r] = MODE == 0 ? opaque_mov(B[r].bv) : 0.0f;
-      } else {
-        const int e = y0 + r + 1;
-        const float4 o4 = ring_p[m2 * NR + e], r4 = ring_p[m1 * NR + e], b4 = ring_p[m1 * NR + e + 1];
-        ou[r] = o4.x; ov[r] = o4.y; ru[r] = r4.x; rv[r] = r4.y; bu[r] = b4.x; bv[r] = b4.y;
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (PREF) load(t + 2, B);
-    const float4 t4 = ring_s[m1 * NR + y0];   // row y0 - 1 (previous lane / row group) at step t-1
-    float nu[R], nv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int y = y0 + r;
-      const bool has_top = y > 0, has_bot = y < h - 1, notop = !has_top, border = notop || !has_bot;
-      const int x = t - y - 2 * s;
-      // top neighbour (x, y-1) after this sweep, and its sv: the lane's own row r-1 of step t-1 for r > 0
-      const float tu = r == 0 ? t4.x : pu[r > 0 ? r - 1 : 0];
-      const float tv = r == 0 ? t4.y : pv[r > 0 ? r - 1 : 0];
-      const float tsv = r == 0 ? t4.z : pvv[r > 0 ? r - 1 : 0];
-      const float hl = x > 0 ? phr[r] : 0.0f;
-      const float vt = has_top ? tsv : 0.0f;
-      const float ur = x < w - 1 ? ru[r] : 0.0f;
-      nv[r] = 0.0f;
-      if (MODE == 0) {
-        const float vr = x < w - 1 ? rv[r] : 0.0f;
-        const float s1 = sor_rhs(border, notop, b1[r], hr[r] * ur, vt * tu, vv[r] * bu[r]);
-        const float s2 = sor_rhs(border, notop, b2[r], hr[r] * vr, vt * tv, vv[r] * bv[r]);
-        const float B1 = x > 0 ? hl * pu[r] + s1 : s1;
-        const float B2 = x > 0 ? hl * pv[r] + s2 : s2;
-        nu[r] = ou[r] + omega * (i11[r] * B1 + i12[r] * B2 - ou[r]);
-        nv[r] = ov[r] + omega * (i12[r] * B1 + i22[r] * B2 - ov[r]);
-      } else {
-        float su = 0.0f, sd = 0.0f;
-        su = has_top ? su - vt * tu : su;           sd = has_top ? sd + vt : sd;
-        su = x > 0 ? su - hl * pu[r] : su;          sd = x > 0 ? sd + hl : sd;
-        su = has_bot ? su - vv[r] * bu[r] : su;     sd = has_bot ? sd + vv[r] : sd;
-        su = x < w - 1 ? su - hr[r] * ur : su;      sd = x < w - 1 ? sd + hr[r] : sd;
-        const float A = i11[r] + sd, Bv = b1[r] - su;
-        nu[r] = (1.0f - omega) * ou[r] + omega * (Bv / A);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int y = y0 + r;
-      ring_s[m0 * NR + y + 1] = make_float4(nu[r], nv[r], vv[r], 0.0f);
-      if (LAST) {
-        const int x = t - y - 2 * s;
-        const unsigned o = y < h && x >= 0 && x < w ? (unsigned)(skrow(t - 2 * s, w, wrap) * h + y) : dump;
-        du[o] = nu[r];
-        if (MODE == 0) dv[o] = nv[r];
-      }
-      pu[r] = nu[r];
-      pv[r] = nv[r];
-      phr[r] = hr[r];
-      pvv[r] = vv[r];
-    }
-    __syncthreads();
-  }
-
-  // U steps with the prefetch distance 2 kept inside the block: no load is in flight across the loop's
-  // back-edge (a loop-carried in-flight register forces a wait or a copy there), at the price of one
-  // exposed load latency per block.
-  template <int J, int U>
-  __device__ __forceinline__ void block(const int t) {
-    step<J & 1, (J + 2 < U)>(t + J);
-    if constexpr (J + 1 < U) block<J + 1, U>(t);
-  }
-
-  __device__ __forceinline__ void run(int T) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) pu[r] = pv[r] = phr[r] = pvv[r] = 0.0f;
-    constexpr int U = 8;
-    int t = 0;
-    for (; t + U <= T; t += U) {
-      load(t, L[0]);
-      load(t + 1, L[1]);
-      block<0, U>(t);
-    }
-    for (; t < T; t += 2) {  // T is even
-      load(t, L[0]);
-      load(t + 1, L[1]);
-      block<0, 2>(t);
-    }
-  }
-};
-
 // Skewed row of anti-diagonal d for a wave-uniform d (SALU only).  Diagonals outside the frame map to a row
 // inside the plane: every lane reading it is outside the frame (its value is never used), and with the
 // 64 dump slots after the rows even lanes beyond h stay inside the plane.
@@ -2097,7 +1935,15 @@ __device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-// Lean form of the sweep-per-wave SOR (one row per lane), same schedule and arithmetic as SorWave:
+// Sweep-per-wave exact-order SOR, one row per lane.  Same wavefront as SorPipe (pixel (x, y) of sweep s at
+// step t = x + y + 2 s), but the S sweeps run on S different waves of the workgroup: wave (g, s) owns rows
+// 64 g .. 64 g + 63 of sweep s.  Per step every wave computes ONE pixel per lane and publishes its values
+// in LDS rings of depth 3 (steps t, t-1, t-2); the wave of sweep s+1 reads its own / right / bottom "old"
+// values there, every wave reads its top neighbour there, and its left neighbour is its own result of
+// step t-1.  Sweep 0 reads the old values from global memory (the previous SOR call's, never yet
+// overwritten: the last sweep writes pixel (x, y) at step x + y + 2 (S-1) > every read of it).  One
+// barrier per step.  Arithmetic and order as SorPipe: bit-identical.  MODE 0: OF block SOR (2x2 inverse
+// precomputed), 2: DE point SOR.  The form is lean:
 //  * addresses are a wave-uniform base (SALU: skewed row of the step's diagonal) plus a per-lane constant:
 //    no per-step vector address arithmetic; lanes outside the frame read real plane slots (sor_row) and
 //    only the stores are masked;
@@ -2343,354 +2189,10 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
   }
 }
 
-// ---------------------------------------------------------------------------------- fused system + SOR
-// One TV inner iteration's system AND its exact-order SOR in one launch, one workgroup per frame
-// (refine_variational.cpp:195-208): per row group g, one producer wave computes the system of diagonal t
-// at step t (sys_compute: the same function k_tv_system uses, hence the same bits) into an LDS ring of
-// coefficients, and S sweep waves run the SorLane schedule one step behind it (sweep s on diagonal
-// t - 1 - 2 s), reading their coefficients from that ring.  The coefficients never leave the CU: the 64
-// B/pixel of coefficient writes and re-reads of the two-kernel form, and one launch per iteration, are
-// gone.  Ring depth 6 covers a diagonal's life from its producer step to the last sweep's read (S <= 3);
-// G <= 2 row groups (h <= 128) keep every LDS offset a compile-time constant.
-
-// Producer: gathers one pixel's system inputs two steps ahead (3 buffers) with wave-uniform row bases.
-template <int MODE>
-struct SysProducer {
-  static constexpr int NOP = MODE == 0 ? 2 : 1;
-  struct In {
-    float s5[5], x5[5], y5[5];
-    float m, u, v;
-    float d[8];  // Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz
-  };
-  In P0, P1, P2;
-  template <int I>
-  __device__ __forceinline__ In &buf() {
-    if constexpr (I == 0) return P0;
-    else if constexpr (I == 1) return P1;
-    else return P2;
-  }
-  const float *S, *WX, *WY, *M, *DU, *DV, *D[8];
-  int y, yu, h, lim, rmax;
-
-  __device__ __forceinline__ void load(int e, In &B) {
-    const unsigned rc = (unsigned)sor_row2(e, lim, rmax) * (unsigned)h;
-    const unsigned rl = (unsigned)sor_row2(e - 1, lim, rmax) * (unsigned)h;
-    const unsigned rr = (unsigned)sor_row2(e + 1, lim, rmax) * (unsigned)h;
-    const unsigned i5[5] = {rc + (unsigned)y, rl + (unsigned)y, rr + (unsigned)y, rl + (unsigned)yu,
-                            rr + (unsigned)y + 1};
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      B.s5[k] = S[i5[k]];
-      B.x5[k] = WX[i5[k]];
-      B.y5[k] = NOP == 2 ? WY[i5[k]] : 0.0f;
-    }
-    B.m = M[i5[0]];
-    B.u = DU[i5[0]];
-    B.v = NOP == 2 ? DV[i5[0]] : 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) B.d[k] = D[k][i5[0]];
-  }
-  __device__ __forceinline__ void compute(const TvArgs &a, int e, const In &B, float4 &c0, float4 &c1) {
-    const float lIx[1] = {B.d[0]}, lIy[1] = {B.d[1]}, lIz[1] = {B.d[2]}, lIxx[1] = {B.d[3]};
-    const float lIxy[1] = {B.d[4]}, lIyy[1] = {B.d[5]}, lIxz[1] = {B.d[6]}, lIyz[1] = {B.d[7]};
-    sys_compute<NOP, 1>(a, e - y, y, B.s5, B.x5, B.y5, B.m, B.u, B.v, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz,
-                        lIyz, c0, c1);
-  }
-};
-
-template <int S, int MODE, int G>
-struct SysSor {
-  static constexpr int NR = 64 * G + 2;  // ring entries: row y at y + 1, rows -1 and 64 G are halos
-  static constexpr int U = 6;
-  struct Ring {
-    float4 c[6][2][NR];  // coefficients of diagonal d in slot d mod 6: c0, c1
-    f2v uv[S][NR][3];    // sweep results (u, v), slot = step mod 3
-    float sv[NR][3];     // sweep 2's own sv, slot = step mod 3: the coefficient slot of the diagonal above
-                         // (d - 1) is refilled by the producer in the very step sweep 2 would read it
-  };
-};
-
-template <int S, int MODE, int G, int SI>
-struct SysSorLane {
-  static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
-  static constexpr int NR = SysSor<S, MODE, G>::NR;
-  using Ring = typename SysSor<S, MODE, G>::Ring;
-  struct Ld {
-    f2v o, b;  // sweep 0: old (u, v) of the pixel and of the one below (the right one: next step's o)
-  };
-  Ld L0, L1, L2;
-  template <int I>
-  __device__ __forceinline__ Ld &buf() {
-    if constexpr (I == 0) return L0;
-    else if constexpr (I == 1) return L1;
-    else return L2;
-  }
-  f2v pp;
-  float phr;
-  const float *du_r, *dv_r;
-  float *du, *dv;
-  Ring *R;
-  int e;  // ring entry of this lane's row
-  int w, h, y, lim, rmax;
-  bool border, notop;
-  float omega;
-
-  __device__ __forceinline__ void load(int t, Ld &B) {
-    if (!FIRST) return;
-    const int d = t - 1;
-    const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)h;
-    const unsigned r1 = (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)h;
-    float ov = 0.0f, bv = 0.0f;
-    if (MODE == 0) {
-      ov = dv_r[r0 + (unsigned)y];
-      bv = dv_r[r1 + (unsigned)y + 1];
-    }
-    B.o = f2v{du_r[r0 + (unsigned)y], ov};
-    B.b = f2v{du_r[r1 + (unsigned)y + 1], bv};
-  }
-
-  template <int J>
-  __device__ __forceinline__ void step(const int t) {
-    constexpr int m0 = J % 3, m1 = (J + 2) % 3, m2 = (J + 1) % 3;  // (u, v) ring slots of steps t, t-1, t-2
-    constexpr int cs = ((J - 1 - 2 * SI) % 6 + 6) % 6;            // coefficient slot of this diagonal
-    constexpr int ct = (cs + 5) % 6;                               // ... of the diagonal before
-    Ld &B = buf<J % 3>();
-    const Ld &Bn = buf<(J + 1) % 3>();
-    load(t + 2, buf<(J + 2) % 3>());
-    const int d = t - 1 - 2 * SI;
-    const int xp = d - y;
-    const bool hasl = xp > 0, hasr = xp < w - 1;
-    const float4 c0 = R->c[cs][0][e], c1 = R->c[cs][1][e];
-    f2v o, r, bt;
-    if (FIRST) {
-      o = B.o; r = Bn.o; bt = B.b;
-    } else {
-      o = R->uv[SI - 1][e][m2]; r = R->uv[SI - 1][e][m1]; bt = R->uv[SI - 1][e + 1][m1];
-    }
-    const f2v tp = R->uv[SI][e - 1][m1];  // row y - 1 at step t-1 (entry 0: zero)
-    f2v nw;
-    float vv;
-    if (MODE == 0) {
-      const float tsv = SI >= 2 ? R->sv[e - 1][m1] : R->c[ct][1][e - 1].w;  // sv of (x, y - 1)
-      const float hr = c1.z;
-      vv = c1.w;
-      const f2v bb = f2v{c1.x, c1.y};
-      const f2v rr = hasr ? r : f2v{0.0f, 0.0f};
-      const f2v X = hr * rr, Y = tsv * tp, Z = vv * bt;
-      const f2v l = X + (border ? bb : Y);
-      const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Y) : Z);
-      const f2v sr = l + rg;
-      const f2v Bv = hasl ? phr * pp + sr : sr;
-      const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;
-      nw = o + omega * ((m_1 + m_2) - o);
-      phr = hr;
-    } else {
-      const float tsv = SI >= 2 ? R->sv[e - 1][m1] : R->c[ct][0][e - 1].w;
-      const float a11 = c0.x, b1 = c0.y, hr = c0.z;
-      vv = c0.w;
-      const bool has_top = !notop, has_bot = !(border && has_top);
-      const float tu = tp.x, ur = hasr ? r.x : 0.0f, hl = phr;
-      float su = 0.0f, sd = 0.0f;
-      su = has_top ? su - tsv * tu : su;   sd = has_top ? sd + tsv : sd;
-      su = hasl ? su - hl * pp.x : su;     sd = hasl ? sd + hl : sd;
-      su = has_bot ? su - vv * bt.x : su;  sd = has_bot ? sd + vv : sd;
-      su = hasr ? su - hr * ur : su;       sd = hasr ? sd + hr : sd;
-      const float A = a11 + sd, Bq = b1 - su;
-      nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
-      phr = hr;
-    }
-    R->uv[SI][e][m0] = nw;
-    if (SI >= 2) R->sv[e][m0] = vv;
-    if (LAST) {
-      if ((unsigned)xp < (unsigned)w && y < h) {
-        const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)h;
-        du[r0 + (unsigned)y] = nw.x;
-        if (MODE == 0) dv[r0 + (unsigned)y] = nw.y;
-      }
-    }
-    pp = nw;
-    __syncthreads();
-  }
-  template <int J>
-  __device__ __forceinline__ void block(const int t) {
-    step<J>(t + J);
-    if constexpr (J + 1 < 6) block<J + 1>(t);
-  }
-  // active diagonals [y0, ymax + w - 1] -> steps [y0 + 1 + 2 SI, ymax + w + 2 SI]
-  __device__ __forceinline__ void run(int T, int y0, int ymax) {
-    pp = f2v{0.0f, 0.0f};
-    phr = 0.0f;
-    const int ta = (y0 + 1 + 2 * SI) / 6 * 6;
-    const int tb = min(T, (ymax + w + 2 * SI) / 6 * 6 + 6);
-    for (int t = 0; t < ta; ++t) __syncthreads();
-    load(ta, L0);
-    load(ta + 1, L1);
-    for (int t = ta; t < tb; t += 6) block<0>(t);
-    for (int t = tb; t < T; ++t) __syncthreads();
-  }
-};
-
-template <int S, int MODE, int G>
-struct SysProdLane {
-  using Ring = typename SysSor<S, MODE, G>::Ring;
-  SysProducer<MODE> P;
-  Ring *R;
-  int e;
-  template <int J>
-  __device__ __forceinline__ void step(const TvArgs &a, const int t) {
-    auto &B = P.template buf<J % 3>();
-    float4 c0, c1;
-    P.compute(a, t, B, c0, c1);
-    P.load(t + 2, P.template buf<(J + 2) % 3>());
-    R->c[J][0][e] = c0;
-    R->c[J][1][e] = c1;
-    __syncthreads();
-  }
-  template <int J>
-  __device__ __forceinline__ void block(const TvArgs &a, const int t) {
-    step<J>(a, t + J);
-    if constexpr (J + 1 < 6) block<J + 1>(a, t);
-  }
-  // active diagonals [y0, ymax + w - 1] (diagonal t at step t)
-  __device__ __forceinline__ void run(const TvArgs &a, int T, int y0, int ymax) {
-    const int ta = y0 / 6 * 6;
-    const int tb = min(T, (ymax + a.w - 1) / 6 * 6 + 6);
-    for (int t = 0; t < ta; ++t) __syncthreads();
-    P.load(ta, P.P0);
-    P.load(ta + 1, P.P1);
-    for (int t = ta; t < tb; t += 6) block<0>(a, t);
-    for (int t = tb; t < T; ++t) __syncthreads();
-  }
-};
-
-template <int S, int MODE, int G>
-__global__ __launch_bounds__(64 * G * (S + 1)) void k_tv_sys_sor(TvArgs a) {
-  using Ring = typename SysSor<S, MODE, G>::Ring;
-  __shared__ Ring ring;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int g = wid / (S + 1), role = wid - g * (S + 1);
-  {
-    float *z = reinterpret_cast<float *>(&ring);
-    for (int i = threadIdx.x; i < (int)(sizeof(Ring) / 4); i += blockDim.x) z[i] = 0.0f;
-  }
-  __syncthreads();
-  const int frame = blockIdx.x;
-  const long fo = (long)frame * a.sp;
-  const int T = ((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 2 + 5) / 6 * 6;  // + 1: sweeps run a step behind
-  const int y0 = g * 64, ymax = min(y0 + 63, a.h - 1);
-  const int y = y0 + lane;
-  const int lim = a.wrap ? a.w : 1 << 30, rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
-  if (role == S) {
-    SysProdLane<S, MODE, G> pr;
-    pr.R = &ring;
-    pr.e = y + 1;
-    SysProducer<MODE> &P = pr.P;
-    P.S = a.s + fo; P.WX = a.wxs + fo; P.WY = a.wys + fo; P.M = a.mask + fo; P.DU = a.du + fo; P.DV = a.dv + fo;
-    P.D[0] = a.Ix + fo; P.D[1] = a.Iy + fo; P.D[2] = a.Iz + fo; P.D[3] = a.Ixx + fo;
-    P.D[4] = a.Ixy + fo; P.D[5] = a.Iyy + fo; P.D[6] = a.Ixz + fo; P.D[7] = a.Iyz + fo;
-    P.y = y; P.yu = y > 0 ? y - 1 : 0; P.h = a.h; P.lim = lim; P.rmax = rmax;
-    pr.run(a, T, y0, ymax);
-    return;
-  }
-  auto sweep = [&](auto &st) {
-    st.du_r = a.du + fo; st.dv_r = a.dv + fo; st.du = a.du + fo; st.dv = a.dv + fo;
-    st.R = &ring; st.e = y + 1;
-    st.w = a.w; st.h = a.h; st.y = y; st.lim = lim; st.rmax = rmax;
-    st.notop = y == 0;
-    st.border = y == 0 || y >= a.h - 1;
-    st.omega = a.omega;
-    st.run(T, y0, ymax);
-  };
-  if (role == 0) {
-    SysSorLane<S, MODE, G, 0> st;
-    sweep(st);
-  } else if (role == 1) {
-    SysSorLane<S, MODE, G, (S > 1 ? 1 : 0)> st;
-    sweep(st);
-  } else {
-    SysSorLane<S, MODE, G, (S > 2 ? 2 : 0)> st;
-    sweep(st);
-  }
-}
-
-template <int S, int MODE>
-static void sys_sor_s(const TvArgs &a, hipStream_t s) {
-  if (a.h <= 64)
-    k_tv_sys_sor<S, MODE, 1><<<a.n, 64 * (S + 1), 0, s>>>(a);
-  else
-    k_tv_sys_sor<S, MODE, 2><<<a.n, 128 * (S + 1), 0, s>>>(a);
-}
-
-// Rows per lane of the sweep-per-wave SOR.  One row per lane and more waves measured faster than 2 or 4
-// rows per lane and fewer waves (1080p op2: 0.76 vs 0.91 ms per step), so 1 is the default; `forced`
-// (option "sor_rows") selects 2 or 4 for A/B runs.
-__host__ __device__ __forceinline__ int sor_rows_per_lane(int h, int forced) {
-  (void)h;
-  return forced > 0 ? forced : 1;
-}
-
-// One frame's SOR call by the whole workgroup (64 * G * S threads, G = ceil(h / (64 R))); ring: S * 3 * NR
-// float4 of LDS.
-template <int S, int MODE, int R>
-__device__ __forceinline__ void sor_waves_frame(const TvArgs &a, int frame, float4 *ring) {
-  const int G = (a.h + 64 * R - 1) / (64 * R);
-  const int NR = G * 64 * R + 2;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int g = wid / S, s = wid - g * S;
-  // clear the rings: pads and not-yet-written slots are read only by lanes whose selects discard the
-  // values, but they are kept finite and deterministic anyway
-  for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) ring[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-  const long fo = (long)frame * a.sp;
-  const int T2 = (((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1) + 1) & ~1;  // step count, even
-  auto setup = [&](auto &st) {
-    st.C = reinterpret_cast<const float4 *>(a.coef) + fo * (MODE == 0 ? 2 : 1);
-    st.du = a.du + fo;
-    st.dv = a.dv + fo;
-    st.ring_s = ring + s * 3 * NR;
-    st.ring_p = ring + (s > 0 ? s - 1 : 0) * 3 * NR;
-    st.w = a.w; st.h = a.h; st.y0 = (g * 64 + lane) * R; st.s = s; st.NR = NR;
-    st.wrap = a.wrap;
-    st.dump = (unsigned)(a.skew_slots + lane);
-    st.omega = a.omega;
-    st.run(T2);
-  };
-  if (s == 0) {
-    SorWave<S, MODE, true, S == 1, R> st;
-    setup(st);
-  } else if (s == S - 1) {
-    SorWave<S, MODE, false, true, R> st;
-    setup(st);
-  } else {
-    SorWave<S, MODE, false, false, R> st;
-    setup(st);
-  }
-}
-
-template <int S, int MODE, int R, int MAXT>
-__global__ __launch_bounds__(MAXT) void k_tv_sor_waves(TvArgs a) {
-  extern __shared__ float4 ring[];  // [S][3][NR]
-  sor_waves_frame<S, MODE, R>(a, blockIdx.x, ring);
-}
-
 template <int S, int MODE, int NB, int MAXT, bool CRING>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
   sor_lanes_frame<S, MODE, NB, CRING ? sor_crn(S, MAXT) : 0>(a, blockIdx.x, ring_uv);
-}
-
-__device__ __forceinline__ void tv_final_px(const TvArgs &a, int x, int y, int f) {
-  const long plane = (long)a.w * a.h;
-  const long o = (long)y * a.w + x;
-  const long fk = (long)f * a.sp + skw(x, y, a.h, a.w, a.wrap);
-  float *WX = a.flow + (long)f * a.nop * plane;
-  if (a.nop == 2) {
-    WX[o] = a.wxs[fk] + a.du[fk];
-    WX[plane + o] = a.wys[fk] + a.dv[fk];
-  } else {
-    const float s = a.wxs[fk] + a.du[fk];
-    WX[o] = a.camlr == 0 ? ssemin(s, 0.0f) : ssemax(s, 0.0f);
-  }
 }
 
 template <int TH>
@@ -2722,40 +2224,6 @@ __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
     WX[o] = sm[0][yl][tx];
     if (a.nop == 2) WX[plane + o] = sm[1][yl][tx];
   }
-}
-
-// One whole refinement level per frame in ONE launch (refine_variational.cpp:152-342): warp + derivatives,
-// then tv_innerit * (level + 1) x [smoothness, system, exact-order SOR], then the flow update.  The
-// workgroup is the sweep-per-wave SOR's (64 * ceil(h/64) * S threads); the data-parallel phases loop over
-// the frame's skewed planes with all its threads, phases are separated by workgroup barriers, and the
-// frame's planes stay in the XCD's L2 / the Infinity Cache between phases.  Same per-pixel functions as
-// the one-phase-per-launch path: bit-identical.
-template <int S, int MODE, int MAXT>
-__global__ __launch_bounds__(MAXT) void k_tv_level(TvArgs a, int n_inner) {
-  extern __shared__ float4 ring[];
-  constexpr int NOP = MODE == 0 ? 2 : 1;
-  const int f = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const int w = a.w, h = a.h, sp = (int)a.sp;
-  for (int p = tid; p < w * h; p += nt) tv_prep_px(a, p % w, p / w, f);
-  __syncthreads();
-  for (int c = 0; c < a.noc; ++c)
-    for (int kk = tid; kk < sp; kk += nt) tv_deriv1_px(a, (long)f * a.noc + c, kk);
-  __syncthreads();
-  for (int c = 0; c < a.noc; ++c)
-    for (int kk = tid; kk < sp; kk += nt) tv_deriv2_px(a, (long)f * a.noc + c, kk);
-  __syncthreads();
-  for (int it = 0; it < n_inner; ++it) {
-    for (int kk = tid; kk < sp; kk += nt) tv_smooth_px<NOP>(a, f, kk, it == 0);
-    __syncthreads();
-    if (a.noc == 1)
-      for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP, 1>(a, f, kk);
-    else
-      for (int kk = tid; kk < sp; kk += nt) tv_system_px<NOP, 3>(a, f, kk);
-    __syncthreads();
-    sor_waves_frame<S, MODE, 1>(a, f, ring);
-    __syncthreads();
-  }
-  for (int p = tid; p < w * h; p += nt) tv_final_px(a, p % w, p / w, f);
 }
 
 // ------------------------------------------------------------------------------------------------ output
@@ -3061,60 +2529,42 @@ static void sor_pipe(const TvArgs &a, hipStream_t s) {
       k_tv_sor_pipe<S, 2, 1024><<<a.n, threads, 0, s>>>(a);
   }
 }
-// MAXT: 512 threads leave 256 registers a lane (R = 2, 4 need them); R = 1 also runs up to 1024 threads.
-template <int S, int R, int MAXT>
-static void sor_waves_r(const TvArgs &a, hipStream_t s) {
-  const int G = (a.h + 64 * R - 1) / (64 * R);
-  const size_t lds = sizeof(float4) * S * 3 * (G * 64 * R + 2);
-  if (R == 1 && a.sor_lean) {
-    const int pd = a.sor_lean;  // prefetch distance: 2, 3 or 5 steps (3, 4 or 6 buffers)
-    constexpr int crn = sor_crn(S, MAXT);
-    const bool cring = crn > 0 && a.sor_cring;
-    const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, a.nop == 2 ? 2 : 1);
-    const int th = 64 * G * S;
-    if (cring) {
-      if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
-      else k_tv_sor_lanes<S, 2, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
-    } else if (a.nop == 2) {
-      if (pd == 5) k_tv_sor_lanes<S, 0, 6, MAXT, false><<<a.n, th, lds, s>>>(a);
-      else if (pd == 3) k_tv_sor_lanes<S, 0, 4, MAXT, false><<<a.n, th, lds, s>>>(a);
-      else k_tv_sor_lanes<S, 0, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
-    } else {
-      if (pd == 5) k_tv_sor_lanes<S, 2, 6, MAXT, false><<<a.n, th, lds, s>>>(a);
-      else if (pd == 3) k_tv_sor_lanes<S, 2, 4, MAXT, false><<<a.n, th, lds, s>>>(a);
-      else k_tv_sor_lanes<S, 2, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
-    }
-    return;
+// Sweep-per-wave SOR (k_tv_sor_lanes): 64 * ceil(h / 64) * S threads, one workgroup per frame.  With S <= 3
+// sweep 0 hands the coefficients to the later sweeps through an LDS ring (option sor_cring, default on).
+template <int S, int MAXT>
+static void sor_lanes(const TvArgs &a, hipStream_t s) {
+  const int G = (a.h + 63) / 64;
+  constexpr int crn = sor_crn(S, MAXT);
+  const bool cring = crn > 0 && a.sor_cring;
+  const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, a.nop == 2 ? 2 : 1);
+  const int th = 64 * G * S;
+  if (cring) {
+    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
+    else k_tv_sor_lanes<S, 2, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
+  } else {
+    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
+    else k_tv_sor_lanes<S, 2, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
   }
-  if (a.nop == 2)
-    k_tv_sor_waves<S, 0, R, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
-  else
-    k_tv_sor_waves<S, 2, R, MAXT><<<a.n, 64 * G * S, lds, s>>>(a);
 }
 template <int S>
-static void sor_waves(const TvArgs &a, hipStream_t s) {
-  switch (sor_rows_per_lane(a.h, a.sor_rows)) {
-    case 1:
-      if (64 * S * ((a.h + 63) / 64) <= 512)
-        sor_waves_r<S, 1, 512>(a, s);
-      else
-        sor_waves_r<S, 1, 1024>(a, s);
-      return;
-    case 2: sor_waves_r<S, 2, 512>(a, s); return;
-    default: sor_waves_r<S, 4, 512>(a, s); return;
-  }
+static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
+  if (64 * S * ((a.h + 63) / 64) <= 512)
+    sor_lanes<S, 512>(a, s);
+  else
+    sor_lanes<S, 1024>(a, s);
 }
+// Exact-order SOR dispatch: the sweep-per-wave form while its S * ceil(h / 64) waves fit one workgroup,
+// the register pipeline (one wave per row group runs all sweeps) for taller levels, the generic
+// global-memory wavefront for the point SOR of the OpenMP build and degenerate sizes.
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
   const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);  // point SOR (solver.c:34-78)
-  const int R = sor_rows_per_lane(a.h, a.sor_rows), G = (a.h + 64 * R - 1) / (64 * R);
-  const size_t lds = sizeof(float4) * a.solverit * 3 * (G * 64 * R + 2);
-  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 &&
-      G * a.solverit <= (R == 1 ? 16 : 8) && (R == 1 || R == 2 || R == 4) && lds <= 160 * 1024) {
+  const int G = (a.h + 63) / 64;
+  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && G * a.solverit <= 16) {
     switch (a.solverit) {
-      case 2: sor_waves<2>(a, s); return;
-      case 3: sor_waves<3>(a, s); return;
-      case 4: sor_waves<4>(a, s); return;
+      case 2: sor_lanes_s<2>(a, s); return;
+      case 3: sor_lanes_s<3>(a, s); return;
+      case 4: sor_lanes_s<4>(a, s); return;
     }
   }
   if (!tiny && a.h <= 1024 && a.solverit <= 4 && !a.sor_generic) {
@@ -3131,47 +2581,6 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
     k_tv_sor<1><<<a.n, 256, 0, s>>>(a);
   else
     k_tv_sor<0><<<a.n, 256, 0, s>>>(a);
-}
-bool tv_sys_sor_fusable(const TvArgs &a) {
-  return a.sys_fused && a.noc == 1 && (a.solverit == 2 || a.solverit == 3) && a.w >= 2 && a.h >= 2 &&
-         a.h <= 128 && !a.sor_point && !a.sor_generic && a.sor_variant == 0;
-}
-void launch_tv_sys_sor(const TvArgs &a, hipStream_t s) {
-  if (a.nop == 2) {
-    if (a.solverit == 2) sys_sor_s<2, 0>(a, s);
-    else sys_sor_s<3, 0>(a, s);
-  } else {
-    if (a.solverit == 2) sys_sor_s<2, 2>(a, s);
-    else sys_sor_s<3, 2>(a, s);
-  }
-}
-template <int S, int MODE>
-static void tv_level_s(const TvArgs &a, int n_inner, hipStream_t s) {
-  const int G = (a.h + 63) / 64;
-  const int threads = 64 * G * S;
-  const size_t lds = sizeof(float4) * S * 3 * (G * 64 + 2);
-  if (threads <= 256)
-    k_tv_level<S, MODE, 256><<<a.n, threads, lds, s>>>(a, n_inner);
-  else if (threads <= 512)
-    k_tv_level<S, MODE, 512><<<a.n, threads, lds, s>>>(a, n_inner);
-  else
-    k_tv_level<S, MODE, 1024><<<a.n, threads, lds, s>>>(a, n_inner);
-}
-bool tv_level_fusable(const TvArgs &a) {
-  const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);
-  const int G = (a.h + 63) / 64;
-  return !tiny && !a.sor_generic && a.sor_variant == 0 && a.solverit >= 2 && a.solverit <= 4 &&
-         G * a.solverit <= 16;
-}
-void launch_tv_level(const TvArgs &a, int n_inner, hipStream_t s) {
-  switch (a.solverit * 2 + (a.nop == 2 ? 0 : 1)) {
-    case 4: tv_level_s<2, 0>(a, n_inner, s); return;
-    case 5: tv_level_s<2, 2>(a, n_inner, s); return;
-    case 6: tv_level_s<3, 0>(a, n_inner, s); return;
-    case 7: tv_level_s<3, 2>(a, n_inner, s); return;
-    case 8: tv_level_s<4, 0>(a, n_inner, s); return;
-    case 9: tv_level_s<4, 2>(a, n_inner, s); return;
-  }
 }
 void launch_tv_final(const TvArgs &a, hipStream_t s) {
   k_tv_final<32><<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, 32), a.n), 256, 0, s>>>(a);

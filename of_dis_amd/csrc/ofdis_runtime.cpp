@@ -26,8 +26,7 @@ using namespace ofdis;
 namespace {
 
 const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_level",
-                                    "tv_sys_sor"};
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -79,15 +78,9 @@ struct ofdis_context {
     ofdis_params p{};
   } gkey;
   hipGraphExec_t gexec = nullptr;
-  int opt_tv_fused = 0;        // 1: one launch per TV level (k_tv_level) instead of one per phase
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
-  int opt_sor_rows = 0;        // rows per lane of the sweep-per-wave SOR (0 auto)
-  int opt_sys_fused = 0;       // 1: system + SOR in one launch where it applies (k_tv_sys_sor; A/B: the
-                               // producer wave's per-step system latency lengthens the wavefront step ~3x)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
-  int opt_sor_cring = 1;       // lean SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
-  int opt_sor_lean = 2;        // sweep-per-wave SOR, one row per lane: lean SorLane form with this prefetch
-                               // distance (2, 3, 5 steps); 0: SorWave (A/B)
+  int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
@@ -104,6 +97,10 @@ struct ofdis_context {
   };
   std::vector<Lane> lanes;
   hipEvent_t entry = nullptr;
+  // call ordering: ev_null hands the legacy NULL stream's queued work to the context's stream; ev_ws marks
+  // the end of the previous call's use of the workspaces (a call on another stream waits for it)
+  hipEvent_t ev_null = nullptr, ev_ws = nullptr;
+  bool ws_pending = false;
   std::mutex mu;
 };
 
@@ -270,9 +267,20 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad, bool init 
   return P;
 }
 
+// A captured graph bakes in the workspace and lane pointers: drop it before any of them is reallocated.
+int drop_graph(ofdis_context *c) {
+  if (!c->gexec) return OFDIS_OK;
+  HIP_OK(hipDeviceSynchronize());  // it may still run on a caller stream
+  HIP_OK(hipGraphExecDestroy(c->gexec));
+  c->gexec = nullptr;
+  return OFDIS_OK;
+}
+
 int ensure_ws(ofdis_context *c, size_t bytes) {
   if (bytes <= c->ws_cap) return OFDIS_OK;
   if (c->ws) {
+    int rc = drop_graph(c);
+    if (rc) return rc;
     HIP_OK(hipDeviceSynchronize());  // callers may have queued work on their own streams
     HIP_OK(hipFree(c->ws));
     c->ws = nullptr;
@@ -297,7 +305,7 @@ int capture(ofdis_context *c, hipStream_t s, const std::vector<float *> &cap, in
 }
 
 struct StageTimes {
-  double poptim = 0, cflow = 0, tvopt = 0;
+  double pconst = 0, pinit = 0, poptim = 0, cflow = 0, tvopt = 0;
 };
 
 // The coarse-to-fine loop (oflow.cpp:182-330) over device pyramids already in the workspace.
@@ -307,7 +315,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
   const int nop = P.nop, noc = P.noc, n = P.n;
   const int novals = noc * p->p_samp_s * p->p_samp_s;
   const int steps = steps_of(p);
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (times)
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
   for (int sl = p->sc_f; sl >= p->sc_l; --sl) {
@@ -358,6 +366,15 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.camlr = 0;
     pa.wave_per_patch = c->opt_wave_per_patch;
     pa.g = g;
+    if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
+      PatchArgs pd = pa;
+      pd.stage = 1;
+      launch_patch(pd, s);
+      HIP_OK(hipEventRecord(ev[1], s));
+      pd.stage = 2;
+      launch_patch(pd, s);
+      HIP_OK(hipEventRecord(ev[2], s));
+    }
     timed(c, 3, s, [&] { launch_patch(pa, s); });
     // usefbcon: the backward grid -- template on image b, target image a, right camera (camlr = 1),
     // initialised from the coarser backward flow (oflow.cpp:158-169, 193-196, 209-211, 231-233)
@@ -388,7 +405,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     ag.g = g;
     ag.cg_p_iter = P.fb ? pb.p_iter : nullptr;
     ag.cg_pweight = P.fb ? pb.pweight : nullptr;
-    if (times) HIP_OK(hipEventRecord(ev[1], s));
+    if (times) HIP_OK(hipEventRecord(ev[3], s));
     timed(c, 4, s, [&] { launch_aggregate(ag, s); });
     float *flow_bw = (float *)(ws + P.off_flow_bw[i]);
     const bool bw_level = P.fb && sl > p->sc_l;  // the backward flow is not needed after the last scale
@@ -401,7 +418,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       ab.flow = flow_bw;
       timed(c, 4, s, [&] { launch_aggregate(ab, s); });
     }
-    if (times) HIP_OK(hipEventRecord(ev[2], s));
+    if (times) HIP_OK(hipEventRecord(ev[4], s));
     int rc = capture(c, s, c->cap_dis, sl, P, flow);
     if (rc) return rc;
 
@@ -452,51 +469,44 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.camlr = dir;
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
-      tv.sor_rows = c->opt_sor_rows;
-      tv.sor_lean = c->opt_sor_lean;
-      tv.sys_fused = c->opt_sys_fused;
       tv.sor_cring = c->opt_sor_cring;
       tv.smsys = c->opt_smsys;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
-      if (c->opt_tv_fused && tv_level_fusable(tv)) {
-        timed(c, 11, s, [&] { launch_tv_level(tv, n_inner, s); });
-      } else {
-        timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
-        timed(c, 6, s, [&] {
-          launch_tv_deriv1(tv, s);
-          launch_tv_deriv2(tv, s);
-        });
-        for (int it = 0; it < n_inner; ++it) {
-          tv.first_iter = it == 0;
-          if (tv_sys_sor_fusable(tv)) {
-            timed(c, 7, s, [&] { launch_tv_smooth(tv, s); });
-            timed(c, 12, s, [&] { launch_tv_sys_sor(tv, s); });
+      timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
+      timed(c, 6, s, [&] {
+        launch_tv_deriv1(tv, s);
+        launch_tv_deriv2(tv, s);
+      });
+      for (int it = 0; it < n_inner; ++it) {
+        tv.first_iter = it == 0;
+        timed(c, 7, s, [&] {
+          if (tv_smsys_ok(tv)) {
+            launch_tv_smsys(tv, s);
           } else {
-            timed(c, 7, s, [&] {
-              if (tv_smsys_ok(tv)) {
-                launch_tv_smsys(tv, s);
-              } else {
-                launch_tv_smooth(tv, s);
-                launch_tv_system(tv, s);
-              }
-            });
-            timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
+            launch_tv_smooth(tv, s);
+            launch_tv_system(tv, s);
           }
-        }
-        timed(c, 9, s, [&] { launch_tv_final(tv, s); });
+        });
+        timed(c, 8, s, [&] { launch_tv_sor(tv, s); });
       }
+      timed(c, 9, s, [&] { launch_tv_final(tv, s); });
     }
     if (times) {
-      HIP_OK(hipEventRecord(ev[3], s));
-      HIP_OK(hipEventSynchronize(ev[3]));
+      HIP_OK(hipEventRecord(ev[5], s));
+      HIP_OK(hipEventSynchronize(ev[5]));
       StageTimes st;
-      float ms;
-      hipEventElapsedTime(&ms, ev[0], ev[1]);
-      st.poptim = ms;
-      hipEventElapsedTime(&ms, ev[1], ev[2]);
-      st.cflow = ms;
-      hipEventElapsedTime(&ms, ev[2], ev[3]);
-      st.tvopt = ms;
+      float t01, t12, t23, t34, t45;
+      hipEventElapsedTime(&t01, ev[0], ev[1]);
+      hipEventElapsedTime(&t12, ev[1], ev[2]);
+      hipEventElapsedTime(&t23, ev[2], ev[3]);
+      hipEventElapsedTime(&t34, ev[3], ev[4]);
+      hipEventElapsedTime(&t45, ev[4], ev[5]);
+      // the optimisation launch repeats construction and initialisation: poptim is the rest of it
+      st.pconst = t01;
+      st.pinit = std::max(0.0, (double)t12 - t01);
+      st.poptim = std::max(0.0, (double)t23 - t12);
+      st.cflow = t34;
+      st.tvopt = t45;
       times->push_back(st);
     }
     rc = capture(c, s, c->cap_tv, sl, P, flow);
@@ -512,9 +522,9 @@ void print_times(const Plan &P, const std::vector<StageTimes> &t, double total_m
     for (size_t k = 0; k < t.size(); ++k) {
       const int sl = P.sc_f - (int)k;
       const LevelGeom &g = P.lv[sl - P.sc_l];
-      const double all = t[k].poptim + t[k].cflow + t[k].tvopt;
+      const double all = t[k].pconst + t[k].pinit + t[k].poptim + t[k].cflow + t[k].tvopt;
       std::printf("TIME (Sc: %i, #p:%6i, pconst, pinit, poptim, cflow, tvopt, total): %8.2f %8.2f %8.2f %8.2f %8.2f -> %8.2f ms.\n",
-                  sl, g.npatch, 0.0, 0.0, t[k].poptim, t[k].cflow, t[k].tvopt, all);
+                  sl, g.npatch, t[k].pconst, t[k].pinit, t[k].poptim, t[k].cflow, t[k].tvopt, all);
     }
   }
   if (verbosity > 0) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", total_ms);
@@ -647,6 +657,7 @@ void ofdis_context_destroy(ofdis_context *c) {
     hipGraphExecDestroy(c->gexec);
     c->gexec = nullptr;
   }
+  if (c->ws_pending) hipEventSynchronize(c->ev_ws);  // the last call's work, on whatever stream it ran
   if (c->stream) hipStreamSynchronize(c->stream);
   drain_timing(c);
   for (auto e : c->pool) hipEventDestroy(e);
@@ -658,6 +669,8 @@ void ofdis_context_destroy(ofdis_context *c) {
     if (L.s) hipStreamDestroy(L.s);
   }
   if (c->entry) hipEventDestroy(c->entry);
+  if (c->ev_null) hipEventDestroy(c->ev_null);
+  if (c->ev_ws) hipEventDestroy(c->ev_ws);
   for (auto e : c->pipe_ev) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -725,6 +738,8 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
     if (!L.done) HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     if (L.cap < bytes) {
       if (L.ws) {
+        int rc = drop_graph(c);
+        if (rc) return rc;
         HIP_OK(hipDeviceSynchronize());
         HIP_OK(hipFree(L.ws));
         L.ws = nullptr;
@@ -739,24 +754,71 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
 
 int stream_count(const ofdis_context *c, int n) { return c->opt_streams > 0 ? c->opt_streams : (n >= 512 ? 2 : 1); }
 
-// Chunks round-robin over opt_streams streams, each chunk's whole pipeline on one stream ("streams").
-int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
-                    const uint8_t *img_b, const float *init, float *flow_out, int n, int width, int height,
-                    int chunk) {
-  const int nchunks = (n + chunk - 1) / chunk;
-  const int k = std::min(stream_count(c, n), nchunks);
-  Plan PC = batch_plan(p, chunk, width, height, init != nullptr);
-  int rc = ensure_lanes(c, k, PC.total);
+// Frames per launch such that every TV plane group (n * noc * sp floats, addressed with 32-bit byte
+// offsets by the system kernels' ldu) stays below 2^30 floats.
+int tv_frame_cap(const ofdis_params *p, int width, int height) {
+  if (!p->usetvref) return 1 << 30;
+  const Plan P1 = batch_plan(p, 1, width, height);
+  const long per = (long)P1.noc * (long)P1.tv_plane;
+  return (int)std::max(1L, std::min((long)(1 << 30), ((1L << 30) - 1) / per));
+}
+
+// How one call is issued: the whole batch on one stream and workspace (single), chunks round-robin over
+// lanes (round robin), or the two-stream software pipeline.  Everything the issue needs -- workspaces,
+// lane streams, events -- is allocated by prepare(), before any capture begins.
+struct CallPlan {
+  enum Kind { kSingle, kRoundRobin, kPipeline } kind = kSingle;
+  int n = 0, width = 0, height = 0, chunk = 0, nchunks = 1, lanes = 0;
+  bool init = false;
+  Plan whole;               // kSingle
+  std::vector<Plan> parts;  // kRoundRobin / kPipeline: one plan per chunk
+};
+
+int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int height, bool init, bool capturing,
+            CallPlan &cp) {
+  cp.n = n;
+  cp.width = width;
+  cp.height = height;
+  cp.init = init;
+  const int nstreams = stream_count(c, n);
+  int chunk = c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : (n + nstreams - 1) / nstreams;
+  chunk = std::min(chunk, tv_frame_cap(p, width, height));
+  cp.chunk = chunk;
+  cp.nchunks = (n + chunk - 1) / chunk;
+  if (cp.nchunks > 1 && capturing) return OFDIS_ERR_UNSUPPORTED;  // stage capture reads frame 0 of one launch
+  if (cp.nchunks == 1) {
+    cp.kind = CallPlan::kSingle;
+    cp.whole = batch_plan(p, n, width, height, init);
+    return ensure_ws(c, cp.whole.total);
+  }
+  cp.kind = c->opt_pipeline && !c->timing ? CallPlan::kPipeline : CallPlan::kRoundRobin;
+  for (int ch = 0; ch < cp.nchunks; ++ch)
+    cp.parts.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height, init));
+  cp.lanes = cp.kind == CallPlan::kPipeline ? 2 : std::min(nstreams, cp.nchunks);
+  int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total);
   if (rc) return rc;
+  if (cp.kind == CallPlan::kPipeline)
+    while ((int)c->pipe_ev.size() < 2 * cp.nchunks) {
+      hipEvent_t e = nullptr;
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->pipe_ev.push_back(e);
+    }
+  return OFDIS_OK;
+}
+
+// Chunks round-robin over the lanes, each chunk's whole pipeline on one lane (fork from s, join into s).
+int issue_round_robin(ofdis_context *c, const CallPlan &cp, hipStream_t s, const ofdis_params *p,
+                      const uint8_t *img_a, const uint8_t *img_b, const float *init, float *flow_out) {
+  const int k = cp.lanes;
   HIP_OK(hipEventRecord(c->entry, s));
   for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
-  const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * PC.nop;
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int f0 = ch * chunk, m = std::min(chunk, n - f0);
+  const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
+  const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
+  for (int ch = 0; ch < cp.nchunks; ++ch) {
+    const size_t f0 = (size_t)ch * cp.chunk;
     auto &L = c->lanes[ch % k];
-    Plan PM = m == chunk ? PC : batch_plan(p, m, width, height, init != nullptr);
-    rc = run_chunk(c, L.ws, PM, p, img_a + f0 * in_frame, img_b + f0 * in_frame, init ? init + f0 * out_frame : nullptr,
-                   flow_out + f0 * out_frame, L.s);
+    int rc = run_chunk(c, L.ws, cp.parts[ch], p, img_a + f0 * in_frame, img_b + f0 * in_frame,
+                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s);
     if (rc) return rc;
   }
   for (int i = 0; i < k; ++i) {
@@ -766,65 +828,42 @@ int run_round_robin(ofdis_context *c, hipStream_t s, const ofdis_params *p, cons
   return OFDIS_OK;
 }
 
-int pipeline_resources(ofdis_context *c, const ofdis_params *p, int width, int height, int chunk, int nchunks,
-                       bool init) {
-  int rc = ensure_lanes(c, 2, batch_plan(p, chunk, width, height, init).total);
-  if (rc) return rc;
-  while ((int)c->pipe_ev.size() < 2 * nchunks) {
-    hipEvent_t e = nullptr;
-    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->pipe_ev.push_back(e);
-  }
-  return OFDIS_OK;
-}
-
 // Two-stream software pipeline over chunks ("pipeline" option).  Lane 0 runs the HBM-streaming stages --
 // the pyramid from the u8 frames and the full-resolution upsample -- and lane 1 the latency-bound
 // DIS + TV chain (run_levels), so chunk ch's chain overlaps chunk ch+1's pyramid and chunk ch-1's
 // upsample.  Issue order on lane 0: pyr 0, pyr 1, up 0, pyr 2, up 1, ...; chunk ch uses workspace
 // ch % 2, which pyr(ch+2) reuses only after up(ch) (same stream, issued before it), which waits for
-// levels(ch).  Every hand-over is an event, so each kernel sees the data of the single-stream order.
-int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
-                  const uint8_t *img_b, const float *init, float *flow_out, int n, int width, int height,
-                  int chunk) {
-  const int nchunks = (n + chunk - 1) / chunk;
-  int rc = pipeline_resources(c, p, width, height, chunk, nchunks, init != nullptr);
-  if (rc) return rc;
-  std::vector<Plan> plans;
-  plans.reserve(nchunks);
-  for (int ch = 0; ch < nchunks; ++ch)
-    plans.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height, init != nullptr));
-  const size_t in_frame = (size_t)width * height * p->noc, out_frame = (size_t)width * height * plans[0].nop;
+// levels(ch).  Every hand-over is an event recorded and waited on within this call (and so within a
+// capture), and both lanes join s at the end.
+int issue_pipeline(ofdis_context *c, const CallPlan &cp, hipStream_t s, const ofdis_params *p,
+                   const uint8_t *img_a, const uint8_t *img_b, const float *init, float *flow_out) {
+  const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
+  const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
   hipStream_t S = c->lanes[0].s, L = c->lanes[1].s;
-  hipEvent_t *ev_pyr = c->pipe_ev.data(), *ev_lev = c->pipe_ev.data() + nchunks;
+  hipEvent_t *ev_pyr = c->pipe_ev.data(), *ev_lev = c->pipe_ev.data() + cp.nchunks;
   HIP_OK(hipEventRecord(c->entry, s));
   HIP_OK(hipStreamWaitEvent(S, c->entry, 0));
   HIP_OK(hipStreamWaitEvent(L, c->entry, 0));
   auto pyr = [&](int ch) -> int {
-    const size_t f0 = (size_t)ch * chunk;
-    int r = run_pyramid(c, c->lanes[ch & 1].ws, plans[ch], img_a + f0 * in_frame, img_b + f0 * in_frame, S);
+    const size_t f0 = (size_t)ch * cp.chunk;
+    char *ws = c->lanes[ch & 1].ws;
+    int r = run_pyramid(c, ws, cp.parts[ch], img_a + f0 * in_frame, img_b + f0 * in_frame, S);
     if (r) return r;
-    if (init && (r = run_init(c, c->lanes[ch & 1].ws, plans[ch], p, init + f0 * out_frame, S))) return r;
+    if (init && (r = run_init(c, ws, cp.parts[ch], p, init + f0 * out_frame, S))) return r;
     HIP_OK(hipEventRecord(ev_pyr[ch], S));
     return OFDIS_OK;
   };
-  static const bool dbg_sync = std::getenv("OFDIS_PIPE_SYNC") && std::getenv("OFDIS_PIPE_SYNC")[0] == '1';
-  OFDIS_TRACE("pipeline: %d chunks of %d, lanes ws %p %p", nchunks, chunk, (void *)c->lanes[0].ws,
-              (void *)c->lanes[1].ws);
-  if ((rc = pyr(0))) return rc;
-  for (int ch = 0; ch < nchunks; ++ch) {
+  int rc = pyr(0);
+  if (rc) return rc;
+  for (int ch = 0; ch < cp.nchunks; ++ch) {
     char *ws = c->lanes[ch & 1].ws;
-    OFDIS_TRACE("pipeline: chunk %d (%d frames)", ch, plans[ch].n);
+    const Plan &P = cp.parts[ch];
     HIP_OK(hipStreamWaitEvent(L, ev_pyr[ch], 0));
-    if (dbg_sync) HIP_OK(hipDeviceSynchronize());
-    if ((rc = run_levels(c, ws, plans[ch], p, L, init ? (const float *)(ws + plans[ch].off_init) : nullptr,
-                         nullptr)))
-      return rc;
-    if (dbg_sync) HIP_OK(hipDeviceSynchronize());
+    if ((rc = run_levels(c, ws, P, p, L, init ? (const float *)(ws + P.off_init) : nullptr, nullptr))) return rc;
     HIP_OK(hipEventRecord(ev_lev[ch], L));
-    if (ch + 1 < nchunks && (rc = pyr(ch + 1))) return rc;
+    if (ch + 1 < cp.nchunks && (rc = pyr(ch + 1))) return rc;
     HIP_OK(hipStreamWaitEvent(S, ev_lev[ch], 0));
-    if ((rc = run_upsample(c, ws, plans[ch], p, flow_out + (size_t)ch * chunk * out_frame, S))) return rc;
+    if ((rc = run_upsample(c, ws, P, p, flow_out + (size_t)ch * cp.chunk * out_frame, S))) return rc;
   }
   for (int i = 0; i < 2; ++i) {
     HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
@@ -833,61 +872,67 @@ int run_pipelined(ofdis_context *c, hipStream_t s, const ofdis_params *p, const 
   return OFDIS_OK;
 }
 
-}  // namespace
-
-int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width, int height,
-                       const ofdis_params *p, float *flow_out, void *stream) {
-  return ofdis_run_batch_u8_init(c, img_a, img_b, nullptr, n, width, height, p, flow_out, stream);
+int issue(ofdis_context *c, const CallPlan &cp, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
+          const uint8_t *img_b, const float *init, float *flow_out) {
+  switch (cp.kind) {
+    case CallPlan::kRoundRobin: return issue_round_robin(c, cp, s, p, img_a, img_b, init, flow_out);
+    case CallPlan::kPipeline: return issue_pipeline(c, cp, s, p, img_a, img_b, init, flow_out);
+    default: return run_chunk(c, c->ws, cp.whole, p, img_a, img_b, init, flow_out, s);
+  }
 }
 
-int ofdis_run_batch_u8_init(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, const float *init, int n,
-                            int width, int height, const ofdis_params *p, float *flow_out, void *stream) {
-  if (!c || !img_a || !img_b || !flow_out || n <= 0 || width <= 0 || height <= 0) return OFDIS_ERR_INVALID_ARGUMENT;
+// Start of a call on stream s: NULL is the legacy default stream (torch's default), which the context's
+// non-blocking stream does not order against -- hand its queued work over with an event; and the
+// workspaces are shared by every call on this context, whatever its stream -- wait for the previous call.
+int call_begin(ofdis_context *c, void *stream, hipStream_t &s) {
+  if (!c->ev_null) HIP_OK(hipEventCreateWithFlags(&c->ev_null, hipEventDisableTiming));
+  if (!c->ev_ws) HIP_OK(hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming));
+  s = stream ? (hipStream_t)stream : c->stream;
+  if (!stream) {
+    HIP_OK(hipEventRecord(c->ev_null, nullptr));
+    HIP_OK(hipStreamWaitEvent(s, c->ev_null, 0));
+  }
+  if (c->ws_pending) HIP_OK(hipStreamWaitEvent(s, c->ev_ws, 0));
+  return OFDIS_OK;
+}
+
+// End of a call: mark the workspaces' release; a NULL-stream caller's later work waits for the result.
+int call_end(ofdis_context *c, void *stream, hipStream_t s) {
+  HIP_OK(hipEventRecord(c->ev_ws, s));
+  c->ws_pending = true;
+  if (!stream) HIP_OK(hipStreamWaitEvent(nullptr, c->ev_ws, 0));
+  return OFDIS_OK;
+}
+
+int validate_call(const ofdis_params *p, int width, int height, bool init) {
   int rc = ofdis_params_validate(p, -1, -1, -1);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lock(c->mu);
-  HIP_OK(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  Plan P = batch_plan(p, n, width, height, init != nullptr);
-  rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
-  if (rc) return rc;
+  Plan P = batch_plan(p, 1, width, height, init);
+  return ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
+}
+
+// The whole-batch device path on stream s (call ordering done by the caller).
+int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8_t *img_b, const float *init, int n,
+              int width, int height, const ofdis_params *p, float *flow_out) {
   const bool capturing = !c->cap_dis.empty() || !c->cap_tv.empty();
-  const int nstreams = stream_count(c, n);
-  const int chunk = c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : (n + nstreams - 1) / nstreams;
-  const int nchunks = (n + chunk - 1) / chunk;
-  // pipelined: the streaming stages of neighbouring chunks overlap the DIS + TV chain of the current one
-  const bool pipelined = c->opt_pipeline && nchunks > 1 && !capturing && !c->timing;
-  if (!pipelined && nchunks > 1 && !capturing)  // chunks over nstreams streams (1: serialised)
-    return run_round_robin(c, s, p, img_a, img_b, init, flow_out, n, width, height, chunk);
-  if (!pipelined) {
-    rc = ensure_ws(c, P.total);
-    if (rc) return rc;
-  }
-  auto issue = [&](hipStream_t st) {
-    return pipelined ? run_pipelined(c, st, p, img_a, img_b, init, flow_out, n, width, height, chunk)
-                     : run_chunk(c, c->ws, P, p, img_a, img_b, init, flow_out, st);
-  };
-  // The pipeline is issued eagerly: its two streams would have to join the capture through events, which
-  // this HIP runtime does not survive (hipStreamEndCapture faults); eager and graph kernel boundaries
-  // cost the same on one stream, and the host issues far ahead of the device.
-  if (!c->opt_graph || capturing || c->timing || pipelined) return issue(s);
-  // ~80 dependent launches per batch: record them once as a HIP graph (on the context's own stream --
-  // the caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's
-  // stream while the pointers, sizes, parameters and options stay the same (set_option drops the graph).
+  CallPlan cp;
+  int rc = prepare(c, p, n, width, height, init != nullptr, capturing, cp);
+  if (rc) return rc;
+  if (!c->opt_graph || capturing || c->timing) return issue(c, cp, s, p, img_a, img_b, init, flow_out);
+  // ~80 dependent launches per chunk: record them once as a HIP graph (on the context's own stream -- the
+  // caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's stream while
+  // the pointers, sizes, parameters and options stay the same (set_option drops the graph).  Multi-lane
+  // issues fork from and join into the capturing stream through events recorded inside the capture.
   ofdis_context::GraphKey key;
   std::memset(&key, 0, sizeof(key));  // padding included: the key is compared bytewise
   key.a = img_a; key.b = img_b; key.out = flow_out; key.ws = c->ws; key.init = init;
   key.n = n; key.w = width; key.h = height; key.p = *p;
   if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
-    if (c->gexec) {  // the previous graph may still be running on a caller stream
-      HIP_OK(hipDeviceSynchronize());
-      HIP_OK(hipGraphExecDestroy(c->gexec));
-      c->gexec = nullptr;
-    }
+    if ((rc = drop_graph(c))) return rc;
     hipGraph_t graph = nullptr;
-    OFDIS_TRACE("graph: capture (pipelined %d, chunk %d)", (int)pipelined, chunk);
+    OFDIS_TRACE("graph: capture (kind %d, %d chunks of %d)", (int)cp.kind, cp.nchunks, cp.chunk);
     HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    rc = issue(c->stream);
+    rc = issue(c, cp, c->stream, p, img_a, img_b, init, flow_out);
     const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
     OFDIS_TRACE("graph: captured rc %d end %d", rc, (int)ce);
     if (rc) {
@@ -903,9 +948,65 @@ int ofdis_run_batch_u8_init(ofdis_context *c, const uint8_t *img_a, const uint8_
     }
     std::memcpy(&c->gkey, &key, sizeof(key));
   }
-  OFDIS_TRACE("graph: launch");
   HIP_OK(hipGraphLaunch(c->gexec, s));
   return OFDIS_OK;
+}
+
+// verbosity 2, one pair (the CLI): the reference's stdout timers -- pyramid (run_dense.cpp:352), grid
+// allocation (oflow.cpp:177), per-scale stages (oflow.cpp:297) and the OFClass total (oflow.cpp:336) --
+// from HIP events around eager launches on the context's stream.
+int run_verbose(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, const float *init, int width,
+                int height, const ofdis_params *p, float *flow_out) {
+  hipStream_t s = c->stream;
+  auto t0 = std::chrono::steady_clock::now();
+  Plan P = batch_plan(p, 1, width, height, init != nullptr);
+  int rc = ensure_ws(c, P.total);
+  if (rc) return rc;
+  const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, s));
+  rc = run_pyramid(c, c->ws, P, img_a, img_b, s);
+  if (!rc && init) rc = run_init(c, c->ws, P, p, init, s);
+  HIP_OK(hipEventRecord(e1, s));
+  HIP_OK(hipEventSynchronize(e1));
+  float pyr_ms = 0.0f;
+  hipEventElapsedTime(&pyr_ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (rc) return rc;
+  std::printf("TIME (Pyramide+Gradients) (ms): %3g\n", pyr_ms);
+  std::printf("TIME (Grid Memo. Alloc. ) (ms): %3g\n", alloc_ms);
+  auto t1 = std::chrono::steady_clock::now();
+  std::vector<StageTimes> times;
+  rc = run_levels(c, c->ws, P, p, s, init ? (const float *)(c->ws + P.off_init) : nullptr, &times);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s));
+  const double ms = alloc_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+  print_times(P, times, ms, p->verbosity);
+  return run_upsample(c, c->ws, P, p, flow_out, s);
+}
+
+}  // namespace
+
+int ofdis_run_batch_u8(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width, int height,
+                       const ofdis_params *p, float *flow_out, void *stream) {
+  return ofdis_run_batch_u8_init(c, img_a, img_b, nullptr, n, width, height, p, flow_out, stream);
+}
+
+int ofdis_run_batch_u8_init(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, const float *init, int n,
+                            int width, int height, const ofdis_params *p, float *flow_out, void *stream) {
+  if (!c || !img_a || !img_b || !flow_out || n <= 0 || width <= 0 || height <= 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  int rc = validate_call(p, width, height, init != nullptr);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  hipStream_t s;
+  if ((rc = call_begin(c, stream, s))) return rc;
+  rc = run_batch(c, s, img_a, img_b, init, n, width, height, p, flow_out);
+  const int rc2 = call_end(c, stream, s);
+  return rc ? rc : rc2;
 }
 
 int ofdis_run_batch_u8_host(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
@@ -932,11 +1033,23 @@ int ofdis_run_batch_u8_init_host(ofdis_context *c, const uint8_t *img_a, const u
       step(hipMemcpyAsync(da, img_a, in, hipMemcpyHostToDevice, c->stream)) &&
       step(hipMemcpyAsync(db, img_b, in, hipMemcpyHostToDevice, c->stream)) &&
       (!init || step(hipMemcpyAsync(dinit, init, out * sizeof(float), hipMemcpyHostToDevice, c->stream)))) {
+    const bool verbose = p->verbosity > 1 && n == 1 && c->cap_dis.empty() && c->cap_tv.empty() && !c->timing;
     auto t0 = std::chrono::steady_clock::now();
-    rc = ofdis_run_batch_u8_init(c, da, db, dinit, n, width, height, p, dout, c->stream);
+    if (verbose) {
+      rc = validate_call(p, width, height, dinit != nullptr);
+      if (!rc) {
+        std::lock_guard<std::mutex> lock(c->mu);
+        hipStream_t s;
+        rc = call_begin(c, c->stream, s);
+        if (!rc) rc = run_verbose(c, da, db, dinit, width, height, p, dout);
+        if (!rc) rc = call_end(c, c->stream, s);
+      }
+    } else {
+      rc = ofdis_run_batch_u8_init(c, da, db, dinit, n, width, height, p, dout, c->stream);
+    }
     if (rc == OFDIS_OK && step(hipStreamSynchronize(c->stream))) {
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      if (p->verbosity > 0) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", ms);
+      if (p->verbosity == 1) std::printf("TIME (O.Flow Run-Time   ) (ms): %3g\n", ms);
       step(hipMemcpy(flow_out, dout, out * sizeof(float), hipMemcpyDeviceToHost));
     }
   }
@@ -971,7 +1084,10 @@ int ofdis_pyramid_u8_host(ofdis_context *c, const uint8_t *img, int width, int h
   uint8_t *d = nullptr;
   HIP_OK(hipMalloc(&d, in));
   HIP_OK(hipMemcpy(d, img, in, hipMemcpyHostToDevice));
-  rc = run_pyramid(c, c->ws, P, d, d, c->stream);
+  hipStream_t st;
+  rc = call_begin(c, c->stream, st);
+  if (rc == OFDIS_OK) rc = run_pyramid(c, c->ws, P, d, d, st);
+  if (rc == OFDIS_OK) rc = call_end(c, c->stream, st);
   if (rc == OFDIS_OK) {
     HIP_OK(hipStreamSynchronize(c->stream));
     for (int s = p->sc_l; s <= p->sc_f; ++s) {
@@ -1001,66 +1117,25 @@ int ofdis_context_set_stage_capture(ofdis_context *c, float *const *dis_flow, fl
 int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   if (!c || !key) return OFDIS_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lock(c->mu);
-  if (c->gexec) {  // a captured graph bakes in the options it was recorded with
+  struct Opt {
+    const char *name;
+    int ofdis_context::*field;
+    int lo, hi;
+  };
+  static const Opt opts[] = {
+      {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
+      {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
+      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 1},
+      {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
+  };
+  for (const Opt &o : opts) {
+    if (std::strcmp(key, o.name) != 0) continue;
+    if (value < o.lo || value > o.hi) return OFDIS_ERR_INVALID_ARGUMENT;
     HIP_OK(hipSetDevice(c->device));
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipGraphExecDestroy(c->gexec));
-    c->gexec = nullptr;
-  }
-  if (std::strcmp(key, "pipeline") == 0) {
-    c->opt_pipeline = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "sor_generic") == 0) {
-    c->opt_sor_generic = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "sor_rows") == 0 && (value == 0 || value == 1 || value == 2 || value == 4)) {
-    c->opt_sor_rows = value;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "sor_lean") == 0 && (value == 0 || value == 2 || value == 3 || value == 5)) {
-    c->opt_sor_lean = value;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "smsys") == 0) {
-    c->opt_smsys = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "sor_cring") == 0) {
-    c->opt_sor_cring = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "sys_fused") == 0) {
-    c->opt_sys_fused = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "wave_per_patch") == 0) {
-    c->opt_wave_per_patch = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "nt_store") == 0) {
-    c->opt_nt_store = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "graph") == 0) {
-    c->opt_graph = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "tv_fused") == 0) {
-    c->opt_tv_fused = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "sor_pipe") == 0) {
-    c->opt_sor_pipe = value != 0;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "streams") == 0 && value >= 0 && value <= 16) {
-    c->opt_streams = value;
-    return OFDIS_OK;
-  }
-  if (std::strcmp(key, "chunk") == 0 && value >= 0) {
-    c->opt_chunk = value;
+    const int rc = drop_graph(c);  // a captured graph bakes in the options it was recorded with
+    if (rc) return rc;
+    c->*o.field = (o.hi == 1) ? (value != 0) : value;
     return OFDIS_OK;
   }
   return OFDIS_ERR_INVALID_ARGUMENT;
@@ -1116,15 +1191,6 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
     if (k == "aggregate") b += px * 4.0 * nop + (double)g.npatch * 4.0 * (nop + novals);
     if (k == "pyr_pad_grad") b += 2.0 * (px * 4.0 * noc + 3.0 * g.W * g.H * 4.0 * noc);
     if (k == "pyr_down" && g.level > p->sc_l) b += 2.0 * noc * 4.0 * (4.0 * px + px);
-    if (p->usetvref && k == "tv_level") {  // the fused level: prep + derivatives + n_inner x (system + SOR) + final
-      b += px * 4.0 * (4 * noc + 1 + 3 * nop) + px * 4.0 * noc * (2 + 4 + 2 + 3) + px * 4.0 * 3 * nop;
-      b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
-      b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
-    }
-    // the fused system + SOR launch: the system's inputs and the SOR's du / dv traffic (coefficients stay
-    // in LDS); the smoothness weights are tv_system's
-    if (k == "tv_sys_sor")
-      b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * 2 * nop);
     if (p->usetvref) {
       if (k == "tv_prep") b += px * 4.0 * (4 * noc + 1 + 3 * nop);
       if (k == "tv_deriv") b += px * 4.0 * noc * (2 + 4 + 2 + 3);
@@ -1164,7 +1230,8 @@ int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx,
   Plan P = make_plan(p, 1, width, height, imgpadding);
   rc = ensure_ws(c, P.total);
   if (rc) return rc;
-  hipStream_t s = c->stream;
+  hipStream_t s;
+  if ((rc = call_begin(c, c->stream, s))) return rc;
   for (int sl = p->sc_l; sl <= p->sc_f; ++sl) {
     const LevelGeom &g = P.lv[sl - p->sc_l];
     const size_t fb = sizeof(float) * (size_t)g.W * g.H * p->noc;
@@ -1197,8 +1264,17 @@ int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx,
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     print_times(P, times, ms, p->verbosity);
   }
+  if (rc == OFDIS_OK) rc = call_end(c, c->stream, s);
   if (dinit) hipFree(dinit);
   return rc;
+}
+
+int ofdis_max_frames_per_launch(const ofdis_params *p, int width, int height, int *frames) {
+  if (!p || !frames || width <= 0 || height <= 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  const int rc = ofdis_params_validate(p, -1, -1, -1);
+  if (rc) return rc;
+  *frames = tv_frame_cap(p, width, height);
+  return OFDIS_OK;
 }
 
 }  // extern "C"

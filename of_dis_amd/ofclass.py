@@ -176,12 +176,10 @@ class Context:
             if tuple(init.shape) != (n, h, w, p.nop) or init.dtype != torch.float32 or not init.is_cuda:
                 raise ValueError("init must be a float32 CUDA tensor [n, h, w, nop]")
             init = init.contiguous()
+        # stream 0 is torch's default (the legacy NULL stream): the C-ABI orders the call after the work queued
+        # there (e.g. the copy kernels of .contiguous() above) and that stream's later work after the call
         self.run_ptr(a.data_ptr(), b.data_ptr(), n, w, h, p, out.data_ptr(), stream,
                      init.data_ptr() if init is not None else 0)
-        if not stream:
-            # torch's default stream is the legacy NULL stream, which the C-ABI reads as "the context's own
-            # (non-blocking) stream": nothing would order later torch work after the flow, so wait here.
-            torch.cuda.synchronize(a.device)
         return out
 
     def run_host(self, a: np.ndarray, b: np.ndarray, p: Params, init: Optional[np.ndarray] = None) -> np.ndarray:
@@ -246,6 +244,13 @@ def kernel_names():
     return lib().ofdis_kernel_names().decode().split(",")
 
 
+def max_frames_per_launch(p: Params, width: int, height: int) -> int:
+    """Frames one launch of the refinement kernels takes at this size (32-bit plane-group offsets)."""
+    v = C.c_int()
+    check(lib().ofdis_max_frames_per_launch(C.byref(p), width, height, C.byref(v)), "max_frames_per_launch")
+    return v.value
+
+
 def algorithmic_bytes(p: Params, width: int, height: int, kernel: str) -> float:
     v = C.c_double()
     check(lib().ofdis_algorithmic_bytes(C.byref(p), width, height, kernel.encode(), C.byref(v)), "bytes")
@@ -254,4 +259,5 @@ def algorithmic_bytes(p: Params, width: int, height: int, kernel: str) -> float:
 
 __all__ = ["OFClass", "Context", "Params", "oppoint", "params_from_strings", "validate", "synth_pair",
            "write_flo", "write_pfm", "read_flo", "read_image", "auto_first_scale", "kernel_names", "algorithmic_bytes",
+           "max_frames_per_launch",
            "MODE_OF", "MODE_DE"]

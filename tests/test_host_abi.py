@@ -221,3 +221,24 @@ def build_dropin(tmp_path):
 def test_oflow_hpp_dropin_compiles(tmp_path):
     """The reference-signature OFC::OFClass wrapper compiles and links as plain C++ (no HIP headers)."""
     assert os.access(build_dropin(tmp_path), os.X_OK)
+
+
+@pytest.mark.parametrize("w,h,noc,op,sc_l", [(640, 480, 3, 2, 0), (960, 540, 1, 2, 0), (1920, 1080, 1, 2, None),
+                                           (3840, 2160, 1, 4, None)])
+def test_max_frames_per_launch_keeps_plane_groups_below_2_30(w, h, noc, op, sc_l):
+    """The refinement kernels address a plane group (frames * noc * skewed plane floats) with 32-bit byte
+    offsets; the runtime chunks a batch so that no launch exceeds 2^30 floats per group."""
+    p = od.oppoint(op, w, 1, noc)
+    if sc_l is not None:
+        p.sc_l = sc_l
+    cap = od.max_frames_per_launch(p, w, h)
+    d = 1 << p.sc_f
+    wp, hp = w + (-w) % d, h + (-h) % d
+    plane = 0
+    for s in range(p.sc_l, p.sc_f + 1):  # skewed plane of the largest level (ofdis_runtime.cpp skew_plane)
+        lw, lh = wp >> s, hp >> s
+        slots = lw * lh if lh <= lw else (lw + lh - 1) * lh
+        plane = max(plane, (slots + 64 + 3) // 4 * 4)
+    assert cap >= 1 and cap * noc * plane < 2 ** 30 <= (cap + 1) * noc * plane
+    p.usetvref = 0
+    assert od.max_frames_per_launch(p, w, h) == 2 ** 30

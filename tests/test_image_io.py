@@ -228,6 +228,24 @@ def test_png_errors(tmp_path):
         assert e.value.code == code, name
 
 
+def test_oversized_headers_fail_cleanly(tmp_path):
+    """A tiny file whose header claims a huge image is refused before any buffer is sized from it
+    (OpenCV's CV_IO_MAX_IMAGE_PIXELS = 2^30), with a status code instead of an abort."""
+    import zlib as _z
+    for w, h in ((1 << 24, 1 << 24), (40000, 40000), (1 << 16, 1 << 15)):
+        ihdr = struct.pack(">IIBBBBB", w, h, 8, 0, 0, 0, 0)
+        png = b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", ihdr) + _chunk(b"IDAT", _z.compress(b"\0" * 64)) + \
+            _chunk(b"IEND", b"")
+        (tmp_path / "huge.png").write_bytes(png)
+        with pytest.raises(od.OfdisError) as e:
+            read(tmp_path / "huge.png", 1)
+        assert e.value.code == _lib.ERR_IO, (w, h)
+    (tmp_path / "huge.pgm").write_bytes(b"P5\n40000 40000\n255\n" + bytes(16))
+    with pytest.raises(od.OfdisError) as e:
+        read(tmp_path / "huge.pgm", 1)
+    assert e.value.code == _lib.ERR_IO
+
+
 @pytest.mark.parametrize("kind", ["P2", "P3", "P5", "P6", "P1", "P4"])
 @pytest.mark.parametrize("want", [1, 3])
 def test_pnm(tmp_path, kind, want):

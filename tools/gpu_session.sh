@@ -16,9 +16,9 @@ step() {  # name, seconds, command...
   return 0
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout=600 -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout=300 --timeout-method=thread -p no:cacheprovider
 step bench 600 python bench.py --steps ${BENCH_STEPS:-10} --warmup 3 --batch ${BENCH_BATCH:-0}
 if [ "${PROFILE:-1}" = "1" ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --batch ${BENCH_BATCH:-0} --cpu-seconds 0
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --batch ${BENCH_BATCH:-0} --cpu-seconds 0 --no-latency
 fi
 echo "== session done"
