@@ -176,9 +176,36 @@ int ofo_build_pyramid(const uint8_t *img, int width, int height, int noc, int sc
 int ofo_build_pyramid_ex(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
                          int gradmag, float **img_pyr, float **dx_pyr, float **dy_pyr) {
   int w = width, h = height;
-  float *cur = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
-  if (!cur) return OFDIS_ERR_OUT_OF_MEMORY;
-  for (size_t i = 0; i < (size_t)w * h * noc; ++i) cur[i] = (float)img[i]; /* convertTo CV_32F (:327) */
+  float *cur;
+  int s0 = 0;
+  if (!gradmag && sc_l >= 1) {
+    /* convertTo CV_32F (:327) and the first 2x2 mean fused: the u8 values are exact in fp32, so
+     * ((a + b) + (d + e)) * 0.25 of the converted samples is computed straight from the bytes */
+    const int nw = w / 2, nh = h / 2, rn = nw * noc;
+    cur = (float *)malloc(sizeof(float) * (size_t)nw * nh * noc);
+    if (!cur) return OFDIS_ERR_OUT_OF_MEMORY;
+    for (int y = 0; y < nh; ++y) {
+      const uint8_t *r0 = img + (size_t)(2 * y) * w * noc, *r1 = r0 + (size_t)w * noc;
+      float *o = cur + (size_t)y * rn;
+      if (noc == 1) {
+        for (int x = 0; x < nw; ++x)
+          o[x] = (((float)r0[2 * x] + (float)r0[2 * x + 1]) + ((float)r1[2 * x] + (float)r1[2 * x + 1])) * 0.25f;
+      } else {
+        for (int x = 0; x < nw; ++x)
+          for (int c = 0; c < noc; ++c) {
+            const int i = 2 * x * noc + c;
+            o[x * noc + c] = (((float)r0[i] + (float)r0[i + noc]) + ((float)r1[i] + (float)r1[i + noc])) * 0.25f;
+          }
+      }
+    }
+    w = nw;
+    h = nh;
+    s0 = 1;
+  } else {
+    cur = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
+    if (!cur) return OFDIS_ERR_OUT_OF_MEMORY;
+    for (size_t i = 0; i < (size_t)w * h * noc; ++i) cur[i] = (float)img[i]; /* convertTo CV_32F (:327) */
+  }
   if (gradmag) { /* SELECTCHANNEL 2 (:139-148): level 0 = sqrt(dx.mul(dx) + dy.mul(dy)), Sobel 3, 1/8 */
     float *gx = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
     float *gy = (float *)malloc(sizeof(float) * (size_t)w * h * noc);
@@ -187,18 +214,20 @@ int ofo_build_pyramid_ex(const uint8_t *img, int width, int height, int noc, int
     for (size_t i = 0; i < (size_t)w * h * noc; ++i) cur[i] = sqrtf(gx[i] * gx[i] + gy[i] * gy[i]);
     free(gx); free(gy);
   }
-  for (int s = 0; s <= sc_f; ++s) {
-    if (s > 0) { /* cv::resize(.5, INTER_LINEAR) -> OpenCV area-fast 2x: mean of the 2x2 block */
+  for (int s = s0; s <= sc_f; ++s) {
+    if (s > s0) { /* cv::resize(.5, INTER_LINEAR) -> OpenCV area-fast 2x: mean of the 2x2 block */
       int nw = w / 2, nh = h / 2;
       float *nx = (float *)malloc(sizeof(float) * (size_t)nw * nh * noc);
       if (!nx) { free(cur); return OFDIS_ERR_OUT_OF_MEMORY; }
-      for (int y = 0; y < nh; ++y)
+      for (int y = 0; y < nh; ++y) {
+        const float *r0 = cur + (size_t)(2 * y) * w * noc, *r1 = r0 + (size_t)w * noc;
+        float *o = nx + (size_t)y * nw * noc;
         for (int x = 0; x < nw; ++x)
           for (int c = 0; c < noc; ++c) {
-            float a = cur[((2 * y) * w + 2 * x) * noc + c], b = cur[((2 * y) * w + 2 * x + 1) * noc + c];
-            float d = cur[((2 * y + 1) * w + 2 * x) * noc + c], e = cur[((2 * y + 1) * w + 2 * x + 1) * noc + c];
-            nx[(y * nw + x) * noc + c] = ((a + b) + (d + e)) * 0.25f;
+            const int i = 2 * x * noc + c;
+            o[x * noc + c] = ((r0[i] + r0[i + noc]) + (r1[i] + r1[i + noc])) * 0.25f;
           }
+      }
       free(cur);
       cur = nx; w = nw; h = nh;
     }
@@ -664,17 +693,19 @@ void ofo_sub_laplacian(float *dst, const float *src, const float *wh, const floa
 
 /* compute_data (opticalflow_aux.c:408-594).  The RGB branch keeps the upstream slips exactly:
  * channel 1's colour term uses Iy of channel 2, and the gradient robust sum keeps only channel 3. */
-void ofo_compute_data(float *a11, float *a12, float *a22, float *b1, float *b2, const float *mask,
-                      const float *du, const float *dv, const float *Ix, const float *Iy, const float *Iz,
-                      const float *Ixx, const float *Ixy, const float *Iyy, const float *Ixz, const float *Iyz,
-                      int w, int h, int noc, float hdo3, float hgo3) {
+static inline __attribute__((always_inline)) void compute_data_body(
+    float *restrict a11, float *restrict a12, float *restrict a22, float *restrict b1, float *restrict b2,
+    const float *restrict mask, const float *restrict du, const float *restrict dv, const float *restrict Ix,
+    const float *restrict Iy, const float *restrict Iz, const float *restrict Ixx, const float *restrict Ixy,
+    const float *restrict Iyy, const float *restrict Ixz, const float *restrict Iyz, int w, int h, const int noc,
+    float hdo3, float hgo3, const int color) {
   const size_t n = (size_t)w * h;
   for (size_t i = 0; i < n; ++i) {
     float A11 = 0.0f, A12 = 0.0f, A22 = 0.0f, B1 = 0.0f, B2 = 0.0f;
     const float u = du[i], v = dv[i], m = mask[i];
     float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
     if (noc == 1) {
-      if (hdo3 != 0.0f) {
+      if (color) {
         tmpx = Ix[i]; tmpy = Iy[i];
         tmp2 = (Iz[i] + tmpx * u) + tmpy * v;
         n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
@@ -709,7 +740,7 @@ void ofo_compute_data(float *a11, float *a12, float *a22, float *b1, float *b2, 
     } else {
       const size_t o2 = n, o3 = 2 * n;
       float n3, n4, n5, n6;
-      if (hdo3 != 0.0f) {
+      if (color) {
         tmpx = Ix[i]; tmpy = Iy[i];
         tmp2 = (Iz[i] + tmpx * u) + tmpy * v;
         n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
@@ -794,6 +825,24 @@ void ofo_compute_data(float *a11, float *a12, float *a22, float *b1, float *b2, 
     }
     a11[i] = A11; a12[i] = A12; a22[i] = A22; b1[i] = B1; b2[i] = B2;
   }
+}
+
+/* The per-pixel expression trees of compute_data, one loop per (noc, colour term) so the compiler can
+ * vectorise it like the reference's SSE code (per-pixel IEEE operations, same order: bit-identical). */
+void ofo_compute_data(float *restrict a11, float *restrict a12, float *restrict a22, float *restrict b1,
+                      float *restrict b2, const float *restrict mask, const float *restrict du,
+                      const float *restrict dv, const float *restrict Ix, const float *restrict Iy,
+                      const float *restrict Iz, const float *restrict Ixx, const float *restrict Ixy,
+                      const float *restrict Iyy, const float *restrict Ixz, const float *restrict Iyz,
+                      int w, int h, int noc, float hdo3, float hgo3) {
+#define OFO_CD(NOC, COL) compute_data_body(a11, a12, a22, b1, b2, mask, du, dv, Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, \
+                                           Iyz, w, h, NOC, hdo3, hgo3, COL)
+  if (noc == 1) {
+    if (hdo3 != 0.0f) OFO_CD(1, 1); else OFO_CD(1, 0);
+  } else {
+    if (hdo3 != 0.0f) OFO_CD(3, 1); else OFO_CD(3, 0);
+  }
+#undef OFO_CD
 }
 
 /* compute_data_DE (opticalflow_aux.c:601-747) */
@@ -1185,11 +1234,16 @@ int ofo_upsample_crop(const float *flow_l, int wl, int hl, int nop, int scale_lo
   const float fct = (float)pow(2.0, scale_log2);
   const int Wd = wl << scale_log2, Hd = hl << scale_log2;
   const double scale = 1.0 / (double)fct;
-  float *row0 = (float *)malloc(sizeof(float) * (size_t)width_org * nop);
-  float *row1 = (float *)malloc(sizeof(float) * (size_t)width_org * nop);
+  const int n = width_org * nop;
   int *xs = (int *)malloc(sizeof(int) * width_org);
   float *xa = (float *)malloc(sizeof(float) * width_org);
   int *xl = (int *)malloc(sizeof(int) * width_org);
+  /* per output value: the two source taps (the right one clamped into the row: it is selected away where
+   * the horizontal interpolation is not linear), the weights 1 - fx, fx and the linear flag */
+  int *i0 = (int *)malloc(sizeof(int) * n), *i1 = (int *)malloc(sizeof(int) * n), *lf = (int *)malloc(sizeof(int) * n);
+  float *wa = (float *)malloc(sizeof(float) * n), *wb = (float *)malloc(sizeof(float) * n);
+  float *rows[2] = {(float *)malloc(sizeof(float) * n), (float *)malloc(sizeof(float) * n)};
+  int rid[2] = {-1, -1};
   int xmax = Wd;
   for (int dx = 0; dx < Wd; ++dx) {
     float fx = (float)((dx + 0.5) * scale - 0.5);
@@ -1206,6 +1260,15 @@ int ofo_upsample_crop(const float *flow_l, int wl, int hl, int nop, int scale_lo
   }
   /* xmax is monotone: re-derive the "linear" flag once the full scan is known */
   for (int x = 0; x < width_org; ++x) xl[x] = (x + offx) < xmax;
+  for (int x = 0; x < width_org; ++x)
+    for (int k = 0; k < nop; ++k) {
+      const int i = x * nop + k;
+      i0[i] = xs[x] * nop + k;
+      i1[i] = (xs[x] + 1 < wl ? xs[x] + 1 : wl - 1) * nop + k;
+      wa[i] = 1.f - xa[x];
+      wb[i] = xa[x];
+      lf[i] = xl[x];
+    }
   for (int y = 0; y < height_org; ++y) {
     int dy = y + offy;
     float fy = (float)((dy + 0.5) * scale - 0.5);
@@ -1214,24 +1277,28 @@ int ofo_upsample_crop(const float *flow_l, int wl, int hl, int nop, int scale_lo
     int r0 = sy >= 0 ? (sy < hl ? sy : hl - 1) : 0;
     int r1 = sy + 1 >= 0 ? (sy + 1 < hl ? sy + 1 : hl - 1) : 0;
     const float b0 = 1.f - fy, b1 = fy;
-    for (int r = 0; r < 2; ++r) {
-      const float *S = flow_l + (size_t)(r == 0 ? r0 : r1) * wl * nop;
-      float *D = r == 0 ? row0 : row1;
-      for (int x = 0; x < width_org; ++x)
-        for (int k = 0; k < nop; ++k) {
-          float s0 = S[xs[x] * nop + k] * fct;
-          if (xl[x]) {
-            float s1 = S[(xs[x] + 1) * nop + k] * fct;
-            D[x * nop + k] = s0 * (1.f - xa[x]) + s1 * xa[x];
-          } else {
-            D[x * nop + k] = s0;
-          }
+    const float *R[2];
+    for (int r = 0; r < 2; ++r) {  /* the horizontally resized source row, computed once per source row */
+      const int want = r == 0 ? r0 : r1;
+      int slot = rid[0] == want ? 0 : (rid[1] == want ? 1 : -1);
+      if (slot < 0) {
+        slot = (rid[0] == (r == 0 ? r1 : r0)) ? 1 : 0;  /* keep the row the other tap still needs */
+        const float *S = flow_l + (size_t)want * wl * nop;
+        float *D = rows[slot];
+        for (int i = 0; i < n; ++i) {
+          const float s0 = S[i0[i]] * fct, s1 = S[i1[i]] * fct;
+          const float lin = s0 * wa[i] + s1 * wb[i];
+          D[i] = lf[i] ? lin : s0;
         }
+        rid[slot] = want;
+      }
+      R[r] = rows[slot];
     }
-    for (int x = 0; x < width_org * nop; ++x) out[(size_t)y * width_org * nop + x] = row0[x] * b0 + row1[x] * b1;
+    float *O = out + (size_t)y * n;
+    for (int i = 0; i < n; ++i) O[i] = R[0][i] * b0 + R[1][i] * b1;
   }
   (void)Hd;
-  free(row0); free(row1); free(xs); free(xa); free(xl);
+  free(rows[0]); free(rows[1]); free(xs); free(xa); free(xl); free(i0); free(i1); free(lf); free(wa); free(wb);
   return 0;
 }
 
@@ -1273,13 +1340,19 @@ int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *ini
   ofo_divisibility_pad(width, height, p->sc_f + (init ? 1 : 0), &padw, &padh);  /* run_dense.cpp:302 */
   const int Wp = width + padw, Hp = height + padh, l = padw / 2, t = padh / 2;
   uint8_t *pa = (uint8_t *)malloc((size_t)Wp * Hp * noc), *pb = (uint8_t *)malloc((size_t)Wp * Hp * noc);
-  for (int y = 0; y < Hp; ++y)
-    for (int x = 0; x < Wp; ++x)
+  for (int y = 0; y < Hp; ++y) { /* copyMakeBorder BORDER_REPLICATE (run_dense.cpp:309-310) */
+    const size_t sr = (size_t)clampi(y - t, 0, height - 1) * width * noc, dr = (size_t)y * Wp * noc;
+    memcpy(pa + dr + (size_t)l * noc, img_a + sr, (size_t)width * noc);
+    memcpy(pb + dr + (size_t)l * noc, img_b + sr, (size_t)width * noc);
+    for (int x = 0; x < Wp; ++x) {
+      if (x >= l && x < l + width) { x = l + width - 1; continue; }
+      const size_t so = sr + (size_t)clampi(x - l, 0, width - 1) * noc, d = dr + (size_t)x * noc;
       for (int c = 0; c < noc; ++c) {
-        size_t s = ((size_t)clampi(y - t, 0, height - 1) * width + clampi(x - l, 0, width - 1)) * noc + c;
-        pa[((size_t)y * Wp + x) * noc + c] = img_a[s];
-        pb[((size_t)y * Wp + x) * noc + c] = img_b[s];
+        pa[d + c] = img_a[so + c];
+        pb[d + c] = img_b[so + c];
       }
+    }
+  }
   float *pyr[6][32];
   memset(pyr, 0, sizeof(pyr));
   int rc = 0;
