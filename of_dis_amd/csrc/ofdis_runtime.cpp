@@ -1105,11 +1105,18 @@ int ofdis_pyramid_u8_host(ofdis_context *c, const uint8_t *img, int width, int h
 
 int ofdis_context_set_stage_capture(ofdis_context *c, float *const *dis_flow, float *const *tv_flow, int nscales) {
   if (!c || nscales < 0) return OFDIS_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lock(c->mu);
   c->cap_dis.assign(nscales, nullptr);
   c->cap_tv.assign(nscales, nullptr);
+  bool any = false;
   for (int i = 0; i < nscales; ++i) {
     if (dis_flow) c->cap_dis[i] = dis_flow[i];
     if (tv_flow) c->cap_tv[i] = tv_flow[i];
+    any = any || c->cap_dis[i] || c->cap_tv[i];
+  }
+  if (!any) {  // no capture: the batch runs as usual (chunked, graph-replayed)
+    c->cap_dis.clear();
+    c->cap_tv.clear();
   }
   return OFDIS_OK;
 }
