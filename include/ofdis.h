@@ -160,8 +160,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "smsys" (0/1, default 1): smoothness and system of a TV iteration in one launch;
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch;
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
- *   "graph" (0/1, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
- *                        parameters repeat (re-captured when they change);
+ *   "graph" (0/1/2, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
+ *                        parameters repeat (re-captured when they change); 1 captures single-stream
+ *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined);
  *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1) and "chunk" (frames, default 0 =
  *                        the batch split evenly over the streams): a batch is cut into chunks that run
  *                        round-robin on that many HIP streams with separate workspaces, overlapping one

@@ -918,7 +918,10 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
   CallPlan cp;
   int rc = prepare(c, p, n, width, height, init != nullptr, capturing, cp);
   if (rc) return rc;
-  if (!c->opt_graph || capturing || c->timing) return issue(c, cp, s, p, img_a, img_b, init, flow_out);
+  OFDIS_TRACE("run_batch: kind %d, %d chunks of %d, %d lanes", (int)cp.kind, cp.nchunks, cp.chunk, cp.lanes);
+  // graph 1: capture single-stream batches; graph 2: also the multi-lane (fork / join) issues
+  const bool graph = c->opt_graph == 2 || (c->opt_graph == 1 && cp.kind == CallPlan::kSingle);
+  if (!graph || capturing || c->timing) return issue(c, cp, s, p, img_a, img_b, init, flow_out);
   // ~80 dependent launches per chunk: record them once as a HIP graph (on the context's own stream -- the
   // caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's stream while
   // the pointers, sizes, parameters and options stay the same (set_option drops the graph).  Multi-lane
@@ -929,10 +932,11 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
   key.n = n; key.w = width; key.h = height; key.p = *p;
   if (!c->gexec || std::memcmp(&key, &c->gkey, sizeof(key)) != 0) {
     if ((rc = drop_graph(c))) return rc;
-    hipGraph_t graph = nullptr;
     OFDIS_TRACE("graph: capture (kind %d, %d chunks of %d)", (int)cp.kind, cp.nchunks, cp.chunk);
     HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     rc = issue(c, cp, c->stream, p, img_a, img_b, init, flow_out);
+    OFDIS_TRACE("graph: issued rc %d", rc);
+    hipGraph_t graph = nullptr;
     const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
     OFDIS_TRACE("graph: captured rc %d end %d", rc, (int)ce);
     if (rc) {
@@ -941,6 +945,7 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
     }
     if (ce != hipSuccess || !graph) return OFDIS_ERR_DEVICE;
     const hipError_t ie = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
+    OFDIS_TRACE("graph: instantiated %d", (int)ie);
     hipGraphDestroy(graph);
     if (ie != hipSuccess) {
       c->gexec = nullptr;
@@ -949,6 +954,7 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
     std::memcpy(&c->gkey, &key, sizeof(key));
   }
   HIP_OK(hipGraphLaunch(c->gexec, s));
+  OFDIS_TRACE("graph: launched");
   return OFDIS_OK;
 }
 
@@ -1133,7 +1139,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
-      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 1},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 2},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {

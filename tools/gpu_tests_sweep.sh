@@ -5,6 +5,9 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${1:-tsweep}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+echo "== graph probe"; date
+timeout -k 10 400 python tools/graph_probe.py > "$OUT/graph_probe.log" 2>&1
+echo "graph probe rc=$?"; grep -E "^==|same|graph:|Fatal|Segm" "$OUT/graph_probe.log" | head -40
 echo "== pytest"; date
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout=300 --timeout-method=thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 3 "$OUT/pytest_gpu.log"
