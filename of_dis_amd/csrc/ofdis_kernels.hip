@@ -2479,7 +2479,9 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
   else
     k_tv_smooth<1><<<dim3(ceil_div(a.sp, 256), a.n), 256, 0, s>>>(a);
 }
-bool tv_smsys_ok(const TvArgs &a) { return a.smsys && smsys_lds(a.h) <= 64 * 1024; }
+// The fused form stages RB + 4 rows for RB computed ones: below RB = 4 (h > 256) the halo re-reads cost
+// more than the smoothness round trip saves (config E, h = 544 / 272: 518 vs 299 us per launch).
+bool tv_smsys_ok(const TvArgs &a) { return a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024; }
 void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
   const dim3 grid(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), smsys_rb(a.h)));
   const size_t lds = smsys_lds(a.h);

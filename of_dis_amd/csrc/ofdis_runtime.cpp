@@ -920,7 +920,11 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
   if (rc) return rc;
   OFDIS_TRACE("run_batch: kind %d, %d chunks of %d, %d lanes", (int)cp.kind, cp.nchunks, cp.chunk, cp.lanes);
   // graph 1: capture single-stream batches; graph 2: also the multi-lane (fork / join) issues
-  const bool graph = c->opt_graph == 2 || (c->opt_graph == 1 && cp.kind == CallPlan::kSingle);
+  // (the two-stream pipeline is always issued eagerly: hipStreamEndCapture of its mutually dependent lanes
+  // -- S waits on L's levels, L on S's pyramids -- segfaults inside the HIP runtime on this image, while the
+  // fork / join of the round robin captures and replays correctly; tools/graph_probe.py)
+  const bool graph = (c->opt_graph == 2 && cp.kind != CallPlan::kPipeline) ||
+                     (c->opt_graph == 1 && cp.kind == CallPlan::kSingle);
   if (!graph || capturing || c->timing) return issue(c, cp, s, p, img_a, img_b, init, flow_out);
   // ~80 dependent launches per chunk: record them once as a HIP graph (on the context's own stream -- the
   // caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's stream while
