@@ -65,6 +65,7 @@ struct PatchArgs {
   float dp_thresh_sq, dr_thresh, res_thresh, outlierthresh;
   int camlr;
   int wave_per_patch;                         // 1: force the one-wave-per-patch kernel (A/B testing)
+  int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;

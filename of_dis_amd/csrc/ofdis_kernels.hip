@@ -26,6 +26,9 @@
 #pragma clang fp contract(off)
 
 namespace ofdis {
+// 16-byte vector with 4-byte alignment: dword-aligned global_load_dwordx4 (gfx950 allows unaligned vector loads)
+typedef float float4_u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float float4_v __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -748,6 +751,300 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
 #pragma unroll
   for (int k = 0; k < PAIRS; ++k) pwo[s8 + 8 * k] = pw[k];
   if (ODD && s8 < 4) pwo[8 * PAIRS + s8] = pw[PAIRS];
+}
+
+// ---------------------------------------------------------------- DIS patches, windowed (eight lanes per patch)
+// Same lane layout, reduction trees and per-patch arithmetic as k_patch8, but the bilinear taps come from
+// LDS: per iteration the eight lanes of a patch copy its (p+1) x (p+1) x noc sample window (rows of
+// contiguous floats) from the target image with 16-byte loads into an LDS tile, then read the four taps of
+// each value there (two ds_read2_b32: (D, C) and (B, A)).  Against four 4-byte gathers per value from L1 this
+// issues (p+1) * ceil((p+1) noc / 4) / 8 vector loads per lane instead of 4 p^2 noc / 8 (p = 12: 7 instead
+// of 72), which is what bounds the gather form (waves parked on vmcnt).  The loss weights of the last
+// evaluation are not kept in registers: one more evaluation at the final position writes them (the
+// evaluation is a pure function of the position: the same bits).
+template <int P, int NOC>
+struct PatchShape {
+  static constexpr int NV = P * P * NOC;
+  static constexpr int PAIRS = NV / 8;
+  static constexpr int ODD = (NV / 4) & 1;
+  static constexpr int V = PAIRS + ODD;
+  static constexpr int WR = (P + 1) * NOC;  // window row (floats)
+  static constexpr int Q4 = (WR + 3) / 4;   // 16-byte loads per window row
+  static constexpr int RS = Q4 * 4;         // LDS row stride (floats)
+  static constexpr int WIN = (P + 1) * RS + 4;  // LDS floats per patch (+4: spreads the 8 patches over banks)
+  static constexpr int NQ = (P + 1) * Q4;   // 16-byte loads per window
+  static constexpr int LPL = (NQ + 7) / 8;  // ... per lane
+  // value v -> v + 8 KP advances the tap offsets by whole patch rows: KP = lcm(8, NV / P) / 8
+  static constexpr int ROWV = P * NOC;
+  static constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
+  static constexpr int KP = (8 / gcd(8, ROWV) * ROWV) / 8;
+  static constexpr int KROWS = 8 * KP / ROWV;  // patch rows per KP values of a lane
+};
+
+// Eigen's SSE redux order (see grp_eigen_sum), accumulated value by value: add(k, x) for k = 0 .. V-1 in order.
+template <int PAIRS, int ODD>
+struct EigenAcc {
+  float acc = 0.0f, tail = 0.0f;
+  __device__ __forceinline__ void add(int k, float x) {
+    if (k < PAIRS)
+      acc = k == 0 ? x : acc + x;
+    else
+      tail = x;
+  }
+  __device__ __forceinline__ float total() const {
+    float r;
+    if (PAIRS > 0) {
+      r = acc + grp_xor4(acc);
+      if (ODD) r = r + tail;
+    } else {
+      r = tail;
+    }
+    r = r + grp_xor2(r);
+    return r + grp_xor1(r);
+  }
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NOP, int P, int NOC>
+__global__ __launch_bounds__(256) void k_patchw(PatchArgs a) {
+  using S = PatchShape<P, NOC>;
+  constexpr int PAIRS = S::PAIRS, ODD = S::ODD, V = S::V, RS = S::RS;
+  extern __shared__ __attribute__((aligned(16))) float win_all[];
+  const LevelGeom &g = a.g;
+  const int s8 = threadIdx.x & 7;
+  const long gp = (long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const bool live = gp < (long)a.n * g.npatch;
+  const long gq = live ? gp : 0;
+  const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
+  const int pxi = ip / g.noph, pyi = ip % g.noph;
+  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+  const long fs = (long)g.W * g.H * NOC;
+  const int W = g.W;
+  const float inv_n = 1.0f / (float)S::NV;
+  constexpr bool pow2 = (S::NV & (S::NV - 1)) == 0;  // x / n == x * (1/n) exactly for n = 2^k
+  auto div_n = [&](float x) { return pow2 ? x * inv_n : x / (float)S::NV; };
+  float *win = win_all + (threadIdx.x >> 3) * S::WIN;
+  // value of slot k of this lane, and its D-tap offset in the window tile
+  auto value = [&](int k) { return k < PAIRS ? s8 + 8 * k : 8 * PAIRS + (s8 & 3); };
+  auto dtap = [&](int v) {
+    const int ch = v % NOC, q = v / NOC;
+    return (q / P) * RS + (q % P) * NOC + ch;
+  };
+  int dbase[S::KP < V ? S::KP : V];
+#pragma unroll
+  for (int k = 0; k < (S::KP < V ? S::KP : V); ++k) dbase[k] = dtap(value(k));
+  const int dtail = dtap(value(V - 1));
+  auto doff = [&](int k) {  // compile-time k
+    if (ODD && k == V - 1) return dtail;
+    return dbase[k % S::KP] + (k / S::KP) * S::KROWS * RS;
+  };
+  // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
+  float tmp[V], gx[V], gy[V];
+  {
+    const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
+    const long base = ((long)(py - P / 2) * W + (px - P / 2)) * NOC;
+    const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const int v = value(k), ch = v % NOC, q = v / NOC;
+      const int o = ((q / P) * W + (q % P)) * NOC + ch;
+      tmp[k] = A[o];
+      gx[k] = DX[o];
+      gy[k] = DY[o];
+    }
+  }
+  if (a.patnorm > 0) {
+    EigenAcc<PAIRS, ODD> m;
+#pragma unroll
+    for (int k = 0; k < V; ++k) m.add(k, tmp[k]);
+    const float mean = div_n(m.total());
+#pragma unroll
+    for (int k = 0; k < V; ++k) tmp[k] = tmp[k] - mean;
+  }
+  // ---- ComputeHessian (patch.cpp:69-86)
+  float H00, H01 = 0.0f, H11 = 0.0f;
+  {
+    EigenAcc<PAIRS, ODD> h0, h1, h2;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      h0.add(k, gx[k] * gx[k]);
+      if (NOP == 2) {
+        h1.add(k, gx[k] * gy[k]);
+        h2.add(k, gy[k] * gy[k]);
+      }
+    }
+    H00 = h0.total();
+    if (NOP == 2) {
+      H01 = h1.total();
+      H11 = h2.total();
+      if (H00 * H11 - H01 * H01 == 0.0f) {
+        H00 = (float)((double)H00 + 1e-10);
+        H11 = (float)((double)H11 + 1e-10);
+      }
+    } else if (H00 == 0.0f) {
+      H00 = (float)((double)H00 + 1e-10);
+    }
+  }
+  const Llt2 fac = llt2_factor(H00, H01, H11);
+  const float fac1 = llt1_factor(H00);
+  if (a.stage == 1) {  // timing diagnostic "pconst": construction only; one store keeps the work alive
+    if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1];
+    return;
+  }
+  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
+  float pin0 = 0.0f, pin1 = 0.0f;
+  if (a.prev) {
+    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
+    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
+    pin0 = pv[0] * 2;
+    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  if (a.stage == 2) {  // "pconst + pinit": construction and initialisation
+    if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1] + pin0 + pin1;
+    return;
+  }
+  const float *Bimg = a.img_b + f * fs;
+  // window loads of this lane: float4 e = s8 + 8 j of the (P+1) x Q4 tile
+  int gofs[S::LPL], lofs[S::LPL];
+#pragma unroll
+  for (int j = 0; j < S::LPL; ++j) {
+    const int e = s8 + 8 * j, e2 = e < S::NQ ? e : S::NQ - 1;
+    const int row = e2 / S::Q4, c4 = e2 % S::Q4;
+    gofs[j] = row * W * NOC + c4 * 4;
+    lofs[j] = row * RS + c4 * 4;
+  }
+  // ---- OptimizeStart (patch.cpp:117-154)
+  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
+  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
+  const float st0 = pt0, st1 = pt1;
+  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
+  int cnt = 0;
+  bool converged = !live;
+  float b0 = 0.0f, b1 = 0.0f;
+  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1):
+  // the residual sums r0 = sum |w|, b0 = sum dx e (, b1 = sum dy e); with `out`, the weights w are stored
+  auto evaluate = [&](float &r0, float *out) {
+    const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
+    const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
+    const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
+    const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
+    const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+    // window origin: the D tap of value 0, one row above and one column left of the A tap
+    const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
+    wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
+#pragma unroll
+    for (int j = 0; j < S::LPL; ++j) {
+      const float4_u t = *reinterpret_cast<const float4_u *>(Q + gofs[j]);
+      if (s8 + 8 * j < S::NQ) *reinterpret_cast<float4_v *>(win + lofs[j]) = t;
+    }
+    wave_lds_sync();
+    float pd[V];
+    EigenAcc<PAIRS, ODD> m;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float *t = win + doff(k);
+      const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
+      pd[k] = w0 * A + w1 * Bv + w2 * C + w3 * D;
+      m.add(k, pd[k]);
+    }
+    if (a.patnorm > 0) {
+      const float mean = div_n(m.total());
+#pragma unroll
+      for (int k = 0; k < V; ++k) pd[k] = pd[k] - mean;
+    }
+    EigenAcc<PAIRS, ODD> ab, ex, ey;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float d = pd[k] - tmp[k];
+      float w, e;
+      if (a.costfct == 0) {
+        e = d;
+        w = fabsf(d);
+      } else if (a.costfct == 1) {
+        w = sqrtf(fabsf(d));
+        e = copysignf(w, d);
+      } else {
+        w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        e = copysignf(w, d);
+      }
+      if (out) {
+        if (k < PAIRS) out[s8 + 8 * k] = w;
+        else if (s8 < 4) out[8 * PAIRS + s8] = w;
+      } else {
+        ab.add(k, fabsf(w));
+        ex.add(k, gx[k] * e);
+        if (NOP == 2) ey.add(k, gy[k] * e);
+      }
+    }
+    if (!out) {
+      r0 = ab.total();
+      b0 = ex.total();
+      if (NOP == 2) b1 = ey.total();
+    }
+  };
+  auto err = [&]() {  // OptimizeComputeErrImg (patch.cpp:275-295)
+    float r0;
+    evaluate(r0, nullptr);
+    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+    if (cnt == 1) sq_init = sq;
+    mares_old = mares;
+    mares = div_n(r0);
+    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+    if (!keep) converged = true;
+  };
+  bool start_oob = false;
+  if (!converged) {
+    if (oob(pt0, pt1)) {
+      converged = true;  // pweight stays 0: never written upstream, defined as 0
+      start_oob = true;
+    } else {
+      mares = 1e5f;
+      err();
+    }
+  }
+  // ---- OptimizeIter loop (patch.cpp:156-210)
+  while (!converged) {
+    ++cnt;
+    if (NOP == 2) {
+      llt2_solve(fac, b0, b1, d0, d1);
+      p0 = p0 - d0;
+      p1 = p1 - d1;
+    } else {
+      d0 = llt1_solve(fac1, b0);
+      p0 = p0 - d0;
+      p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+    }
+    pt0 = ptr0 + p0;
+    if (NOP == 2) pt1 = ptr1 + p1;
+    const float ex = st0 - pt0, ey = st1 - pt1;
+    if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+      p0 = pin0;
+      p1 = pin1;
+      pt0 = ptr0 + p0;
+      if (NOP == 2) pt1 = ptr1 + p1;
+      converged = true;
+    }
+    err();
+  }
+  // ---- outputs: the flow, and the loss weights of the last evaluation (re-evaluated at the final position)
+  float *pwo = a.pweight + gq * S::NV;
+  if (live && !start_oob) {
+    float r0;
+    evaluate(r0, pwo);
+  } else if (live) {
+#pragma unroll
+    for (int k = 0; k < PAIRS; ++k) pwo[s8 + 8 * k] = 0.0f;
+    if (ODD && s8 < 4) pwo[8 * PAIRS + s8] = 0.0f;
+  }
+  if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }
 
 // ------------------------------------------------------------------------------------------------ aggregation
@@ -2438,7 +2735,24 @@ static void patch8(const PatchArgs &a, hipStream_t s) {
   else
     k_patch8<1, PAIRS, ODD><<<ceil_div(patches, 32), 256, 0, s>>>(a);
 }
+template <int P, int NOC>
+static void patchw(const PatchArgs &a, hipStream_t s) {
+  const long patches = (long)a.n * a.g.npatch;
+  const size_t lds = sizeof(float) * 32 * PatchShape<P, NOC>::WIN;
+  if (a.nop == 2)
+    k_patchw<2, P, NOC><<<ceil_div(patches, 32), 256, lds, s>>>(a);
+  else
+    k_patchw<1, P, NOC><<<ceil_div(patches, 32), 256, lds, s>>>(a);
+}
 void launch_patch(const PatchArgs &a, hipStream_t s) {
+  if (a.window && !a.wave_per_patch) {  // LDS-windowed eight-lane form for the shapes of the op-points
+    switch (a.p * 4 + a.noc) {
+      case 8 * 4 + 1: patchw<8, 1>(a, s); return;
+      case 12 * 4 + 1: patchw<12, 1>(a, s); return;
+      case 8 * 4 + 3: patchw<8, 3>(a, s); return;
+      case 12 * 4 + 3: patchw<12, 3>(a, s); return;
+    }
+  }
   if (!a.wave_per_patch) {
     switch (a.novals) {  // eight lanes per patch for the common shapes
       case 64: patch8<8, 0>(a, s); return;    // p 8, gray

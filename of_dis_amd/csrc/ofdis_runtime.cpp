@@ -82,6 +82,7 @@ struct ofdis_context {
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
+  int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
@@ -227,8 +228,8 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad, bool init 
     const LevelGeom &g = P.lv[i];
     P.off_lvl[i] = off;
     off = align_up(off + sizeof(float) * 2 * (size_t)n * g.w * g.h * P.noc);
-    P.off_img[i] = off;
-    off = align_up(off + sizeof(float) * 2 * (size_t)n * g.W * g.H * P.noc);
+    P.off_img[i] = off;  // (+64 floats: the windowed patch kernel's 16-byte row loads may read past the last row)
+    off = align_up(off + sizeof(float) * (2 * (size_t)n * g.W * g.H * P.noc + 64));
     P.off_dx[i] = off;
     off = align_up(off + sizeof(float) * 2 * (size_t)n * g.W * g.H * P.noc);
     P.off_dy[i] = off;
@@ -365,6 +366,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.outlierthresh = (float)p->p_samp_s / 2;
     pa.camlr = 0;
     pa.wave_per_patch = c->opt_wave_per_patch;
+    pa.window = c->opt_patch_window;
     pa.g = g;
     if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
       PatchArgs pd = pa;
@@ -1144,6 +1146,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 2},
+      {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {
