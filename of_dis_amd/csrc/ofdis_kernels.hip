@@ -810,8 +810,9 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int NOP, int P, int NOC>
-__global__ __launch_bounds__(256) void k_patchw(PatchArgs a) {
+// MINW: waves per SIMD the register allocation must allow (amdgpu_waves_per_eu)
+template <int NOP, int P, int NOC, int MINW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchw(PatchArgs a) {
   using S = PatchShape<P, NOC>;
   constexpr int PAIRS = S::PAIRS, ODD = S::ODD, V = S::V, RS = S::RS;
   extern __shared__ __attribute__((aligned(16))) float win_all[];
@@ -2735,22 +2736,23 @@ static void patch8(const PatchArgs &a, hipStream_t s) {
   else
     k_patch8<1, PAIRS, ODD><<<ceil_div(patches, 32), 256, 0, s>>>(a);
 }
-template <int P, int NOC>
+// MINW1 / MINW2: waves per SIMD for the depth (nop 1) / flow (nop 2) forms, chosen so that nothing spills
+template <int P, int NOC, int MINW1, int MINW2>
 static void patchw(const PatchArgs &a, hipStream_t s) {
   const long patches = (long)a.n * a.g.npatch;
   const size_t lds = sizeof(float) * 32 * PatchShape<P, NOC>::WIN;
   if (a.nop == 2)
-    k_patchw<2, P, NOC><<<ceil_div(patches, 32), 256, lds, s>>>(a);
+    k_patchw<2, P, NOC, MINW2><<<ceil_div(patches, 32), 256, lds, s>>>(a);
   else
-    k_patchw<1, P, NOC><<<ceil_div(patches, 32), 256, lds, s>>>(a);
+    k_patchw<1, P, NOC, MINW1><<<ceil_div(patches, 32), 256, lds, s>>>(a);
 }
 void launch_patch(const PatchArgs &a, hipStream_t s) {
   if (a.window && !a.wave_per_patch) {  // LDS-windowed eight-lane form for the shapes of the op-points
     switch (a.p * 4 + a.noc) {
-      case 8 * 4 + 1: patchw<8, 1>(a, s); return;
-      case 12 * 4 + 1: patchw<12, 1>(a, s); return;
-      case 8 * 4 + 3: patchw<8, 3>(a, s); return;
-      case 12 * 4 + 3: patchw<12, 3>(a, s); return;
+      case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
+      case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
+      case 8 * 4 + 3: patchw<8, 3, 2, 2>(a, s); return;
+      case 12 * 4 + 3: patchw<12, 3, 1, 1>(a, s); return;
     }
   }
   if (!a.wave_per_patch) {
