@@ -151,13 +151,17 @@ int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int
  * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL). */
 int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, float *const *tv_flow, int nscales);
 
-/* Tuning / A-B switches (all exact: results never depend on them):
+/* Tuning / A-B switches:
  *   "sor_generic" (0/1): force the generic global-memory SOR wavefront;
  *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline (the default for tall levels)
  *                        instead of the sweep-per-wave SOR;
  *   "sor_cring" (0/1, default 1): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
  *                        hands them to the later sweeps through LDS (solverit <= 3);
  *   "smsys" (0/1, default 1): smoothness and system of a TV iteration in one launch;
+ *   "sor_mode" (0/1, default 0): 0 = sor_coupled's exact lexicographic order (the reference's bits);
+ *                        1 = red-black order (SURVEY §7 4(ii) throughput mode: every half-sweep fully
+ *                        parallel; a different iteration -- NOT the reference's bits, end-point error
+ *                        gated against the exact path; the one option that changes results);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch;
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
  *   "graph" (0/1/2, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
@@ -172,7 +176,7 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
  * Setting any option drops the captured graph.  Unknown keys and out-of-range values return
- * OFDIS_ERR_INVALID_ARGUMENT. */
+ * OFDIS_ERR_INVALID_ARGUMENT.  Apart from "sor_mode", results never depend on these settings. */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);
 
 /* Largest number of frame pairs one launch of the refinement kernels takes at this size (their plane groups

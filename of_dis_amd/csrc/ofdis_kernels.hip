@@ -1972,6 +1972,143 @@ __device__ __forceinline__ float sor_rhs(bool border, bool notop, float b, float
   const float r = (border ? -0.0f : b) + (border ? (notop ? Z : Y) : Z);
   return l + r;
 }
+// ---------------------------------------------------------------------------------- red-black SOR (opt-in)
+// The throughput mode of SURVEY §7 4(ii): the same per-pixel block SOR update as sor_coupled (2x2 inverse
+// precomputed by the system kernel, solver.c's right-hand-side trees via sor_rhs) but in red-black order --
+// all pixels with x + y even, then all odd ones, 2 * solverit half-sweeps -- instead of the lexicographic
+// order, so every half-sweep is fully parallel.  A different iteration: results are NOT the reference's bits;
+// the parity gate is an end-point tolerance (tests/test_gpu_redblack.py).  MODE 0: OF block SOR, 2: DE
+// point SOR.
+struct RbPix {
+  float i11, i12, i22, b1, b2, hr, hl, vb, vt;
+};
+template <int MODE>
+__device__ __forceinline__ RbPix rb_load(const TvArgs &a, int f, int x, int y) {
+  const float4 *C = reinterpret_cast<const float4 *>(a.coef);
+  const long fo = (long)f * a.sp;
+  const long o = fo + skw(x, y, a.h, a.w, a.wrap);
+  RbPix d;
+  if (MODE == 0) {
+    const float4 c0 = C[2 * o], c1 = C[2 * o + 1];
+    d.i11 = c0.x; d.i12 = c0.y; d.i22 = c0.w; d.b1 = c1.x; d.b2 = c1.y; d.hr = c1.z; d.vb = c1.w;
+    d.hl = x > 0 ? C[2 * (fo + skw(x - 1, y, a.h, a.w, a.wrap)) + 1].z : 0.0f;
+    d.vt = y > 0 ? C[2 * (fo + skw(x, y - 1, a.h, a.w, a.wrap)) + 1].w : 0.0f;
+  } else {
+    const float4 c0 = C[o];
+    d.i11 = c0.x; d.i12 = 0.0f; d.i22 = 0.0f; d.b1 = c0.y; d.b2 = 0.0f; d.hr = c0.z; d.vb = c0.w;
+    d.hl = x > 0 ? C[fo + skw(x - 1, y, a.h, a.w, a.wrap)].z : 0.0f;
+    d.vt = y > 0 ? C[fo + skw(x, y - 1, a.h, a.w, a.wrap)].w : 0.0f;
+  }
+  return d;
+}
+// One pixel's update from its four neighbours' current values (l, r, t, b; OF: u and v).
+template <int MODE>
+__device__ __forceinline__ void rb_update(const RbPix &d, int x, int y, int w, int h, float omega, float ul,
+                                          float ur, float ut, float ub, float vl, float vr, float vt, float vb,
+                                          float &u, float &v) {
+  const bool border = y == 0 || y >= h - 1, notop = y == 0;
+  ur = x < w - 1 ? ur : 0.0f;
+  vr = x < w - 1 ? vr : 0.0f;
+  if (MODE == 0) {
+    const float s1 = sor_rhs(border, notop, d.b1, d.hr * ur, d.vt * ut, d.vb * ub);
+    const float s2 = sor_rhs(border, notop, d.b2, d.hr * vr, d.vt * vt, d.vb * vb);
+    const float B1 = x > 0 ? d.hl * ul + s1 : s1;
+    const float B2 = x > 0 ? d.hl * vl + s2 : s2;
+    const float nu = u + omega * (d.i11 * B1 + d.i12 * B2 - u);
+    v = v + omega * (d.i12 * B1 + d.i22 * B2 - v);
+    u = nu;
+  } else {
+    float su = 0.0f, sd = 0.0f;
+    if (y > 0) { su = su - d.vt * ut; sd = sd + d.vt; }
+    if (x > 0) { su = su - d.hl * ul; sd = sd + d.hl; }
+    if (y < h - 1) { su = su - d.vb * ub; sd = sd + d.vb; }
+    if (x < w - 1) { su = su - d.hr * ur; sd = sd + d.hr; }
+    const float A = d.i11 + sd, Bv = d.b1 - su;
+    u = (1.0f - omega) * u + omega * (Bv / A);
+  }
+}
+
+// Whole red-black SOR call of one frame in one workgroup (levels of <= kRbPix pixels): u (, v) live in LDS,
+// row-major; each thread keeps its pixels' coefficients in registers for all 2 S half-sweeps.
+constexpr int kRbThreads = 1024, kRbPpt = 8, kRbPix = kRbThreads * kRbPpt;
+template <int MODE>
+__global__ __launch_bounds__(kRbThreads) void k_tv_sor_rb_lds(TvArgs a) {
+  extern __shared__ float rb_uv[];  // u [w*h], then v [w*h] (OF)
+  const int f = blockIdx.x, w = a.w, h = a.h, n = w * h;
+  float *U = rb_uv, *Vv = rb_uv + n;
+  const long fo = (long)f * a.sp;
+  RbPix d[kRbPpt];
+#pragma unroll
+  for (int k = 0; k < kRbPpt; ++k) {
+    const int p = threadIdx.x + k * kRbThreads;
+    if (p < n) {
+      const int x = p % w, y = p / w;
+      d[k] = rb_load<MODE>(a, f, x, y);
+      const long o = fo + skw(x, y, h, w, a.wrap);
+      U[p] = a.du[o];
+      if (MODE == 0) Vv[p] = a.dv[o];
+    }
+  }
+  __syncthreads();
+  for (int it = 0; it < 2 * a.solverit; ++it) {
+    const int color = it & 1;
+#pragma unroll
+    for (int k = 0; k < kRbPpt; ++k) {
+      const int p = threadIdx.x + k * kRbThreads;
+      if (p >= n) continue;
+      const int x = p % w, y = p / w;
+      if (((x + y) & 1) != color) continue;
+      const float ul = x > 0 ? U[p - 1] : 0.0f, ur = x < w - 1 ? U[p + 1] : 0.0f;
+      const float ut = y > 0 ? U[p - w] : 0.0f, ub = y < h - 1 ? U[p + w] : 0.0f;
+      float vl = 0.0f, vr = 0.0f, vt = 0.0f, vb = 0.0f, v = 0.0f;
+      if (MODE == 0) {
+        vl = x > 0 ? Vv[p - 1] : 0.0f; vr = x < w - 1 ? Vv[p + 1] : 0.0f;
+        vt = y > 0 ? Vv[p - w] : 0.0f; vb = y < h - 1 ? Vv[p + w] : 0.0f;
+        v = Vv[p];
+      }
+      float u = U[p];
+      rb_update<MODE>(d[k], x, y, w, h, a.omega, ul, ur, ut, ub, vl, vr, vt, vb, u, v);
+      U[p] = u;
+      if (MODE == 0) Vv[p] = v;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < kRbPpt; ++k) {
+    const int p = threadIdx.x + k * kRbThreads;
+    if (p < n) {
+      const long o = fo + skw(p % w, p / w, h, w, a.wrap);
+      a.du[o] = U[p];
+      if (MODE == 0) a.dv[o] = Vv[p];
+    }
+  }
+}
+
+// One half-sweep of one colour over global memory (larger levels): thread = pixel.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_tv_sor_rb(TvArgs a, int color) {
+  const int p = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y, w = a.w, h = a.h;
+  if (p >= w * h) return;
+  const int x = p % w, y = p / w;
+  if (((x + y) & 1) != color) return;
+  const long fo = (long)f * a.sp;
+  const RbPix d = rb_load<MODE>(a, f, x, y);
+  auto at = [&](int xx, int yy) { return fo + skw(xx, yy, h, w, a.wrap); };
+  const long o = at(x, y);
+  const float ul = x > 0 ? a.du[at(x - 1, y)] : 0.0f, ur = x < w - 1 ? a.du[at(x + 1, y)] : 0.0f;
+  const float ut = y > 0 ? a.du[at(x, y - 1)] : 0.0f, ub = y < h - 1 ? a.du[at(x, y + 1)] : 0.0f;
+  float vl = 0.0f, vr = 0.0f, vt = 0.0f, vb = 0.0f, v = 0.0f;
+  if (MODE == 0) {
+    vl = x > 0 ? a.dv[at(x - 1, y)] : 0.0f; vr = x < w - 1 ? a.dv[at(x + 1, y)] : 0.0f;
+    vt = y > 0 ? a.dv[at(x, y - 1)] : 0.0f; vb = y < h - 1 ? a.dv[at(x, y + 1)] : 0.0f;
+    v = a.dv[o];
+  }
+  float u = a.du[o];
+  rb_update<MODE>(d, x, y, w, h, a.omega, ul, ur, ut, ub, vl, vr, vt, vb, u, v);
+  a.du[o] = u;
+  if (MODE == 0) a.dv[o] = v;
+}
+
 // Register-pipelined exact-order SOR: thread = row y (h <= 1024), one workgroup per frame.  At step t the
 // thread runs sweep s on pixel x_s = t - y - 2 s for every s < S.  Left/right/own values come from its own
 // registers (results of steps t-1 / t-2), top/bottom values from the neighbouring lanes by DPP (through LDS
@@ -2878,6 +3015,21 @@ static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
   const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);  // point SOR (solver.c:34-78)
+  if (a.sor_redblack && !tiny) {  // opt-in red-black order (not the reference's bits)
+    const int n = a.w * a.h;
+    if (n <= kRbPix) {
+      const size_t lds = sizeof(float) * (size_t)n * (a.nop == 2 ? 2 : 1);
+      if (a.nop == 2) k_tv_sor_rb_lds<0><<<a.n, kRbThreads, lds, s>>>(a);
+      else k_tv_sor_rb_lds<2><<<a.n, kRbThreads, lds, s>>>(a);
+    } else {
+      const dim3 grid(ceil_div(n, 256), a.n);
+      for (int it = 0; it < 2 * a.solverit; ++it) {
+        if (a.nop == 2) k_tv_sor_rb<0><<<grid, 256, 0, s>>>(a, it & 1);
+        else k_tv_sor_rb<2><<<grid, 256, 0, s>>>(a, it & 1);
+      }
+    }
+    return;
+  }
   const int G = (a.h + 63) / 64;
   if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && G * a.solverit <= 16) {
     switch (a.solverit) {

@@ -82,6 +82,7 @@ struct ofdis_context {
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
+  int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
@@ -473,6 +474,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_cring = c->opt_sor_cring;
       tv.smsys = c->opt_smsys;
+      tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
       timed(c, 6, s, [&] {
@@ -1147,6 +1149,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 2},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
+      {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {
