@@ -779,6 +779,9 @@ struct PatchShape {
   static constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
   static constexpr int KP = (8 / gcd(8, ROWV) * ROWV) / 8;
   static constexpr int KROWS = 8 * KP / ROWV;  // patch rows per KP values of a lane
+  // big shapes (p = 12 RGB: 54 values per lane) trade registers for LDS reads: the taps are read twice (for
+  // the mean, then for the loss) instead of keeping the samples, and the window offsets are recomputed
+  static constexpr bool LEAN = V > 24;
 };
 
 // Eigen's SSE redux order (see grp_eigen_sum), accumulated value by value: add(k, x) for k = 0 .. V-1 in order.
@@ -911,13 +914,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   const float *Bimg = a.img_b + f * fs;
   // window loads of this lane: float4 e = s8 + 8 j of the (P+1) x Q4 tile
-  int gofs[S::LPL], lofs[S::LPL];
-#pragma unroll
-  for (int j = 0; j < S::LPL; ++j) {
+  constexpr int LPLK = S::LEAN ? 1 : S::LPL;
+  int gofs[LPLK], lofs[LPLK];
+  auto woff = [&](int j, int &go, int &lo) {
     const int e = s8 + 8 * j, e2 = e < S::NQ ? e : S::NQ - 1;
     const int row = e2 / S::Q4, c4 = e2 % S::Q4;
-    gofs[j] = row * W * NOC + c4 * 4;
-    lofs[j] = row * RS + c4 * 4;
+    go = row * W * NOC + c4 * 4;
+    lo = row * RS + c4 * 4;
+  };
+  if (!S::LEAN) {
+#pragma unroll
+    for (int j = 0; j < LPLK; ++j) woff(j, gofs[j], lofs[j]);
   }
   // ---- OptimizeStart (patch.cpp:117-154)
   float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
@@ -939,30 +946,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     // window origin: the D tap of value 0, one row above and one column left of the A tap
     const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
     wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
+    if (S::LEAN) {  // in batches of 4 loads: bounded registers in flight
 #pragma unroll
-    for (int j = 0; j < S::LPL; ++j) {
-      const float4_u t = *reinterpret_cast<const float4_u *>(Q + gofs[j]);
-      if (s8 + 8 * j < S::NQ) *reinterpret_cast<float4_v *>(win + lofs[j]) = t;
+      for (int j0 = 0; j0 < S::LPL; j0 += 4) {
+        float4_u t[4];
+        int lo[4];
+#pragma unroll
+        for (int j = j0; j < j0 + 4 && j < S::LPL; ++j) {
+          int go;
+          woff(j, go, lo[j - j0]);
+          t[j - j0] = *reinterpret_cast<const float4_u *>(Q + go);
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + 4 && j < S::LPL; ++j)
+          if (s8 + 8 * j < S::NQ) *reinterpret_cast<float4_v *>(win + lo[j - j0]) = t[j - j0];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < S::LPL; ++j) {
+        const float4_u t = *reinterpret_cast<const float4_u *>(Q + gofs[j]);
+        if (s8 + 8 * j < S::NQ) *reinterpret_cast<float4_v *>(win + lofs[j]) = t;
+      }
     }
     wave_lds_sync();
-    float pd[V];
-    EigenAcc<PAIRS, ODD> m;
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
+    auto sample = [&](int k) {
       const float *t = win + doff(k);
       const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
-      pd[k] = w0 * A + w1 * Bv + w2 * C + w3 * D;
-      m.add(k, pd[k]);
-    }
-    if (a.patnorm > 0) {
-      const float mean = div_n(m.total());
+      return w0 * A + w1 * Bv + w2 * C + w3 * D;
+    };
+    constexpr int VK = S::LEAN ? 1 : V;
+    float pd[VK];
+    float mean = 0.0f;
+    if (a.patnorm > 0 || !S::LEAN) {
+      EigenAcc<PAIRS, ODD> m;
 #pragma unroll
-      for (int k = 0; k < V; ++k) pd[k] = pd[k] - mean;
+      for (int k = 0; k < V; ++k) {
+        const float x = sample(k);
+        if (!S::LEAN) pd[k] = x;
+        m.add(k, x);
+      }
+      if (a.patnorm > 0) mean = div_n(m.total());
     }
     EigenAcc<PAIRS, ODD> ab, ex, ey;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const float d = pd[k] - tmp[k];
+      float x = S::LEAN ? sample(k) : pd[k];
+      if (a.patnorm > 0) x = x - mean;
+      const float d = x - tmp[k];
       float w, e;
       if (a.costfct == 0) {
         e = d;
@@ -2889,8 +2919,7 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
       case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
       case 8 * 4 + 3: patchw<8, 3, 2, 2>(a, s); return;
-      // p = 12 RGB (432 values, 54 per lane) needs ~400 registers in this form: one wave per SIMD measured
-      // 38 % slower than the one-wave-per-patch k_patch (config C: 29.7 vs 21.5 ms per step)
+      case 12 * 4 + 3: patchw<12, 3, 2, 2>(a, s); return;
     }
   }
   if (!a.wave_per_patch) {
