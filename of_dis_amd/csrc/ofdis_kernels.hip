@@ -932,7 +932,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   const float st0 = pt0, st1 = pt1;
   float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
   int cnt = 0;
-  bool converged = !live;
+  bool converged = false;
   float b0 = 0.0f, b1 = 0.0f;
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1):
@@ -1019,61 +1019,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (NOP == 2) b1 = ey.total();
     }
   };
-  auto err = [&]() {  // OptimizeComputeErrImg (patch.cpp:275-295)
-    float r0;
-    evaluate(r0, nullptr);
-    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
-    if (cnt == 1) sq_init = sq;
-    mares_old = mares;
-    mares = div_n(r0);
-    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
-                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
-                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
-    if (!keep) converged = true;
-  };
-  bool start_oob = false;
-  if (!converged) {
-    if (oob(pt0, pt1)) {
-      converged = true;  // pweight stays 0: never written upstream, defined as 0
-      start_oob = true;
-    } else {
-      mares = 1e5f;
-      err();
-    }
-  }
-  // ---- OptimizeIter loop (patch.cpp:156-210)
-  while (!converged) {
-    ++cnt;
-    if (NOP == 2) {
-      llt2_solve(fac, b0, b1, d0, d1);
-      p0 = p0 - d0;
-      p1 = p1 - d1;
-    } else {
-      d0 = llt1_solve(fac1, b0);
-      p0 = p0 - d0;
-      p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
-    }
-    pt0 = ptr0 + p0;
-    if (NOP == 2) pt1 = ptr1 + p1;
-    const float ex = st0 - pt0, ey = st1 - pt1;
-    if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
-      p0 = pin0;
-      p1 = pin1;
-      pt0 = ptr0 + p0;
-      if (NOP == 2) pt1 = ptr1 + p1;
-      converged = true;
-    }
-    err();
-  }
-  // ---- outputs: the flow, and the loss weights of the last evaluation (re-evaluated at the final position)
+  // One evaluation site for the start evaluation, every iteration and the final weight store (the kernel body
+  // is unrolled over the values: one copy keeps it inside the instruction cache).  Per patch:
+  //   OptimizeStart (patch.cpp:117-154): evaluate at the start position (unless it is out of bounds);
+  //   OptimizeIter (patch.cpp:156-210): while not converged, solve, update, outlier reset, evaluate;
+  //   then one more evaluation at the final position that stores the loss weights.
   float *pwo = a.pweight + gq * S::NV;
-  if (live && !start_oob) {
-    float r0;
-    evaluate(r0, pwo);
-  } else if (live) {
+  bool done = !live, store = false, first = true;
+  if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
 #pragma unroll
     for (int k = 0; k < PAIRS; ++k) pwo[s8 + 8 * k] = 0.0f;
     if (ODD && s8 < 4) pwo[8 * PAIRS + s8] = 0.0f;
+    done = true;
+  } else {
+    mares = 1e5f;
+  }
+  while (!done) {
+    if (!first && !store) {
+      ++cnt;
+      if (NOP == 2) {
+        llt2_solve(fac, b0, b1, d0, d1);
+        p0 = p0 - d0;
+        p1 = p1 - d1;
+      } else {
+        d0 = llt1_solve(fac1, b0);
+        p0 = p0 - d0;
+        p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+      }
+      pt0 = ptr0 + p0;
+      if (NOP == 2) pt1 = ptr1 + p1;
+      const float ex = st0 - pt0, ey = st1 - pt1;
+      if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+        p0 = pin0;
+        p1 = pin1;
+        pt0 = ptr0 + p0;
+        if (NOP == 2) pt1 = ptr1 + p1;
+        converged = true;
+      }
+    }
+    float r0 = 0.0f;
+    evaluate(r0, store ? pwo : nullptr);
+    if (store) {
+      done = true;
+    } else {  // OptimizeComputeErrImg (patch.cpp:275-295)
+      sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+      if (cnt == 1) sq_init = sq;
+      mares_old = mares;
+      mares = div_n(r0);
+      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                        ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                        ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+      if (!keep) converged = true;
+      store = converged;
+    }
+    first = false;
   }
   if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }
