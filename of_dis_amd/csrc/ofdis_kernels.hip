@@ -937,7 +937,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1):
   // the residual sums r0 = sum |w|, b0 = sum dx e (, b1 = sum dy e); with `out`, the weights w are stored
-  auto evaluate = [&](float &r0, float *out) {
+  auto evaluate = [&](float &r0, float *out, auto store_t) {
+    constexpr int STORE = decltype(store_t)::value;  // 1: weights only (the final store), 0: sums only, 2: runtime
     const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
     const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
@@ -1004,23 +1005,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
         e = copysignf(w, d);
       }
-      if (out) {
+      if (STORE == 1 || (STORE == 2 && out)) {
         if (k < PAIRS) out[s8 + 8 * k] = w;
         else if (s8 < 4) out[8 * PAIRS + s8] = w;
-      } else {
+      }
+      if (STORE == 0 || (STORE == 2 && !out)) {
         ab.add(k, fabsf(w));
         ex.add(k, gx[k] * e);
         if (NOP == 2) ey.add(k, gy[k] * e);
       }
     }
-    if (!out) {
+    if (STORE == 0 || (STORE == 2 && !out)) {
       r0 = ab.total();
       b0 = ex.total();
       if (NOP == 2) b1 = ey.total();
     }
   };
-  // One evaluation site for the start evaluation, every iteration and the final weight store (the kernel body
-  // is unrolled over the values: one copy keeps it inside the instruction cache).  Per patch:
+  // Big shapes (LEAN): one evaluation site for the start evaluation, every iteration and the final weight store
+  // (the body is unrolled over the values: one copy keeps it inside the instruction cache); smaller shapes
+  // keep a separate weights-only copy for the final store (no per-value branch in the loop).  Per patch:
   //   OptimizeStart (patch.cpp:117-154): evaluate at the start position (unless it is out of bounds);
   //   OptimizeIter (patch.cpp:156-210): while not converged, solve, update, outlier reset, evaluate;
   //   then one more evaluation at the final position that stores the loss weights.
@@ -1058,7 +1061,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     }
     float r0 = 0.0f;
-    evaluate(r0, store ? pwo : nullptr);
+    if (S::LEAN) {
+      evaluate(r0, store ? pwo : nullptr, std::integral_constant<int, 2>());
+    } else if (store) {
+      evaluate(r0, pwo, std::integral_constant<int, 1>());
+    } else {
+      evaluate(r0, nullptr, std::integral_constant<int, 0>());
+    }
     if (store) {
       done = true;
     } else {  // OptimizeComputeErrImg (patch.cpp:275-295)
