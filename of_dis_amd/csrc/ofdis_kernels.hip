@@ -1021,23 +1021,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (NOP == 2) b1 = ey.total();
     }
   };
-  // Big shapes (LEAN): one evaluation site for the start evaluation, every iteration and the final weight store
-  // (the body is unrolled over the values: one copy keeps it inside the instruction cache); smaller shapes
-  // keep a separate weights-only copy for the final store (no per-value branch in the loop).  Per patch:
+  // The evaluation is unrolled over the values; the loop holds one copy of it (start evaluation and every
+  // iteration), the final weights-only evaluation another (big shapes, LEAN: one copy for all three, with a
+  // runtime store flag, to stay inside the instruction cache).  Per patch:
   //   OptimizeStart (patch.cpp:117-154): evaluate at the start position (unless it is out of bounds);
   //   OptimizeIter (patch.cpp:156-210): while not converged, solve, update, outlier reset, evaluate;
   //   then one more evaluation at the final position that stores the loss weights.
   float *pwo = a.pweight + gq * S::NV;
-  bool done = !live, store = false, first = true;
+  bool start_oob = false, first = true, store = false;
+  converged = !live;
   if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
 #pragma unroll
     for (int k = 0; k < PAIRS; ++k) pwo[s8 + 8 * k] = 0.0f;
     if (ODD && s8 < 4) pwo[8 * PAIRS + s8] = 0.0f;
-    done = true;
+    converged = true;
+    start_oob = true;
   } else {
     mares = 1e5f;
   }
-  while (!done) {
+  while (!converged || (S::LEAN && store)) {
     if (!first && !store) {
       ++cnt;
       if (NOP == 2) {
@@ -1063,25 +1065,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     float r0 = 0.0f;
     if (S::LEAN) {
       evaluate(r0, store ? pwo : nullptr, std::integral_constant<int, 2>());
-    } else if (store) {
-      evaluate(r0, pwo, std::integral_constant<int, 1>());
+      if (store) {
+        store = false;
+        break;
+      }
     } else {
       evaluate(r0, nullptr, std::integral_constant<int, 0>());
     }
-    if (store) {
-      done = true;
-    } else {  // OptimizeComputeErrImg (patch.cpp:275-295)
-      sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
-      if (cnt == 1) sq_init = sq;
-      mares_old = mares;
-      mares = div_n(r0);
-      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
-                        ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
-                        ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
-      if (!keep) converged = true;
-      store = converged;
-    }
+    // OptimizeComputeErrImg (patch.cpp:275-295)
+    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+    if (cnt == 1) sq_init = sq;
+    mares_old = mares;
+    mares = div_n(r0);
+    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+    if (!keep) converged = true;
+    if (S::LEAN && converged) store = true;
     first = false;
+  }
+  if (!S::LEAN && live && !start_oob) {
+    float r0;
+    evaluate(r0, pwo, std::integral_constant<int, 1>());
   }
   if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }
