@@ -35,7 +35,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # BASELINE.json configs -> (binary, width, height, noc, mode, oppoint, explicit 20 parameters or None, batch)
 CONFIGS = {
     "A": ("run_OF_INT", 640, 480, 1, 1, 2, None, 1024),
-    "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 1024),
+    # 2048 pairs per GPU per step = two 1024-pair chunks on two streams (measured best: 1024 pairs 266k,
+    # 1536 282k, 2048 298k, 3072 285k, 4096 293k MPix/s; profiles/r02/sweep3)
+    "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 2048),
     # op-point 3 as the config text states it ("finer scale, L1 cost"): op3 values with costfct = 1
     "C": ("run_OF_RGB", 1920, 1080, 3, 1, 3, "6 2 16 16 0.05 0.95 0 12 0.75 0 1 1 1 10 10 5 1 3 1.6 2", 64),
     # op-point 3 as run_dense.cpp:248-253 defines it (costfct 0, L2); SURVEY §8(d): report both
