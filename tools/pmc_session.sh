@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $c"; date
   timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/$c" -o run --output-format csv -- \
-    python bench.py --steps 2 --warmup 1 --batch "$B" --no-kernel-timing --cpu-seconds 0 > "$OUT/$c.log" 2>&1
+    python bench.py --steps 2 --warmup 1 --batch "$B" --no-kernel-timing --cpu-seconds 0 --no-latency > "$OUT/$c.log" 2>&1
   rc=$?
   echo "== pmc $c rc=$rc"; tail -n 3 "$OUT/$c.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
