@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-pair latency leg")
     ap.add_argument("--dry-run", action="store_true", help="rank/shard bookkeeping on gloo, no GPU (CPU test)")
+    ap.add_argument("--parity-frames", type=int, default=8,
+                    help="timed-pass frames re-checked against the CPU oracle on rank 0 (1 per rank at N > 1)")
     return ap.parse_args()
 
 
@@ -375,7 +377,7 @@ def main():
     if args.cpu_seconds > 0:
         from oracle import pyoracle as O
         q = oracle_params(O, p)
-        ncmp = nd if world == 1 else 1
+        ncmp = max(1, min(nd, args.parity_frames)) if world == 1 else 1
         for k in range(ncmp):
             ref = O.run_u8(pairs[k][0], pairs[k][1], q)
             g = timed_out[k]
