@@ -249,7 +249,8 @@ def test_oflow_hpp_dropin_program(oracle, od, tmp_path):
 
 
 @pytest.mark.parametrize("exe_name,noc,mode,over", [("run_OF_INT", 1, 1, {}), ("run_OF_RGB", 3, 1, {}),
-                                                     ("run_DE_INT", 1, 2, {}), ("run_OF_GRAD", 1, 1, {"gradmag": 1}),
+                                                     ("run_DE_INT", 1, 2, {}), ("run_DE_RGB", 3, 2, {}),
+                                                     ("run_OF_GRAD", 1, 1, {"gradmag": 1}),
                                                      ("run_DE_GRAD", 1, 2, {"gradmag": 1}),
                                                      ("run_OF_INT_OMP", 1, 1, {"omp_build": 1})])
 def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode, over):
@@ -312,3 +313,33 @@ def test_auto_two_streams_bitexact(oracle, od, ctx):
     for f in (0, 259, 260, 519):  # first / last frame of each 260-pair chunk
         ref = oracle.run_u8(pairs[f % nd][0], pairs[f % nd][1], q)
         assert_bitexact(auto[f], ref, f"frame {f}")
+
+
+def test_cli_stdout_timers(od, tmp_path):
+    """run_OF_INT at the default verbosity 2 prints the reference's stdout timers in its order
+    (run_dense.cpp:319,352,428; oflow.cpp:177,297,336), with the per-scale patch counts."""
+    import os
+    import re
+    import subprocess
+    w, h = 640, 480
+    a, b = od.synth_pair(w, h, 1, 2, 1)
+    for name, im in (("a.pgm", a), ("b.pgm", b)):
+        (tmp_path / name).write_bytes(f"P5\n{w} {h}\n255\n".encode() + im.tobytes())
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "of_dis_amd", "bin", "run_OF_INT")
+    r = subprocess.run([exe, str(tmp_path / "a.pgm"), str(tmp_path / "b.pgm"), str(tmp_path / "o.flo")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("TIME")]
+    heads = [re.match(r"TIME \(([^)]*)\)", ln).group(1).split(",")[0].strip() for ln in lines]
+    assert heads[:3] == ["Image loading", "Pyramide+Gradients", "Grid Memo. Alloc."], heads
+    assert heads[-2:] == ["O.Flow Run-Time", "Saving flow file"], heads
+    scales = [ln for ln in lines if ln.startswith("TIME (Sc:")]
+    p = od.oppoint(2, w, 1, 1)
+    assert len(scales) == p.sc_f - p.sc_l + 1
+    for ln, s in zip(scales, range(p.sc_f, p.sc_l - 1, -1)):
+        m = re.match(r"TIME \(Sc: (\d+), #p:\s*(\d+), pconst, pinit, poptim, cflow, tvopt, total\):"
+                     r"\s+([\d.]+)\s+([\d.]+)\s+([\d.]+)\s+([\d.]+)\s+([\d.]+) ->\s+([\d.]+) ms\.", ln)
+        assert m, ln
+        assert int(m.group(1)) == s
+        ws, hs = w >> s, h >> s
+        assert int(m.group(2)) == -(-ws // 4) * -(-hs // 4)  # nopw * noph, steps 4 (patchgrid.cpp:43-46)
