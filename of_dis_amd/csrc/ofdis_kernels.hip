@@ -769,9 +769,7 @@ struct PatchShape {
   static constexpr int ODD = (NV / 4) & 1;
   static constexpr int V = PAIRS + ODD;
   static constexpr int WR = (P + 1) * NOC;  // window row (floats)
-  // 16-byte loads per window row: the row is read from the 16-byte boundary at or below its start (up to 3
-  // floats early) whenever the image row pitch is a multiple of 4 floats, so every load is aligned
-  static constexpr int Q4 = (WR + 3 + 3) / 4;
+  static constexpr int Q4 = (WR + 3) / 4;   // 16-byte loads per window row
   static constexpr int RS = Q4 * 4;         // LDS row stride (floats)
   static constexpr int WIN = (P + 1) * RS + 4;  // LDS floats per patch (+4: spreads the 8 patches over banks)
   static constexpr int NQ = (P + 1) * Q4;   // 16-byte loads per window
@@ -915,7 +913,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     return;
   }
   const float *Bimg = a.img_b + f * fs;
-  const bool aligned_rows = ((W * NOC) & 3) == 0 && ((uintptr_t)a.img_b & 15) == 0;
   // window loads of this lane: float4 e = s8 + 8 j of the (P+1) x Q4 tile
   constexpr int LPLK = S::LEAN ? 1 : S::LPL;
   int gofs[LPLK], lofs[LPLK];
@@ -948,9 +945,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
     const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
     // window origin: the D tap of value 0, one row above and one column left of the A tap
-    const long qo = ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
-    const int shift = aligned_rows ? (int)(qo & 3) : 0;  // window origin's offset past a 16-byte boundary
-    const float *Q = Bimg + (qo - shift);
+    const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
     wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
     if (S::LEAN) {  // in batches of 4 loads: bounded registers in flight
 #pragma unroll
@@ -976,7 +971,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     }
     wave_lds_sync();
     auto sample = [&](int k) {
-      const float *t = win + shift + doff(k);
+      const float *t = win + doff(k);
       const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
       return w0 * A + w1 * Bv + w2 * C + w3 * D;
     };
@@ -1244,7 +1239,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     return;
   }
   const float *Bimg = a.img_b + f * fs;
-  const bool aligned_rows = ((W * NOC) & 3) == 0 && ((uintptr_t)a.img_b & 15) == 0;
   float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
   float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
   const float st0 = pt0, st1 = pt1;
@@ -1260,9 +1254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
     const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
     const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
-    const long qo = ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
-    const int shift = aligned_rows ? (int)(qo & 3) : 0;
-    const float *Q = Bimg + (qo - shift);
+    const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
     wave_lds_sync();
 #pragma unroll
     for (int j0 = 0; j0 < S16::LPL; j0 += 4) {
@@ -1283,7 +1275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     float pd[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const float *t = win + shift + doff(k);
+      const float *t = win + doff(k);
       const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
       pd[k] = w0 * A + w1 * Bv + w2 * C + w3 * D;
     }
@@ -3220,13 +3212,13 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
       case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
       case 8 * 4 + 3: patchw<8, 3, 2, 2>(a, s); return;
-      case 12 * 4 + 3: {  // eight lanes per patch; A/B: sixteen lanes (window 2: 2 waves/SIMD, 3: 3 waves/SIMD)
-        if (a.window == 1) {
+      case 12 * 4 + 3: {  // sixteen lanes per patch (a.window == 2: the eight-lane form, A/B)
+        if (a.window == 2) {
           patchw<12, 3, 2, 2>(a, s);
         } else {
           const long patches = (long)a.n * a.g.npatch;
           const size_t lds = sizeof(float) * 16 * PatchShape16<12, 3>::SLOT;
-          if (a.window == 2) {
+          if (a.window == 3) {
             if (a.nop == 2) k_patchw16<2, 12, 3, 2><<<ceil_div(patches, 16), 256, lds, s>>>(a);
             else k_patchw16<1, 12, 3, 2><<<ceil_div(patches, 16), 256, lds, s>>>(a);
           } else {
