@@ -3212,13 +3212,13 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
       case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
       case 8 * 4 + 3: patchw<8, 3, 2, 2>(a, s); return;
-      case 12 * 4 + 3: {  // sixteen lanes per patch (a.window == 2: the eight-lane form, A/B)
-        if (a.window == 2) {
+      case 12 * 4 + 3: {  // eight lanes per patch; A/B: sixteen lanes (window 2: 2 waves/SIMD, 3: 3 waves/SIMD)
+        if (a.window == 1) {
           patchw<12, 3, 2, 2>(a, s);
         } else {
           const long patches = (long)a.n * a.g.npatch;
           const size_t lds = sizeof(float) * 16 * PatchShape16<12, 3>::SLOT;
-          if (a.window == 3) {
+          if (a.window == 2) {
             if (a.nop == 2) k_patchw16<2, 12, 3, 2><<<ceil_div(patches, 16), 256, lds, s>>>(a);
             else k_patchw16<1, 12, 3, 2><<<ceil_div(patches, 16), 256, lds, s>>>(a);
           } else {
