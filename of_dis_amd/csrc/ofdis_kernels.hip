@@ -1091,286 +1091,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }
 
-// ---------------------------------------------------------------- DIS patches, sixteen lanes per patch
-// For the largest shape (p = 12 RGB: 432 values) eight lanes per patch need ~400 registers (54 values per
-// lane).  Here sixteen lanes share a patch: lane (s, h), s = lane % 8, h = lane / 8 % 2, holds the values
-// v = s + 8 (k + h K) of Eigen chain s, k < K = PAIRS / 2 -- the lower half of each chain on lane (s, 0), the
-// upper half on lane (s, 1).  A chain is one ordered sum, so it is relayed: the upper lanes publish their
-// terms in LDS, the lower lane adds its own terms and then the published ones in order (the reference's
-// sequence), and the DPP tree over the eight lower lanes finishes the total, which lane (s, 1) then reads
-// by DPP.  Registers per lane halve (three waves per SIMD instead of one), the window tile is shared.
-template <int P, int NOC>
-struct PatchShape16 {
-  using S = PatchShape<P, NOC>;
-  static constexpr int K = S::PAIRS / 2;             // values per lane
-  static_assert(S::ODD == 0 && S::PAIRS % 2 == 0, "sixteen-lane form: an even number of packet pairs");
-  static constexpr int LPL = (S::NQ + 15) / 16;        // window loads per lane
-  static constexpr int RELAY = 8 * 3 * K;              // published upper-half terms (three reductions)
-  static constexpr int SLOT = ((S::WIN > RELAY ? S::WIN : RELAY) + 3) / 4 * 4 + 4;  // LDS floats per patch
-};
-
-template <int K>
-struct ChainLo {  // the lower half of one Eigen chain, then the relayed upper half (lower lanes only)
-  float acc = 0.0f;
-  __device__ __forceinline__ void add(int k, float x) { acc = k == 0 ? x : acc + x; }
-};
-
-// lane i <- lane i - 8 within its 16-lane row (row_shr:8)
-__device__ __forceinline__ float row_from_minus8(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x118, 0xF, 0xF, true));
-}
-// Finish a chain: the lower lane's acc (its own K terms, then the K published terms), the packet tree over
-// lanes s = 0..7 of the lower half, and the total on all sixteen lanes.
-__device__ __forceinline__ float chain_total16(float acc, bool lower) {
-  float r = acc + grp_xor4(acc);  // res0 + res1 (lower lanes; upper lanes compute a discarded value)
-  r = r + grp_xor2(r);
-  r = r + grp_xor1(r);
-  const float up = row_from_minus8(r);
-  return lower ? r : up;
-}
-
-template <int NOP, int P, int NOC, int MINW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchw16(PatchArgs a) {
-  using S = PatchShape<P, NOC>;
-  using S16 = PatchShape16<P, NOC>;
-  constexpr int K = S16::K, RS = S::RS, NV = S::NV;
-  extern __shared__ __attribute__((aligned(16))) float slot_all[];
-  const LevelGeom &g = a.g;
-  const int l16 = threadIdx.x & 15, s8 = l16 & 7, hh = l16 >> 3;
-  const bool lower = hh == 0;
-  const long gp = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
-  const bool live = gp < (long)a.n * g.npatch;
-  const long gq = live ? gp : 0;
-  const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
-  const int pxi = ip / g.noph, pyi = ip % g.noph;
-  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
-  const long fs = (long)g.W * g.H * NOC;
-  const int W = g.W;
-  auto div_n = [&](float x) { return x / (float)NV; };  // 432: not a power of two
-  float *win = slot_all + (threadIdx.x >> 4) * S16::SLOT;
-  float *relay = win;  // reused once the taps are read: [3][K][8]
-  auto value = [&](int k) { return s8 + 8 * (k + hh * K); };
-  auto dtap = [&](int v) {
-    const int ch = v % NOC, q = v / NOC;
-    return (q / P) * RS + (q % P) * NOC + ch;
-  };
-  // tap offsets: value v -> v + 8 KP is KROWS patch rows further
-  int dbase[S::KP];
-#pragma unroll
-  for (int k = 0; k < S::KP; ++k) dbase[k] = dtap(value(k));
-  auto doff = [&](int k) { return dbase[k % S::KP] + (k / S::KP) * S::KROWS * RS; };
-  // ---- template + gradients (getPatchStaticNNGrad, patch.cpp:297-343)
-  float tmp[K], gx[K], gy[K];
-  {
-    const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
-    const long base = ((long)(py - P / 2) * W + (px - P / 2)) * NOC;
-    const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int v = value(k), ch = v % NOC, q = v / NOC;
-      const int o = ((q / P) * W + (q % P)) * NOC + ch;
-      tmp[k] = A[o];
-      gx[k] = DX[o];
-      gy[k] = DY[o];
-    }
-  }
-  // reduce R arrays of per-value terms (term(k, r)) over the patch in Eigen's order; out[r] on all lanes
-  auto reduce = [&](auto term, float *out, auto R_t) {
-    constexpr int R = decltype(R_t)::value;
-    ChainLo<K> c[R];
-    wave_lds_sync();  // earlier readers of the relay region are done
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float x = term(k, r);
-        if (lower) c[r].add(k, x);
-        else relay[(r * K + k) * 8 + s8] = x;
-      }
-    wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int r = 0; r < R; ++r) c[r].acc = c[r].acc + relay[(r * K + k) * 8 + s8];
-#pragma unroll
-    for (int r = 0; r < R; ++r) out[r] = chain_total16(c[r].acc, lower);
-  };
-  if (a.patnorm > 0) {
-    float m[1];
-    reduce([&](int k, int) { return tmp[k]; }, m, std::integral_constant<int, 1>());
-    const float mean = div_n(m[0]);
-#pragma unroll
-    for (int k = 0; k < K; ++k) tmp[k] = tmp[k] - mean;
-  }
-  // ---- ComputeHessian (patch.cpp:69-86)
-  float H00, H01 = 0.0f, H11 = 0.0f;
-  {
-    float hh3[3];
-    if (NOP == 2) {
-      reduce([&](int k, int r) { return r == 0 ? gx[k] * gx[k] : (r == 1 ? gx[k] * gy[k] : gy[k] * gy[k]); }, hh3,
-             std::integral_constant<int, 3>());
-      H00 = hh3[0]; H01 = hh3[1]; H11 = hh3[2];
-      if (H00 * H11 - H01 * H01 == 0.0f) {
-        H00 = (float)((double)H00 + 1e-10);
-        H11 = (float)((double)H11 + 1e-10);
-      }
-    } else {
-      reduce([&](int k, int) { return gx[k] * gx[k]; }, hh3, std::integral_constant<int, 1>());
-      H00 = hh3[0];
-      if (H00 == 0.0f) H00 = (float)((double)H00 + 1e-10);
-    }
-  }
-  const Llt2 fac = llt2_factor(H00, H01, H11);
-  const float fac1 = llt1_factor(H00);
-  if (a.stage == 1) {
-    if (live && l16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[K - 1];
-    return;
-  }
-  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
-  float pin0 = 0.0f, pin1 = 0.0f;
-  if (a.prev) {
-    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
-    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
-    pin0 = pv[0] * 2;
-    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
-  }
-  if (a.stage == 2) {
-    if (live && l16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[K - 1] + pin0 + pin1;
-    return;
-  }
-  const float *Bimg = a.img_b + f * fs;
-  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
-  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
-  const float st0 = pt0, st1 = pt1;
-  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
-  int cnt = 0;
-  bool converged = false;
-  float b0 = 0.0f, b1 = 0.0f;
-  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
-  // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
-  auto evaluate = [&](float &r0, float *out) {
-    const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
-    const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
-    const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
-    const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
-    const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
-    const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
-    wave_lds_sync();
-#pragma unroll
-    for (int j0 = 0; j0 < S16::LPL; j0 += 4) {
-      float4_u t[4];
-      int lo[4];
-#pragma unroll
-      for (int j = j0; j < j0 + 4 && j < S16::LPL; ++j) {
-        const int e = l16 + 16 * j, e2 = e < S::NQ ? e : S::NQ - 1;
-        const int row = e2 / S::Q4, c4 = e2 % S::Q4;
-        lo[j - j0] = row * RS + c4 * 4;
-        t[j - j0] = *reinterpret_cast<const float4_u *>(Q + row * W * NOC + c4 * 4);
-      }
-#pragma unroll
-      for (int j = j0; j < j0 + 4 && j < S16::LPL; ++j)
-        if (l16 + 16 * j < S::NQ) *reinterpret_cast<float4_v *>(win + lo[j - j0]) = t[j - j0];
-    }
-    wave_lds_sync();
-    float pd[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float *t = win + doff(k);
-      const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
-      pd[k] = w0 * A + w1 * Bv + w2 * C + w3 * D;
-    }
-    if (a.patnorm > 0) {
-      float m[1];
-      reduce([&](int k, int) { return pd[k]; }, m, std::integral_constant<int, 1>());
-      const float mean = div_n(m[0]);
-#pragma unroll
-      for (int k = 0; k < K; ++k) pd[k] = pd[k] - mean;
-    }
-    // loss: pd <- e; the weight w = |e| exactly (e is d (L2) or copysign(w, d) with w >= 0)
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float d = pd[k] - tmp[k];
-      float e;
-      if (a.costfct == 0) {
-        e = d;
-      } else if (a.costfct == 1) {
-        e = copysignf(sqrtf(fabsf(d)), d);
-      } else {
-        e = copysignf(sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f), d);
-      }
-      pd[k] = e;
-    }
-    if (out) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) out[value(k)] = fabsf(pd[k]);
-      return;
-    }
-    float red[3];
-    if (NOP == 2) {
-      reduce([&](int k, int r) { return r == 0 ? fabsf(pd[k]) : (r == 1 ? gx[k] * pd[k] : gy[k] * pd[k]); }, red,
-             std::integral_constant<int, 3>());
-      b1 = red[2];
-    } else {
-      reduce([&](int k, int r) { return r == 0 ? fabsf(pd[k]) : gx[k] * pd[k]; }, red,
-             std::integral_constant<int, 2>());
-    }
-    r0 = red[0];
-    b0 = red[1];
-  };
-  float *pwo = a.pweight + gq * NV;
-  bool first = true, store = false;
-  converged = !live;
-  if (live && oob(pt0, pt1)) {  // pweight never written upstream, defined as 0
-#pragma unroll
-    for (int k = 0; k < K; ++k) pwo[value(k)] = 0.0f;
-    converged = true;
-  } else {
-    mares = 1e5f;
-  }
-  // one evaluation copy for the start, the iterations and the final weight store (instruction cache)
-  while (!converged || store) {
-    if (!first && !store) {
-      ++cnt;
-      if (NOP == 2) {
-        llt2_solve(fac, b0, b1, d0, d1);
-        p0 = p0 - d0;
-        p1 = p1 - d1;
-      } else {
-        d0 = llt1_solve(fac1, b0);
-        p0 = p0 - d0;
-        p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
-      }
-      pt0 = ptr0 + p0;
-      if (NOP == 2) pt1 = ptr1 + p1;
-      const float ex = st0 - pt0, ey = st1 - pt1;
-      if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
-        p0 = pin0;
-        p1 = pin1;
-        pt0 = ptr0 + p0;
-        if (NOP == 2) pt1 = ptr1 + p1;
-        converged = true;
-      }
-    }
-    float r0 = 0.0f;
-    evaluate(r0, store ? pwo : nullptr);
-    if (store) {
-      store = false;
-      break;
-    }
-    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
-    if (cnt == 1) sq_init = sq;
-    mares_old = mares;
-    mares = div_n(r0);
-    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
-                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
-                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
-    if (!keep) converged = true;
-    if (converged) store = true;
-    first = false;
-  }
-  if (live && l16 < NOP) a.p_iter[gp * NOP + l16] = l16 == 0 ? p0 : p1;
-}
-
 // ------------------------------------------------------------------------------------------------ aggregation
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -3212,22 +2932,7 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
       case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
       case 8 * 4 + 3: patchw<8, 3, 2, 2>(a, s); return;
-      case 12 * 4 + 3: {  // eight lanes per patch; A/B: sixteen lanes (window 2: 2 waves/SIMD, 3: 3 waves/SIMD)
-        if (a.window == 1) {
-          patchw<12, 3, 2, 2>(a, s);
-        } else {
-          const long patches = (long)a.n * a.g.npatch;
-          const size_t lds = sizeof(float) * 16 * PatchShape16<12, 3>::SLOT;
-          if (a.window == 2) {
-            if (a.nop == 2) k_patchw16<2, 12, 3, 2><<<ceil_div(patches, 16), 256, lds, s>>>(a);
-            else k_patchw16<1, 12, 3, 2><<<ceil_div(patches, 16), 256, lds, s>>>(a);
-          } else {
-            if (a.nop == 2) k_patchw16<2, 12, 3, 3><<<ceil_div(patches, 16), 256, lds, s>>>(a);
-            else k_patchw16<1, 12, 3, 3><<<ceil_div(patches, 16), 256, lds, s>>>(a);
-          }
-        }
-        return;
-      }
+      case 12 * 4 + 3: patchw<12, 3, 2, 2>(a, s); return;
     }
   }
   if (!a.wave_per_patch) {

@@ -1148,7 +1148,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 2},
-      {"patch_window", &ofdis_context::opt_patch_window, 0, 3},
+      {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
