@@ -113,7 +113,6 @@ struct UpArgs {
   float *out;         // [n][H0][W0][nop]
   int n, nop, wl, hl, log2s, W0, H0, offx, offy;
   int nt_store;       // non-temporal output stores (A/B option "nt_store")
-  int rows;           // output rows per workgroup of k_upsample_rows (8, 16, 32; option "up_rows")
 };
 
 // Initial flow (run_dense.cpp:356-379): full-resolution [n][H0][W0][nop] -> replicate-padded, x sc,

@@ -2751,10 +2751,10 @@ __device__ __forceinline__ float up_px(const float *P, long r0, long r1, const X
 // float value.  Horizontal taps are per source row (HResizeLinear), the vertical blend per output row
 // (VResizeLinear), exactly as in OpenCV's generic float path.
 constexpr int kUpCols = 1024;
+constexpr int kUpRows = 8;
+constexpr int kUpSrcRows = kUpRows / 2 + 3;  // source rows a block can touch (2^l >= 2)
 typedef float v4f __attribute__((ext_vector_type(4)));
-template <int kUpRows>
 __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
-  constexpr int kUpSrcRows = kUpRows / 2 + 3;  // source rows a block can touch (2^l >= 2)
   __shared__ float src[kUpSrcRows][2][kUpCols / 2 + 8];  // [row][comp][col]
   const int y0 = blockIdx.y * kUpRows, f = blockIdx.z;
   const int dx0 = blockIdx.x * kUpCols + a.offx;  // first output column of the block (uncropped coordinates)
@@ -3131,13 +3131,8 @@ void launch_init_area(const InitArgs &a, hipStream_t s) {
 }
 
 void launch_upsample(const UpArgs &a, hipStream_t s) {
-  if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0) {
-    switch (a.rows) {
-      case 16: k_upsample_rows<16><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 16), a.n), 256, 0, s>>>(a); return;
-      case 32: k_upsample_rows<32><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 32), a.n), 256, 0, s>>>(a); return;
-      default: k_upsample_rows<8><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 8), a.n), 256, 0, s>>>(a); return;
-    }
-  }
+  if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
+    k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
   else
     k_upsample<<<dim3(ceil_div(a.W0, 256), a.H0, a.n), 256, 0, s>>>(a);
 }

@@ -79,7 +79,6 @@ struct ofdis_context {
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
-  int opt_up_rows = 8;         // output rows per upsample workgroup (8, 16, 32; A/B)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
@@ -698,7 +697,6 @@ int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *
   up.offx = P.padl;
   up.offy = P.padt;
   up.nt_store = c->opt_nt_store;
-  up.rows = c->opt_up_rows;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
@@ -1149,7 +1147,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
-      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_rows", &ofdis_context::opt_up_rows, 8, 32},     {"graph", &ofdis_context::opt_graph, 0, 2},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 2},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
