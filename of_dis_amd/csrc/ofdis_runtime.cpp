@@ -89,7 +89,6 @@ struct ofdis_context {
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
   // chains on two streams), else 1; chunk 0 = the batch split evenly over the streams.
   int opt_streams = 0, opt_chunk = 0;
-  int opt_stagger = 0;               // round robin: lanes start one stage apart (1: pyramid, 2: levels; A/B)
   int opt_pipeline = 0;              // two-stream pipeline: streaming stages beside the DIS + TV chain
   std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
@@ -724,19 +723,13 @@ int run_init(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, c
 }
 
 // One chunk of frames through the whole pipeline on stream s with workspace ws.
-// mark[0] / mark[1]: events recorded after the pyramid / after the levels (or NULL); wait: an event the chunk
-// waits on before its pyramid (or NULL).
 int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
-              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s,
-              hipEvent_t wait = nullptr, hipEvent_t mark_pyr = nullptr, hipEvent_t mark_lev = nullptr) {
-  if (wait) HIP_OK(hipStreamWaitEvent(s, wait, 0));
+              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s) {
   int rc = run_pyramid(c, ws, P, img_a, img_b, s);
   if (rc) return rc;
   if (init && (rc = run_init(c, ws, P, p, init, s))) return rc;
-  if (mark_pyr) HIP_OK(hipEventRecord(mark_pyr, s));
   rc = run_levels(c, ws, P, p, s, init ? (const float *)(ws + P.off_init) : nullptr, nullptr);
   if (rc) return rc;
-  if (mark_lev) HIP_OK(hipEventRecord(mark_lev, s));
   return run_upsample(c, ws, P, p, flow_out, s);
 }
 
@@ -808,7 +801,7 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
   cp.lanes = cp.kind == CallPlan::kPipeline ? 2 : std::min(nstreams, cp.nchunks);
   int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total);
   if (rc) return rc;
-  if (cp.kind == CallPlan::kPipeline || c->opt_stagger)
+  if (cp.kind == CallPlan::kPipeline)
     while ((int)c->pipe_ev.size() < 2 * cp.nchunks) {
       hipEvent_t e = nullptr;
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -825,17 +818,11 @@ int issue_round_robin(ofdis_context *c, const CallPlan &cp, hipStream_t s, const
   for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
   const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
   const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
-  // stagger 1 / 2: a lane's first chunk starts once the previous lane's first chunk has finished its pyramid /
-  // its levels, so one lane's streaming stages meet the other's latency-bound chain
-  hipEvent_t *ev = c->pipe_ev.data();
   for (int ch = 0; ch < cp.nchunks; ++ch) {
     const size_t f0 = (size_t)ch * cp.chunk;
     auto &L = c->lanes[ch % k];
-    const bool st = c->opt_stagger > 0 && ch < k;
-    hipEvent_t wait = st && ch > 0 ? ev[ch - 1] : nullptr;
-    hipEvent_t mpyr = st && c->opt_stagger == 1 ? ev[ch] : nullptr, mlev = st && c->opt_stagger == 2 ? ev[ch] : nullptr;
     int rc = run_chunk(c, L.ws, cp.parts[ch], p, img_a + f0 * in_frame, img_b + f0 * in_frame,
-                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s, wait, mpyr, mlev);
+                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s);
     if (rc) return rc;
   }
   for (int i = 0; i < k; ++i) {
@@ -1157,7 +1144,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     int lo, hi;
   };
   static const Opt opts[] = {
-      {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"stagger", &ofdis_context::opt_stagger, 0, 2},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
+      {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 2},
