@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 
 # BASELINE.json configs -> (binary, width, height, noc, mode, oppoint, explicit 20 parameters or None, batch)
 CONFIGS = {
-    "A": ("run_OF_INT", 640, 480, 1, 1, 2, None, 1024),
+    "A": ("run_OF_INT", 640, 480, 1, 1, 2, None, 2048),  # 1024: 110k, 2048: 113k MPix/s (profiles/r02/sweep6)
     # 2048 pairs per GPU per step = two 1024-pair chunks on two streams (measured best: 1024 pairs 266k,
     # 1536 282k, 2048 298k, 3072 285k, 4096 293k MPix/s; profiles/r02/sweep3)
     "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 2048),
