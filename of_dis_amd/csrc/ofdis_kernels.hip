@@ -813,8 +813,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// MINW: waves per SIMD the register allocation must allow (amdgpu_waves_per_eu)
-template <int NOP, int P, int NOC, int MINW>
+// MINW: waves per SIMD the register allocation must allow (amdgpu_waves_per_eu).  COST: costfct as a
+// compile-time constant (a runtime switch inside the unrolled value loop was if-converted: every value paid
+// for the L1 and pseudo-Huber losses' square roots and division).
+template <int NOP, int P, int NOC, int MINW, int COST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchw(PatchArgs a) {
   using S = PatchShape<P, NOC>;
   constexpr int PAIRS = S::PAIRS, ODD = S::ODD, V = S::V, RS = S::RS;
@@ -995,10 +997,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (a.patnorm > 0) x = x - mean;
       const float d = x - tmp[k];
       float w, e;
-      if (a.costfct == 0) {
+      if (COST == 0) {
         e = d;
         w = fabsf(d);
-      } else if (a.costfct == 1) {
+      } else if (COST == 1) {
         w = sqrtf(fabsf(d));
         e = copysignf(w, d);
       } else {
@@ -2921,10 +2923,15 @@ template <int P, int NOC, int MINW1, int MINW2>
 static void patchw(const PatchArgs &a, hipStream_t s) {
   const long patches = (long)a.n * a.g.npatch;
   const size_t lds = sizeof(float) * 32 * PatchShape<P, NOC>::WIN;
-  if (a.nop == 2)
-    k_patchw<2, P, NOC, MINW2><<<ceil_div(patches, 32), 256, lds, s>>>(a);
-  else
-    k_patchw<1, P, NOC, MINW1><<<ceil_div(patches, 32), 256, lds, s>>>(a);
+  const dim3 grid(ceil_div(patches, 32));
+  switch (a.costfct * 2 + (a.nop == 2 ? 1 : 0)) {
+    case 0: k_patchw<1, P, NOC, MINW1, 0><<<grid, 256, lds, s>>>(a); return;
+    case 1: k_patchw<2, P, NOC, MINW2, 0><<<grid, 256, lds, s>>>(a); return;
+    case 2: k_patchw<1, P, NOC, MINW1, 1><<<grid, 256, lds, s>>>(a); return;
+    case 3: k_patchw<2, P, NOC, MINW2, 1><<<grid, 256, lds, s>>>(a); return;
+    case 4: k_patchw<1, P, NOC, MINW1, 2><<<grid, 256, lds, s>>>(a); return;
+    default: k_patchw<2, P, NOC, MINW2, 2><<<grid, 256, lds, s>>>(a); return;
+  }
 }
 void launch_patch(const PatchArgs &a, hipStream_t s) {
   if (a.window && !a.wave_per_patch) {  // LDS-windowed eight-lane form for the shapes of the op-points
