@@ -10,7 +10,8 @@ import os
 import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libofdis.so")
+# OFDIS_LIB: another build of the same library (A/B timing of kernel variants, tools/ab_session.sh)
+LIB_PATH = os.environ.get("OFDIS_LIB") or os.path.join(PKG_DIR, "libofdis.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 OK = 0

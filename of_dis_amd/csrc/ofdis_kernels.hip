@@ -20,6 +20,7 @@
 //   k_tv_final      refine_variational.cpp:209-227,305-323
 //   k_upsample      run_dense.cpp:407-415 (x2^l, cv::resize INTER_LINEAR, crop)
 #include "ofdis_internal.h"
+#include "ofdis_math.h"
 
 #include <cstdlib>
 
@@ -29,6 +30,7 @@ namespace ofdis {
 // 16-byte vector with 4-byte alignment: dword-aligned global_load_dwordx4 (gfx950 allows unaligned vector loads)
 typedef float float4_u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float float4_v __attribute__((ext_vector_type(4)));
+typedef float float2_p __attribute__((ext_vector_type(2)));  // v_pk_mul_f32 operand pairs
 
 namespace {
 
@@ -355,10 +357,10 @@ __device__ __forceinline__ void patch_eval(const PatchCtx<JM> &c, float mx, floa
       pd[j] = d;
       w = fabsf(d);
     } else if (c.costfct == 1) {
-      w = sqrtf(fabsf(d));
+      w = sqrt_nonneg(fabsf(d));
       pd[j] = copysignf(w, d);
     } else {
-      w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+      w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
       pd[j] = copysignf(w, d);
     }
     pw[j] = w;
@@ -517,7 +519,7 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
     pt0 = ptr0 + p0;
     if (NOP == 2) pt1 = ptr1 + p1;
     const float ex = st0 - pt0, ey = st1 - pt1;
-    if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+    if (sqrt_nonneg(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
       p0 = pin0;
       p1 = pin1;
       pt0 = ptr0 + p0;
@@ -689,10 +691,10 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
         e = d;
         w = fabsf(d);
       } else if (a.costfct == 1) {
-        w = sqrtf(fabsf(d));
+        w = sqrt_nonneg(fabsf(d));
         e = copysignf(w, d);
       } else {
-        w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
         e = copysignf(w, d);
       }
       pw[k] = w;
@@ -735,7 +737,7 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
     pt0 = ptr0 + p0;
     if (NOP == 2) pt1 = ptr1 + p1;
     const float ex = st0 - pt0, ey = st1 - pt1;
-    if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+    if (sqrt_nonneg(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
       p0 = pin0;
       p1 = pin1;
       pt0 = ptr0 + p0;
@@ -939,15 +941,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1):
   // the residual sums r0 = sum |w|, b0 = sum dx e (, b1 = sum dy e); with `out`, the weights w are stored
-  auto evaluate = [&](float &r0, float *out, auto store_t) {
-    constexpr int STORE = decltype(store_t)::value;  // 1: weights only (the final store), 0: sums only, 2: runtime
+  // STORE 0: sums only; 1: weights only (the final store, to `out`); 2 (LEAN): wave-uniform `st` selects
+  auto evaluate = [&](float &r0, float *out, bool st, bool nowin, auto store_t) {
+    constexpr int STORE = decltype(store_t)::value;
     const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
     const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
     const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
     const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
-    // window origin: the D tap of value 0, one row above and one column left of the A tap
+    const float2_p wab = {w0, w1}, wcd = {w2, w3};
+    // window origin: the D tap of value 0, one row above and one column left of the A tap (a lane without a
+    // position of its own -- LEAN store pass: out of range or out of bounds at the start -- reads the frame's
+    // first rows and stores zeros)
     const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
+    if (STORE == 2 && nowin) Q = Bimg;
     wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
     if (S::LEAN) {  // in batches of 4 loads: bounded registers in flight
 #pragma unroll
@@ -972,10 +979,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     }
     wave_lds_sync();
-    auto sample = [&](int k) {
-      const float *t = win + doff(k);
-      const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
-      return w0 * A + w1 * Bv + w2 * C + w3 * D;
+    auto sample = [&](int k) {  // w0 A + w1 B + w2 C + w3 D; the products as two v_pk_mul_f32 (LEAN: left to
+      const float *t = win + doff(k);  // the compiler, which packs them too; explicit pairs make it spill there)
+      if (S::LEAN) {
+        const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
+        return w0 * A + w1 * Bv + w2 * C + w3 * D;
+      }
+      const float2_p ab = float2_p{t[RS + NOC], t[RS]} * wab, cd = float2_p{t[NOC], t[0]} * wcd;
+      return ((ab.x + ab.y) + cd.x) + cd.y;
     };
     constexpr int VK = S::LEAN ? 1 : V;
     float pd[VK];
@@ -990,47 +1001,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
       if (a.patnorm > 0) mean = div_n(m.total());
     }
+    // LEAN: re-read the taps rather than let the compiler keep the first pass's loads alive (it would CSE them)
+    if (S::LEAN) __asm__ volatile("" ::: "memory");
     EigenAcc<PAIRS, ODD> ab, ex, ey;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      float x = S::LEAN ? sample(k) : pd[k];
-      if (a.patnorm > 0) x = x - mean;
+      const float x = (S::LEAN ? sample(k) : pd[k]) - mean;  // mean = 0 without normalisation: x - 0 == x
       const float d = x - tmp[k];
       float w, e;
       if (COST == 0) {
         e = d;
         w = fabsf(d);
       } else if (COST == 1) {
-        w = sqrtf(fabsf(d));
+        w = sqrt_nonneg(fabsf(d));
         e = copysignf(w, d);
       } else {
-        w = sqrtf((sqrtf(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
         e = copysignf(w, d);
       }
-      if (STORE == 1 || (STORE == 2 && out)) {
-        if (k < PAIRS) out[s8 + 8 * k] = w;
-        else if (s8 < 4) out[8 * PAIRS + s8] = w;
-      }
-      if (STORE == 0 || (STORE == 2 && !out)) {
+      if (STORE != 1) {  // (the LEAN store pass accumulates too: cheaper than a second branch per value)
         ab.add(k, fabsf(w));
         ex.add(k, gx[k] * e);
         if (NOP == 2) ey.add(k, gy[k] * e);
+        if (STORE == 2) {  // keep the sums here: sunk past the store branches they hold every w live
+          __asm__ volatile("" : "+v"(ab.acc), "+v"(ex.acc), "+v"(ey.acc));
+        }
+      }
+      if (STORE == 1 || (STORE == 2 && st)) {
+        const float ws = (STORE == 2 && nowin) ? 0.0f : w;
+        if (k < PAIRS) out[s8 + 8 * k] = ws;
+        else if (s8 < 4) out[8 * PAIRS + s8] = ws;
       }
     }
-    if (STORE == 0 || (STORE == 2 && !out)) {
+    if (STORE == 0 || (STORE == 2 && !st)) {
       r0 = ab.total();
       b0 = ex.total();
       if (NOP == 2) b1 = ey.total();
     }
   };
   // The evaluation is unrolled over the values; the loop holds one copy of it (start evaluation and every
-  // iteration), the final weights-only evaluation another (big shapes, LEAN: one copy for all three, with a
-  // runtime store flag, to stay inside the instruction cache).  Per patch:
+  // iteration), the final weights-only evaluation another (big shapes, LEAN: one copy for both, to stay
+  // inside the instruction cache).  Per patch:
   //   OptimizeStart (patch.cpp:117-154): evaluate at the start position (unless it is out of bounds);
   //   OptimizeIter (patch.cpp:156-210): while not converged, solve, update, outlier reset, evaluate;
   //   then one more evaluation at the final position that stores the loss weights.
-  float *pwo = a.pweight + gq * S::NV;
-  bool start_oob = false, first = true, store = false;
+  // LEAN: patches that converge wait (masked) for the rest of the wave, then all eight take the store pass
+  // together, so its store / sum choice is wave-uniform (a scalar branch, not an exec mask per value).  Lanes
+  // past the last patch store into the buffer's 32-patch tail (ofdis_runtime.cpp make_plan), lanes out
+  // of bounds at the start store zeros again.
+  float *pwo = a.pweight + (S::LEAN ? gp : gq) * S::NV;
+  bool start_oob = false, first = true;
   converged = !live;
   if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
 #pragma unroll
@@ -1041,54 +1061,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   } else {
     mares = 1e5f;
   }
-  while (!converged || (S::LEAN && store)) {
-    if (!first && !store) {
-      ++cnt;
-      if (NOP == 2) {
-        llt2_solve(fac, b0, b1, d0, d1);
-        p0 = p0 - d0;
-        p1 = p1 - d1;
-      } else {
-        d0 = llt1_solve(fac1, b0);
-        p0 = p0 - d0;
-        p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
-      }
-      pt0 = ptr0 + p0;
-      if (NOP == 2) pt1 = ptr1 + p1;
-      const float ex = st0 - pt0, ey = st1 - pt1;
-      if (sqrtf(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
-        p0 = pin0;
-        p1 = pin1;
+  const bool nowin = !live || start_oob;
+  for (;;) {
+    const bool st = S::LEAN && __builtin_amdgcn_ballot_w64(!converged) == 0;  // wave-uniform
+    if (!S::LEAN && __builtin_amdgcn_ballot_w64(!converged) == 0) break;
+    if (st || !converged) {
+      if (!first && !st) {
+        ++cnt;
+        if (NOP == 2) {
+          llt2_solve(fac, b0, b1, d0, d1);
+          p0 = p0 - d0;
+          p1 = p1 - d1;
+        } else {
+          d0 = llt1_solve(fac1, b0);
+          p0 = p0 - d0;
+          p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+        }
         pt0 = ptr0 + p0;
         if (NOP == 2) pt1 = ptr1 + p1;
-        converged = true;
+        const float ex = st0 - pt0, ey = st1 - pt1;
+        if (sqrt_nonneg(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+          p0 = pin0;
+          p1 = pin1;
+          pt0 = ptr0 + p0;
+          if (NOP == 2) pt1 = ptr1 + p1;
+          converged = true;
+        }
+      }
+      float r0 = 0.0f;
+      if (S::LEAN)
+        evaluate(r0, pwo, st, nowin, std::integral_constant<int, 2>());
+      else
+        evaluate(r0, nullptr, false, false, std::integral_constant<int, 0>());
+      if (!st) {
+        // OptimizeComputeErrImg (patch.cpp:275-295)
+        sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+        if (cnt == 1) sq_init = sq;
+        mares_old = mares;
+        mares = div_n(r0);
+        const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                          ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                          ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+        if (!keep) converged = true;
       }
     }
-    float r0 = 0.0f;
-    if (S::LEAN) {
-      evaluate(r0, store ? pwo : nullptr, std::integral_constant<int, 2>());
-      if (store) {
-        store = false;
-        break;
-      }
-    } else {
-      evaluate(r0, nullptr, std::integral_constant<int, 0>());
-    }
-    // OptimizeComputeErrImg (patch.cpp:275-295)
-    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
-    if (cnt == 1) sq_init = sq;
-    mares_old = mares;
-    mares = div_n(r0);
-    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
-                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
-                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
-    if (!keep) converged = true;
-    if (S::LEAN && converged) store = true;
+    if (st) break;
     first = false;
   }
   if (!S::LEAN && live && !start_oob) {
     float r0;
-    evaluate(r0, pwo, std::integral_constant<int, 1>());
+    evaluate(r0, pwo, true, false, std::integral_constant<int, 1>());
   }
   if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }

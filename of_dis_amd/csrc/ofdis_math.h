@@ -1,0 +1,22 @@
+// Device math helpers shared by the kernels and tools/sqrt_probe.hip (which checks them exhaustively).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ofdis {
+
+// Correctly rounded sqrtf for x >= +0, +inf or NaN: the sequence the compiler expands sqrtf into on gfx950
+// (denormal range scaled by 2^32, v_sqrt_f32, then the neighbour ulps s -/+ 1 tested with one fma residual
+// each) without its final class test, which only changes the result for negative inputs.  Bit-identical to
+// sqrtf over every non-negative float (tools/sqrt_probe.hip); callers pass |d| or sums of squares.
+__device__ __forceinline__ float sqrt_nonneg(float x) {
+  const bool tiny = x < 0x1p-96f;
+  const float xs = tiny ? x * 0x1p+32f : x;
+  const float s = __builtin_amdgcn_sqrtf(xs);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  float r = __builtin_fmaf(-sm, s, xs) <= 0.0f ? sm : s;
+  r = __builtin_fmaf(-sp, s, xs) > 0.0f ? sp : r;
+  return tiny ? r * 0x1p-16f : r;
+}
+
+}  // namespace ofdis
