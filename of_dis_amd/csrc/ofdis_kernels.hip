@@ -30,7 +30,6 @@ namespace ofdis {
 // 16-byte vector with 4-byte alignment: dword-aligned global_load_dwordx4 (gfx950 allows unaligned vector loads)
 typedef float float4_u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float float4_v __attribute__((ext_vector_type(4)));
-typedef float float2_p __attribute__((ext_vector_type(2)));  // v_pk_mul_f32 operand pairs
 
 namespace {
 
@@ -949,7 +948,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
     const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
     const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
-    const float2_p wab = {w0, w1}, wcd = {w2, w3};
     // window origin: the D tap of value 0, one row above and one column left of the A tap (a lane without a
     // position of its own -- LEAN store pass: out of range or out of bounds at the start -- reads the frame's
     // first rows and stores zeros)
@@ -979,14 +977,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     }
     wave_lds_sync();
-    auto sample = [&](int k) {  // w0 A + w1 B + w2 C + w3 D; the products as two v_pk_mul_f32 (LEAN: left to
-      const float *t = win + doff(k);  // the compiler, which packs them too; explicit pairs make it spill there)
-      if (S::LEAN) {
-        const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
-        return w0 * A + w1 * Bv + w2 * C + w3 * D;
-      }
-      const float2_p ab = float2_p{t[RS + NOC], t[RS]} * wab, cd = float2_p{t[NOC], t[0]} * wcd;
-      return ((ab.x + ab.y) + cd.x) + cd.y;
+    // (the compiler packs the products into v_pk_mul_f32 pairs itself; written as explicit float2 pairs they
+    // cost E 5 % and made the LEAN shapes spill)
+    auto sample = [&](int k) {
+      const float *t = win + doff(k);
+      const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
+      return w0 * A + w1 * Bv + w2 * C + w3 * D;
     };
     constexpr int VK = S::LEAN ? 1 : V;
     float pd[VK];
