@@ -67,6 +67,8 @@ def parse():
                     help="also time the host-buffer entry point (PCIe-inclusive rate, reported separately)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-pair latency leg")
+    ap.add_argument("--probe-regions", type=int, default=0,
+                    help="diagnostic: time this many extra K-step regions before the reported one (stderr)")
     ap.add_argument("--dry-run", action="store_true", help="rank/shard bookkeeping on gloo, no GPU (CPU test)")
     ap.add_argument("--parity-frames", type=int, default=8,
                     help="timed-pass frames re-checked against the CPU oracle on rank 0 (1 per rank at N > 1)")
@@ -297,6 +299,12 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    for r in range(args.probe_regions):  # diagnostic (stderr only): run-to-run spread inside one process
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        print(f"probe region {r}: {(time.perf_counter() - t) / args.steps * 1e3:.3f} ms/step", file=sys.stderr)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -940,19 +940,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1):
   // the residual sums r0 = sum |w|, b0 = sum dx e (, b1 = sum dy e); with `out`, the weights w are stored
-  // STORE 0: sums only; 1: weights only (the final store, to `out`); 2 (LEAN): wave-uniform `st` selects
-  auto evaluate = [&](float &r0, float *out, bool st, bool nowin, auto store_t) {
-    constexpr int STORE = decltype(store_t)::value;
+  auto evaluate = [&](float &r0, float *out, auto store_t) {
+    constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
     const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
     const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
     const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
     const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
-    // window origin: the D tap of value 0, one row above and one column left of the A tap (a lane without a
-    // position of its own -- LEAN store pass: out of range or out of bounds at the start -- reads the frame's
-    // first rows and stores zeros)
+    // window origin: the D tap of value 0, one row above and one column left of the A tap
     const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
-    if (STORE == 2 && nowin) Q = Bimg;
     wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
     if (S::LEAN) {  // in batches of 4 loads: bounded registers in flight
 #pragma unroll
@@ -978,7 +974,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     }
     wave_lds_sync();
     // (the compiler packs the products into v_pk_mul_f32 pairs itself; written as explicit float2 pairs they
-    // cost E 5 % and made the LEAN shapes spill)
+    // cost config E 5 % and made the LEAN shapes spill)
     auto sample = [&](int k) {
       const float *t = win + doff(k);
       const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
@@ -997,8 +993,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
       if (a.patnorm > 0) mean = div_n(m.total());
     }
-    // LEAN: re-read the taps rather than let the compiler keep the first pass's loads alive (it would CSE them)
-    if (S::LEAN) __asm__ volatile("" ::: "memory");
     EigenAcc<PAIRS, ODD> ab, ex, ey;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -1015,37 +1009,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
         e = copysignf(w, d);
       }
-      if (STORE != 1) {  // (the LEAN store pass accumulates too: cheaper than a second branch per value)
+      if (STORE == 0) {
         ab.add(k, fabsf(w));
         ex.add(k, gx[k] * e);
         if (NOP == 2) ey.add(k, gy[k] * e);
-        if (STORE == 2) {  // keep the sums here: sunk past the store branches they hold every w live
-          __asm__ volatile("" : "+v"(ab.acc), "+v"(ex.acc), "+v"(ey.acc));
-        }
-      }
-      if (STORE == 1 || (STORE == 2 && st)) {
-        const float ws = (STORE == 2 && nowin) ? 0.0f : w;
-        if (k < PAIRS) out[s8 + 8 * k] = ws;
-        else if (s8 < 4) out[8 * PAIRS + s8] = ws;
+      } else {
+        if (k < PAIRS) out[s8 + 8 * k] = w;
+        else if (s8 < 4) out[8 * PAIRS + s8] = w;
       }
     }
-    if (STORE == 0 || (STORE == 2 && !st)) {
+    if (STORE == 0) {
       r0 = ab.total();
       b0 = ex.total();
       if (NOP == 2) b1 = ey.total();
     }
   };
   // The evaluation is unrolled over the values; the loop holds one copy of it (start evaluation and every
-  // iteration), the final weights-only evaluation another (big shapes, LEAN: one copy for both, to stay
-  // inside the instruction cache).  Per patch:
+  // iteration), the final weights-only evaluation another.  Per patch:
   //   OptimizeStart (patch.cpp:117-154): evaluate at the start position (unless it is out of bounds);
   //   OptimizeIter (patch.cpp:156-210): while not converged, solve, update, outlier reset, evaluate;
   //   then one more evaluation at the final position that stores the loss weights.
-  // LEAN: patches that converge wait (masked) for the rest of the wave, then all eight take the store pass
-  // together, so its store / sum choice is wave-uniform (a scalar branch, not an exec mask per value).  Lanes
-  // past the last patch store into the buffer's 32-patch tail (ofdis_runtime.cpp make_plan), lanes out
-  // of bounds at the start store zeros again.
-  float *pwo = a.pweight + (S::LEAN ? gp : gq) * S::NV;
+  float *pwo = a.pweight + gq * S::NV;
   bool start_oob = false, first = true;
   converged = !live;
   if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
@@ -1057,12 +1041,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   } else {
     mares = 1e5f;
   }
-  const bool nowin = !live || start_oob;
+  // (a wave-uniform exit test around a masked body: smaller code than the divergent while, same work)
   for (;;) {
-    const bool st = S::LEAN && __builtin_amdgcn_ballot_w64(!converged) == 0;  // wave-uniform
-    if (!S::LEAN && __builtin_amdgcn_ballot_w64(!converged) == 0) break;
-    if (st || !converged) {
-      if (!first && !st) {
+    if (__builtin_amdgcn_ballot_w64(!converged) == 0) break;
+    if (!converged) {
+      if (!first) {
         ++cnt;
         if (NOP == 2) {
           llt2_solve(fac, b0, b1, d0, d1);
@@ -1085,28 +1068,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         }
       }
       float r0 = 0.0f;
-      if (S::LEAN)
-        evaluate(r0, pwo, st, nowin, std::integral_constant<int, 2>());
-      else
-        evaluate(r0, nullptr, false, false, std::integral_constant<int, 0>());
-      if (!st) {
-        // OptimizeComputeErrImg (patch.cpp:275-295)
-        sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
-        if (cnt == 1) sq_init = sq;
-        mares_old = mares;
-        mares = div_n(r0);
-        const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
-                          ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
-                          ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
-        if (!keep) converged = true;
-      }
+      evaluate(r0, nullptr, std::integral_constant<int, 0>());
+      // OptimizeComputeErrImg (patch.cpp:275-295)
+      sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+      if (cnt == 1) sq_init = sq;
+      mares_old = mares;
+      mares = div_n(r0);
+      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                        ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                        ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+      if (!keep) converged = true;
     }
-    if (st) break;
     first = false;
   }
-  if (!S::LEAN && live && !start_oob) {
+  if (live && !start_oob) {
     float r0;
-    evaluate(r0, pwo, true, false, std::integral_constant<int, 1>());
+    evaluate(r0, pwo, std::integral_constant<int, 1>());
   }
   if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }

@@ -245,13 +245,11 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad, bool init 
   P.off_piter = off;
   off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
   P.off_pw = off;
-  // +32 patches: the windowed patch kernel's store pass writes whole waves; lanes past the last patch of the
-  // launch store into this tail (k_patchw, LEAN shapes)
-  off = align_up(off + sizeof(float) * ((size_t)n * max_np + 32) * novals);
+  off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
   P.off_piter_bw = off;
   if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
   P.off_pw_bw = off;
-  if (P.fb) off = align_up(off + sizeof(float) * ((size_t)n * max_np + 32) * novals);
+  if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
   P.off_tv = off;
   size_t max_sp = 0;  // skewed TV plane
   for (const LevelGeom &g : P.lv) max_sp = std::max(max_sp, (size_t)skew_plane(g.w, g.h));
