@@ -772,7 +772,10 @@ struct PatchShape {
   static constexpr int WR = (P + 1) * NOC;  // window row (floats)
   static constexpr int Q4 = (WR + 3) / 4;   // 16-byte loads per window row
   static constexpr int RS = Q4 * 4;         // LDS row stride (floats)
-  static constexpr int WIN = (P + 1) * RS + 4;  // LDS floats per patch (+4: spreads the 8 patches over banks)
+  // LDS floats per patch, padded to 8 (mod 32): a ds_read2_b32 is banked (a/4) mod 32 per 32-lane half, i.e.
+  // four patches of eight lanes; with their windows 8 banks apart the 8 consecutive values a patch's lanes
+  // read never share a bank with another patch's (a group that wraps a window row still can: 2-way)
+  static constexpr int WIN = (P + 1) * RS + (8 - ((P + 1) * RS) % 32 + 32) % 32;
   static constexpr int NQ = (P + 1) * Q4;   // 16-byte loads per window
   static constexpr int LPL = (NQ + 7) / 8;  // ... per lane
   // value v -> v + 8 KP advances the tap offsets by whole patch rows: KP = lcm(8, NV / P) / 8
