@@ -23,6 +23,8 @@
 #include "ofdis_math.h"
 
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 #pragma clang fp contract(off)
 
@@ -811,6 +813,55 @@ struct EigenAcc {
   }
 };
 
+typedef float f2p __attribute__((ext_vector_type(2)));
+
+// x / c, correctly rounded, for the divisors c = p^2 noc of the windowed shapes that are not powers of two:
+// q0 = x * RN(1/c), r = x - q0 c (exact by FMA), q = q0 + r RN(1/c).  Checked against IEEE x / c for every
+// finite float x (tools/divcheck.c): identical for x = 0 and 2^-60 <= |x| <= 2^100 when c is 144, 192 or 432;
+// any other x of the wave (tiny, huge, inf, NaN) takes the IEEE division in a wave-uniform branch.
+template <int C>
+__device__ __forceinline__ float div_by_const(float x) {
+  static_assert(C == 144 || C == 192 || C == 432, "divisor not checked by tools/divcheck.c");
+  constexpr float c = (float)C, y = 1.0f / (float)C;
+  const float q0 = x * y;
+  const float r = __builtin_fmaf(-q0, c, x);
+  float q = __builtin_fmaf(r, y, q0);
+  q = x == 0.0f ? x : q;
+  const float ax = fabsf(x);
+  const bool slow = x != 0.0f && !(ax >= 0x1p-60f && ax <= 0x1p100f);
+  if (__builtin_amdgcn_ballot_w64(slow) != 0) q = slow ? x / c : q;
+  return q;
+}
+
+// Compile-time loops (the index is a constant expression: template arguments, asm immediates).
+template <class F, int... Is>
+__device__ __forceinline__ void static_for_seq(F &&f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_seq(f, std::make_integer_sequence<int, N>{});
+}
+
+// ds_read2_b32 of the dwords at byte address addr + 4 O0 and addr + 4 O1 into one register pair.  The
+// compiler's own LDS load combining pairs adjacent dwords only; the packed patch evaluation needs two taps
+// that lie whole window rows apart.  The compiler does not track these loads: lds_wait<N>() (at most N LDS /
+// scalar-memory operations outstanding; LDS completes in order) then reg_fence() on each result order the
+// consumers after the data has arrived.
+template <int O0, int O1>
+__device__ __forceinline__ f2p lds_read2(unsigned addr) {
+  static_assert(O0 >= 0 && O1 >= 0 && O0 <= 255 && O1 <= 255, "ds_read2_b32 offsets are 8-bit dword counts");
+  f2p r;
+  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(r) : "v"(addr), "n"(O0), "n"(O1) : "memory");
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt is 4 bits");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void reg_fence(f2p &x) { asm volatile("" : "+v"(x)); }
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -835,9 +886,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
   const long fs = (long)g.W * g.H * NOC;
   const int W = g.W;
-  const float inv_n = 1.0f / (float)S::NV;
+  constexpr float inv_n = 1.0f / (float)S::NV;
   constexpr bool pow2 = (S::NV & (S::NV - 1)) == 0;  // x / n == x * (1/n) exactly for n = 2^k
-  auto div_n = [&](float x) { return pow2 ? x * inv_n : x / (float)S::NV; };
+  auto div_n = [&](float x) {
+    if constexpr (pow2)
+      return x * inv_n;
+    else
+      return div_by_const<S::NV>(x);
+  };
+  // PK: the per-value arithmetic of an evaluation on value pairs (k, k + 1) in packed fp32 -- every lane of a
+  // v_pk_mul_f32 / v_pk_add_f32 rounds like the scalar instruction, so the pairs keep each value's operation
+  // order; the taps of a pair come straight from one ds_read2_b32 into a register pair
+  constexpr bool PK = !S::LEAN && S::ODD == 0 && V % (2 * S::KP) == 0;
   float *win = win_all + (threadIdx.x >> 3) * S::WIN;
   // value of slot k of this lane, and its D-tap offset in the window tile
   auto value = [&](int k) { return k < PAIRS ? s8 + 8 * k : 8 * PAIRS + (s8 & 3); };
@@ -918,6 +978,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1] + pin0 + pin1;
     return;
   }
+  // template and gradients as value pairs for the packed form (register pairs; the scalar arrays die here)
+  constexpr int V2 = PK ? V / 2 : 1;
+  f2p tmp2[V2], gx2[V2], gy2[V2];
+  // pair j = (k, k + KP) with k = (j / KP) 2 KP + j mod KP: the lane's values v and v + 8 KP are whole patch
+  // rows (KROWS) apart, so their taps are a fixed number of window floats apart whatever the lane
+  if (PK) {
+#pragma unroll
+    for (int j = 0; j < V2; ++j) {
+      const int k = (j / S::KP) * 2 * S::KP + j % S::KP;
+      tmp2[j] = f2p{tmp[k], tmp[k + S::KP]};
+      gx2[j] = f2p{gx[k], gx[k + S::KP]};
+      if (NOP == 2) gy2[j] = f2p{gy[k], gy[k + S::KP]};
+    }
+  }
+  auto tmpv = [&](int k) -> float {  // compile-time k
+    if constexpr (PK) {
+      const int g = k / (2 * S::KP), r = k % (2 * S::KP);
+      return r < S::KP ? tmp2[g * S::KP + r].x : tmp2[g * S::KP + r - S::KP].y;
+    } else {
+      return tmp[k];
+    }
+  };
   const float *Bimg = a.img_b + f * fs;
   // window loads of this lane: float4 e = s8 + 8 j of the (P+1) x Q4 tile
   constexpr int LPLK = S::LEAN ? 1 : S::LPL;
@@ -976,8 +1058,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     }
     wave_lds_sync();
-    // (the compiler packs the products into v_pk_mul_f32 pairs itself; written as explicit float2 pairs they
-    // cost config E 5 % and made the LEAN shapes spill)
+    if constexpr (PK && STORE == 0) {
+      // value pairs (k, k + KP): tap X of both values is one ds_read2_b32 into a register pair (taps PD floats
+      // apart), then ((w0 A + w1 B) + w2 C) + w3 D, (x - mean) - tmp and gx e run two values per packed
+      // instruction; the Eigen chains (mean, |w|, gx e, gy e) stay scalar, value by value in order.  Groups of
+      // 2 KP values; the next group's 4 KP reads are in flight while a group is computed.
+      constexpr int KP = S::KP, PD = S::KROWS * RS, NG = V / (2 * KP);
+      const unsigned wb = (unsigned)(uintptr_t)win;
+      f2p pd2[V2], q[2][4];
+      auto issue = [&](auto jc) {  // the four taps of pair j (in flight: this pair and the next)
+        constexpr int j = decltype(jc)::value, i = j % KP, o = 2 * (j / KP) * PD;
+        const unsigned b = wb + 4u * (unsigned)dbase[i];
+        q[j & 1][0] = lds_read2<o, o + PD>(b);                        // D
+        q[j & 1][1] = lds_read2<o + NOC, o + NOC + PD>(b);            // C
+        q[j & 1][2] = lds_read2<o + RS, o + RS + PD>(b);              // B
+        q[j & 1][3] = lds_read2<o + RS + NOC, o + RS + NOC + PD>(b);  // A
+      };
+      issue(std::integral_constant<int, 0>{});
+      static_for<V2>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j + 1 < V2) {
+          issue(std::integral_constant<int, j + 1>{});
+          lds_wait<4>();
+        } else {
+          lds_wait<0>();
+        }
+        f2p *t = q[j & 1];
+        static_for<4>([&](auto ic) { reg_fence(t[decltype(ic)::value]); });
+        f2p x = t[3] * w0 + t[2] * w1;
+        x = x + t[1] * w2;
+        x = x + t[0] * w3;
+        pd2[j] = x;
+      });
+      EigenAcc<PAIRS, ODD> m;
+      static_for<V>([&](auto kc) {  // value order: pair g KP + i holds values g 2KP + i (.x), g 2KP + KP + i (.y)
+        constexpr int k = decltype(kc)::value, g = k / (2 * KP), r = k % (2 * KP);
+        m.add(k, r < KP ? pd2[g * KP + r].x : pd2[g * KP + r - KP].y);
+      });
+      const float mean = a.patnorm > 0 ? div_n(m.total()) : 0.0f;
+      EigenAcc<PAIRS, ODD> ab, ex, ey;
+      static_for<NG>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        f2p qx[KP], qy[KP], wv[KP];
+        static_for<KP>([&](auto ic) {
+          constexpr int i = decltype(ic)::value, j = g * KP + i;
+          const f2p d = (pd2[j] - mean) - tmp2[j];
+          f2p e;
+          if (COST == 0) {
+            e = d;
+            wv[i] = d;
+          } else {
+            float w[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float dh = h ? d.y : d.x;
+              w[h] = COST == 1 ? sqrt_nonneg(fabsf(dh))
+                               : sqrt_nonneg((sqrt_nonneg(1.0f + (dh * dh) / 25.0f) - 1.0f) * 50.0f);
+            }
+            wv[i] = f2p{w[0], w[1]};
+            e = f2p{copysignf(w[0], d.x), copysignf(w[1], d.y)};
+          }
+          qx[i] = gx2[j] * e;
+          if (NOP == 2) qy[i] = gy2[j] * e;
+        });
+        static_for<2 * KP>([&](auto rc) {  // the chains in value order: .x halves, then .y halves
+          constexpr int r = decltype(rc)::value, i = r % KP, h = r / KP, k = g * 2 * KP + r;
+          ab.add(k, fabsf(h ? wv[i].y : wv[i].x));
+          ex.add(k, h ? qx[i].y : qx[i].x);
+          if (NOP == 2) ey.add(k, h ? qy[i].y : qy[i].x);
+        });
+      });
+      r0 = ab.total();
+      b0 = ex.total();
+      if (NOP == 2) b1 = ey.total();
+    } else {
+    // (the compiler packs the products into v_pk_mul_f32 pairs itself; written as explicit float2 pairs
+    // within a value -- (B, A), (D, C) -- they cost config E 5 % and made the LEAN shapes spill)
     auto sample = [&](int k) {
       const float *t = win + doff(k);
       const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
@@ -1000,7 +1156,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const float x = (S::LEAN ? sample(k) : pd[k]) - mean;  // mean = 0 without normalisation: x - 0 == x
-      const float d = x - tmp[k];
+      const float d = x - tmpv(k);
       float w, e;
       if (COST == 0) {
         e = d;
@@ -1025,6 +1181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       r0 = ab.total();
       b0 = ex.total();
       if (NOP == 2) b1 = ey.total();
+    }
     }
   };
   // The evaluation is unrolled over the values; the loop holds one copy of it (start evaluation and every
@@ -1077,9 +1234,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (cnt == 1) sq_init = sq;
       mares_old = mares;
       mares = div_n(r0);
-      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
-                        ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
-                        ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+      // the two rate tests count only from min_iter on: their divisions run in a wave-uniform branch that
+      // the op-points (min_iter = max_iter) never enter
+      bool rates = true;
+      if (__builtin_amdgcn_ballot_w64(cnt >= a.min_iter) != 0)
+        rates = (cnt < a.min_iter) | ((sq / sq_init >= a.dp_thresh_sq) & (mares / mares_old <= a.dr_thresh));
+      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) & rates;
       if (!keep) converged = true;
     }
     first = false;
