@@ -1023,6 +1023,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   bool converged = false;
   float b0 = 0.0f, b1 = 0.0f;
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  int lpos0 = -0x7fffffff, lpos1 = 0;  // integer tap position of the tile in LDS (none yet)
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1):
   // the residual sums r0 = sum |w|, b0 = sum dx e (, b1 = sum dy e); with `out`, the weights w are stored
   auto evaluate = [&](float &r0, float *out, auto store_t) {
@@ -1034,6 +1035,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
     // window origin: the D tap of value 0, one row above and one column left of the A tap
     const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
+    // the tile is a function of (pos0, pos1) alone: reloaded only when a patch of the wave has moved to
+    // another integer tap position since its last load (late iterations mostly stay put)
+    if (__builtin_amdgcn_ballot_w64(pos0 != lpos0 || pos1 != lpos1) != 0) {
+    lpos0 = pos0;
+    lpos1 = pos1;
     wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
     if (S::LEAN) {  // in batches of 4 loads: bounded registers in flight
 #pragma unroll
@@ -1058,6 +1064,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     }
     wave_lds_sync();
+    }
     if constexpr (PK && STORE == 0) {
       // value pairs (k, k + KP): tap X of both values is one ds_read2_b32 into a register pair (taps PD floats
       // apart), then ((w0 A + w1 B) + w2 C) + w3 D, (x - mean) - tmp and gx e run two values per packed
