@@ -164,9 +164,12 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        gated against the exact path; the one option that changes results);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch;
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
- *   "graph" (0/1/2, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
+ *   "graph" (0/1/2/3, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
  *                        parameters repeat (re-captured when they change); 1 captures single-stream
- *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined);
+ *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined; the
+ *                        two-stream pipeline only under a HIP runtime >= 7.2: the one bundled with
+ *                        PyTorch's ROCm 7.0 build crashes capturing its mutually waiting lanes, so there
+ *                        it is issued eagerly); 3 captures the pipeline whatever the runtime (diagnostic);
  *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1) and "chunk" (frames, default 0 =
  *                        the batch split evenly over the streams): a batch is cut into chunks that run
  *                        round-robin on that many HIP streams with separate workspaces, overlapping one

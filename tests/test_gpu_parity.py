@@ -5,6 +5,8 @@ patterns), stage by stage: pyramid, flow after patch aggregation per scale, flow
 scale, and the full-resolution output.  At BASELINE's full 1080p size the check is the same (the oracle
 finishes in well under a second per pair).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -175,11 +177,12 @@ def test_batch_equals_singles(od, ctx):
     b = torch.from_numpy(np.stack([x[1] for x in pairs])).cuda()
     p = od.oppoint(2, w, 1, 1)
     outs = []
-    configs = ((1, 0, 1, 0), (1, 0, 1, 0), (1, 0, 0, 0), (3, 2, 1, 0), (4, 1, 1, 0),
-               (1, 2, 1, 1), (1, 2, 1, 1), (1, 2, 0, 1), (1, 1, 1, 1), (1, 3, 0, 1))
+    configs = ((1, 0, 1, 0), (1, 0, 1, 0), (1, 0, 0, 0), (3, 2, 1, 0), (4, 1, 1, 0), (3, 2, 2, 0), (3, 2, 2, 0),
+               (1, 2, 1, 1), (1, 2, 1, 1), (1, 2, 0, 1), (1, 1, 1, 1), (1, 3, 0, 1), (1, 2, 2, 1))
     for streams, chunk, graph, pipeline in configs:
-        # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams;
-        # the two-stream pipeline (ragged last chunk; captured + replayed, and eager)
+        # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams (also
+        # captured with their fork / join); the two-stream pipeline (ragged last chunk; eager -- graph 2 under
+        # torch's HIP runtime too, see test_pipeline_capture_native)
         ctx.set_option("streams", streams)
         ctx.set_option("chunk", chunk)
         ctx.set_option("graph", graph)
@@ -227,6 +230,25 @@ def test_full_1080p_bitexact(oracle, od, ctx):
     got = ctx.run_host(a, b, p)
     ref = oracle.run_u8(a, b, oracle.oppoint(2, 1920, 1, 1))
     assert_bitexact(got, ref, "1080p op2")
+
+
+def test_pipeline_capture_native(od, tmp_path):
+    """The two-stream pipeline captured as a HIP graph (option graph=2) in a process of its own, i.e. under the
+    ROCm runtime libofdis.so links (>= 7.2): captured, replayed, bit-identical to its eager issue.  (Under the
+    runtime bundled with PyTorch the pipeline is issued eagerly: that runtime crashes in hipStreamEndCapture
+    on the lanes' mutual waits, tools/capture_repro.hip.)"""
+    import subprocess
+    from test_host_abi import ROOT
+    libdir = os.path.dirname(od._lib.LIB_PATH)
+    exe = str(tmp_path / "pipe_capture")
+    subprocess.run(["g++", "-std=c++14", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "pipe_capture.cpp"), "-L", libdir, "-lofdis",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True, capture_output=True, timeout=300)
+    r = subprocess.run([exe, "2"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, OFDIS_TRACE="1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("same 1") == 2, r.stdout
+    assert "graph: capture (kind 2" in r.stderr and "graph: captured rc 0 end 0" in r.stderr, r.stderr[-2000:]
 
 
 def test_oflow_hpp_dropin_program(oracle, od, tmp_path):

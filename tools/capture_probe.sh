@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${1:-capture}; mkdir -p "$OUT"
-for m in 0 1 3 2; do
+for m in ${MODES:-0 1 3 2 5 4}; do
   echo "== mode $m"
   timeout -k 10 60 tools/bin/capture_repro $m 3 > "$OUT/mode$m.log" 2>&1
   rc=$?
