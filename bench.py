@@ -250,13 +250,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}")
+    # OFDIS_BENCH_REHEARSAL=1: rehearse the multi-rank path on a box with fewer GPUs than ranks -- ranks share
+    # the GPUs round robin and the control collectives go over gloo (RCCL refuses two ranks on one GPU)
+    rehearsal = os.environ.get("OFDIS_BENCH_REHEARSAL") == "1"
+    gpu = local % max(1, torch.cuda.device_count()) if rehearsal else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
 
     import of_dis_amd as od
     from of_dis_amd import distributed as odd
