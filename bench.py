@@ -112,9 +112,13 @@ def kernel_roofline(od, p, W, H, B, per_launch, cfg, steps, kernels, name):
             traffic = None if ent is None else round(ent["bytes_per_launch"])
         except Exception:
             traffic = None
-    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_us": round(k["avg_us"], 2)}
+    out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_us": round(k["avg_us"], 2)}
+    if name == "patch":  # not an HBM-bound kernel: say what bounds it
+        out["limiter"] = ("VALU issue: SQ_ACTIVE_INST_VALU x waves/SIMD ~ 1.0 of SIMD cycles at configs C and E "
+                          "(profiles/r02/pmc); bytes = compulsory per patch (template, gradients, one window, outputs)")
+    return out
 
 
 def params_of(mod, cfg):

@@ -80,6 +80,7 @@ struct ofdis_context {
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
+  int opt_sstream = 1;         // tall levels: the streaming form of the fused launch (0: two launches, A/B)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
@@ -486,6 +487,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
         timed(c, 7, s, [&] {
           if (tv_smsys_ok(tv)) {
             launch_tv_smsys(tv, s);
+          } else if (c->opt_sstream && tv_smsys_stream_ok(tv)) {
+            launch_tv_smsys_stream(tv, s);
           } else {
             launch_tv_smooth(tv, s);
             launch_tv_system(tv, s);
@@ -1172,6 +1175,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
+      {"smsys_stream", &ofdis_context::opt_sstream, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
@@ -1235,8 +1239,10 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
     const int n_inner = p->usetvref ? p->tv_innerit * (g.level + 1) : 0;
     if (k == "tv_sor") b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
     if (k == "tv_system") b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
-    if (k == "patch") b += (double)g.npatch * (12.0 * novals + 4.0 * (p->p_samp_s + 1) * (p->p_samp_s + 1) * noc *
-                                                                   (double)(p->max_iter + 1) + 4.0 * (nop + novals));
+    // patch: per patch the template + gradients, ONE (p+1)^2 target window, the outputs (the compulsory bytes;
+    // re-reads of the window over the iterations are cache-resident, and the kernel is VALU-issue bound)
+    if (k == "patch") b += (double)g.npatch * (12.0 * novals + 4.0 * (p->p_samp_s + 1) * (p->p_samp_s + 1) * noc +
+                                               4.0 * (nop + novals));
     if (k == "aggregate") b += px * 4.0 * nop + (double)g.npatch * 4.0 * (nop + novals);
     if (k == "pyr_pad_grad") b += 2.0 * (px * 4.0 * noc + 3.0 * g.W * g.H * 4.0 * noc);
     if (k == "pyr_down" && g.level > p->sc_l) b += 2.0 * noc * 4.0 * (4.0 * px + px);
