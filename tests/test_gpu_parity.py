@@ -59,6 +59,8 @@ CASES = [
     (240, 120, 1, 2, 4, {"usefbcon": 1, "max_iter": 16, "min_iter": 16}),  # ... depth (right camera clamp)
     (400, 300, 1, 1, 2, {"sc_l": 0, "sc_f": 2}),              # 300 rows: 5 row groups x 3 sweep waves
     (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows: register pipeline, 1024 threads
+    (300, 280, 3, 1, 2, {"sc_l": 0, "sc_f": 1}),              # RGB, 280 rows: streaming smoothness + system
+    (200, 300, 3, 2, 2, {"sc_l": 0, "sc_f": 1}),              # ... RGB depth, tall (unfolded) layout
     (160, 120, 1, 1, 2, {"omp_build": 1}),                    # USE_OPENMP build: point SOR (solver.c:34-78)
     (240, 200, 1, 1, 2, {"sc_l": 1, "sc_f": 2, "tv_solverit": 2}),  # fused system + SOR: 2 sweeps, 2 row groups
     (248, 232, 1, 2, 2, {"sc_l": 1, "sc_f": 2}),              # ... depth, 116 rows (2 row groups)
