@@ -138,8 +138,6 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
 bool tv_smsys_ok(const TvArgs &a);
 void launch_tv_smsys(const TvArgs &a, hipStream_t s);
-bool tv_smsys_stream_ok(const TvArgs &a);
-void launch_tv_smsys_stream(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);

@@ -2071,141 +2071,6 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
   }
 }
 
-// ---- streaming smoothness + system for tall levels (h > 256, where k_tv_smsys's halo re-reads lose)
-// A workgroup walks kSsSeg consecutive rows of one frame's skewed plane in chunks of RB rows, keeping the
-// staged (wx, [wy,] du [, dv]) rows and the s rows it still needs in LDS rings: every row is staged once (plus
-// 4 halo rows per segment) and s never goes to memory.  Per chunk: stage rows r0+2 .. r1+1, s of rows
-// r0+1 .. r1, the system of rows r0 .. r1-1 (three barriers; a slot is overwritten only after its last use).
-// Same functions as k_tv_smsys (smooth_compute, sys_compute), same bits.
-constexpr int kSsSeg = 32;
-__host__ __device__ __forceinline__ int smsys_stream_rb(int h, int nop) {
-  const size_t st = nop == 2 ? 16 : 8;
-  return (size_t)(4 + 4) * h * st + (size_t)(4 + 2) * h * 4 <= 80 * 1024 ? 4 : 2;
-}
-__host__ __device__ __forceinline__ size_t smsys_stream_lds(int h, int nop) {
-  const int rb = smsys_stream_rb(h, nop);
-  return (size_t)(rb + 4) * h * (nop == 2 ? 16 : 8) + (size_t)(rb + 2) * h * 4;
-}
-
-template <int NOP, int NOC>
-__global__ __launch_bounds__(256) void k_tv_smsys_stream(TvArgs a) {
-  using SV = typename std::conditional<NOP == 2, float4, float2>::type;  // (wx, du) or (wx, wy, du, dv)
-  extern __shared__ float4 ss_mem[];
-  const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
-  const int rb = smsys_stream_rb(h, NOP), NS = rb + 4, NSS = rb + 2;
-  SV *st = reinterpret_cast<SV *>(ss_mem);
-  float *sl = reinterpret_cast<float *>(st + (size_t)NS * h);
-  const int f = blockIdx.x, R0 = blockIdx.y * kSsSeg, R1 = min(R0 + kSsSeg, rows);
-  const long f0 = (long)f * a.sp;
-  const bool first = a.first_iter != 0;
-  auto prow = [&](int r) { return a.wrap ? (r < 0 ? r + w : (r >= w ? r - w : r)) : (r < 0 || r >= rows ? -1 : r); };
-  auto pix = [&](int r, int y, int &x) {  // plane (row, column) -> pixel x; false outside the level
-    if (r < 0) return false;
-    x = r - y;
-    if (a.wrap) {
-      if (x < 0) x += w;
-      return true;
-    }
-    return x >= 0 && x < w;
-  };
-  auto sti = [&](int r) { return ((r - R0 + 2) % NS) * h; };   // staged ring row base of logical row r
-  auto sli = [&](int r) { return ((r - R0 + 1) % NSS) * h; };  // s ring row base of logical row r
-  for (int r0 = R0; r0 < R1; r0 += rb) {
-    const int r1 = min(r0 + rb, R1);
-    // ---- stage rows (first chunk: R0 - 2 ..) r0 + 2 .. r1 + 1
-    const int sa = r0 == R0 ? R0 - 2 : r0 + 2, sn = r1 + 2 - sa;
-    for (int i = threadIdx.x; i < sn * h; i += blockDim.x) {
-      const int ri = i / h, y = i - ri * h, r = sa + ri;
-      const int pr = prow(r);
-      SV v;
-      if (NOP == 2) {
-        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (pr >= 0) {
-          const long o = f0 + (long)pr * h + y;
-          q = make_float4(a.wxs[o], a.wys[o], a.du[o], a.dv[o]);
-        }
-        v = *reinterpret_cast<SV *>(&q);
-      } else {
-        float2 q = make_float2(0.f, 0.f);
-        if (pr >= 0) {
-          const long o = f0 + (long)pr * h + y;
-          q = make_float2(a.wxs[o], a.du[o]);
-        }
-        v = *reinterpret_cast<SV *>(&q);
-      }
-      st[sti(r) + y] = v;
-    }
-    __syncthreads();
-    // ---- s of rows (first chunk: R0 - 1 ..) r0 + 1 .. r1
-    const int ma = r0 == R0 ? R0 - 1 : r0 + 1, mn = r1 + 1 - ma;
-    for (int i = threadIdx.x; i < mn * h; i += blockDim.x) {
-      const int ri = i / h, y = i - ri * h, r = ma + ri;
-      int x;
-      float sv = 0.0f;
-      if (pix(prow(r), y, x)) {
-        const int bc = sti(r), bm = sti(r - 1), bp = sti(r + 1);
-        const SV q0 = st[bc + y], q1 = st[x > 0 ? bm + y : bc + y], q2 = st[x < w - 1 ? bp + y : bc + y];
-        const SV q3 = st[y > 0 ? bm + y - 1 : bc + y], q4 = st[y < h - 1 ? bp + y + 1 : bc + y];
-        float wx5[5], du5[5], wy5[5], dv5[5];
-        if constexpr (NOP == 2) {
-          const float4 qq[5] = {q0, q1, q2, q3, q4};
-#pragma unroll
-          for (int k = 0; k < 5; ++k) { wx5[k] = qq[k].x; wy5[k] = qq[k].y; du5[k] = qq[k].z; dv5[k] = qq[k].w; }
-        } else {
-          const float2 qq[5] = {q0, q1, q2, q3, q4};
-#pragma unroll
-          for (int k = 0; k < 5; ++k) { wx5[k] = qq[k].x; du5[k] = qq[k].y; wy5[k] = 0.0f; dv5[k] = 0.0f; }
-        }
-        sv = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
-      }
-      sl[sli(r) + y] = sv;
-    }
-    __syncthreads();
-    // ---- the system of rows r0 .. r1 - 1
-    for (int i = threadIdx.x; i < (r1 - r0) * h; i += blockDim.x) {
-      const int ri = i / h, y = i - ri * h, rr = r0 + ri;
-      int x;
-      if (!pix(prow(rr), y, x)) continue;
-      const int yu = y > 0 ? -1 : 0, yd = y < h - 1 ? 1 : 0;  // clamped columns; absent neighbours are discarded
-      const int sc = sli(rr) + y, sm = sli(rr - 1) + y, sp1 = sli(rr + 1) + y;
-      const int tc = sti(rr) + y, tm = sti(rr - 1) + y, tp = sti(rr + 1) + y;
-      const int s5[5] = {sc, sm, sp1, sm + yu, sp1 + yd};
-      const int t5[5] = {tc, tm, tp, tm + yu, tp + yd};
-      float S5[5], X5[5], Y5[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        S5[k] = sl[s5[k]];
-        const SV q = st[t5[k]];
-        X5[k] = q.x;
-        if constexpr (NOP == 2) Y5[k] = q.y; else Y5[k] = 0.0f;
-      }
-      const SV qc = st[tc];
-      float uc, vc;
-      if constexpr (NOP == 2) { uc = qc.z; vc = qc.w; } else { uc = qc.y; vc = 0.0f; }
-      const long idx = f0 + (long)prow(rr) * h + y;
-      const float m = a.mask[idx];
-      const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)prow(rr) * h + y);
-      float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
-#pragma unroll
-      for (int ch = 0; ch < NOC; ++ch) {
-        const unsigned o = qd + (unsigned)(ch * a.sp);
-        lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
-        lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
-      }
-      float4 c0, c1;
-      sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, uc, vc, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz, lIyz, c0, c1);
-      if (NOP == 2) {
-        float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
-        C[0] = c0;
-        C[1] = c1;
-      } else {
-        reinterpret_cast<float4 *>(a.coef)[idx] = c0;
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // Generic exact-order SOR (any size / sweep count): one workgroup per frame, in-place skewed arrays in
 // global memory, one barrier per wavefront step.  Pixel (x, y) of sweep s runs at step t = x + y + 2 s:
 // its left/top neighbours of the same sweep ran at t-1, its right/bottom neighbours of the previous
@@ -3148,6 +3013,83 @@ __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
   }
 }
 
+// The same for depth (nop = 1): lane i of wave wv owns the four output columns xb + 4i .. xb + 4i + 3
+// (xb = block + 256 wv): one 16-byte store per row, 1 KiB contiguous per wave-instruction.
+__global__ __launch_bounds__(256) void k_upsample_rows1(UpArgs a) {
+  __shared__ float src[kUpSrcRows][kUpCols / 2 + 8];
+  const int y0 = blockIdx.y * kUpRows, f = blockIdx.z;
+  const int dx0 = blockIdx.x * kUpCols + a.offx;
+  const int fct_i = 1 << a.log2s;
+  const float fct = (float)fct_i, half_inv = 1.0f / (float)(2 * fct_i);
+  const float *F = a.flow + (long)f * a.wl * a.hl;
+  auto src_row = [&](int dy, float &fy) {
+    fy = (float)(2 * dy + 1 - fct_i) * half_inv;
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    return sy;
+  };
+  auto clip_row = [&](int r) { return r >= 0 ? (r < a.hl ? r : a.hl - 1) : 0; };
+  const int yl = min(y0 + kUpRows, a.H0) - 1;
+  float dummy;
+  const int r_first = clip_row(src_row(y0 + a.offy, dummy));
+  const int r_last = clip_row(src_row(yl + a.offy, dummy) + 1);
+  const int nr = r_last - r_first + 1;
+  const int c_lo = max(0, (int)floorf((float)(2 * dx0 + 1 - fct_i) * half_inv));
+  const int ncol = kUpCols / fct_i + 2;
+  for (int k = threadIdx.x; k < nr * ncol; k += blockDim.x) {
+    const int col = k % ncol, r = k / ncol;
+    src[r][col] = F[(long)(r_first + r) * a.wl + min(c_lo + col, a.wl - 1)] * fct;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int xb = blockIdx.x * kUpCols + wv * 256 + 4 * lane;
+  int cc[4];
+  float fxs[4];
+  bool lin[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int dx = xb + i + a.offx;
+    float fx = (float)(2 * dx + 1 - fct_i) * half_inv;
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    bool l = true;
+    if (sx + 1 >= a.wl) {
+      l = false;
+      if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
+    }
+    cc[i] = min(max(sx - c_lo, 0), kUpCols / 2 + 6);  // columns past W0 are computed, never stored
+    fxs[i] = fx;
+    lin[i] = l;
+  }
+#pragma unroll
+  for (int i = 0; i < kUpRows; ++i) {
+    const int y = y0 + i;
+    if (y >= a.H0) break;
+    float fy;
+    const int sy = src_row(y + a.offy, fy);
+    const int j0 = clip_row(sy) - r_first, j1 = clip_row(sy + 1) - r_first;
+    const float b0 = 1.f - fy, b1 = fy;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = cc[q];
+      const float s00 = src[j0][c], s10 = src[j1][c];
+      const float h0 = lin[q] ? s00 * (1.f - fxs[q]) + src[j0][c + 1] * fxs[q] : s00;
+      const float h1 = lin[q] ? s10 * (1.f - fxs[q]) + src[j1][c + 1] * fxs[q] : s10;
+      v[q] = h0 * b0 + h1 * b1;
+    }
+    float *row = a.out + ((long)f * a.H0 + y) * a.W0;
+    if (xb + 4 <= a.W0) {
+      *reinterpret_cast<v4f *>(row + xb) = v4f{v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (xb + q < a.W0) row[xb + q] = v[q];
+    }
+  }
+}
+
 // Generic path (any nop, 2^l = 1, unaligned output): one output pixel per thread.
 __global__ __launch_bounds__(256) void k_upsample(UpArgs a) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
@@ -3300,22 +3242,6 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
       k_tv_smsys<1, 3><<<grid, 256, lds, s>>>(a);
   }
 }
-bool tv_smsys_stream_ok(const TvArgs &a) { return a.smsys && smsys_stream_lds(a.h, a.nop) <= 80 * 1024; }
-void launch_tv_smsys_stream(const TvArgs &a, hipStream_t s) {
-  const dim3 grid(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), kSsSeg));
-  const size_t lds = smsys_stream_lds(a.h, a.nop);
-  if (a.nop == 2) {
-    if (a.noc == 1)
-      k_tv_smsys_stream<2, 1><<<grid, 256, lds, s>>>(a);
-    else
-      k_tv_smsys_stream<2, 3><<<grid, 256, lds, s>>>(a);
-  } else {
-    if (a.noc == 1)
-      k_tv_smsys_stream<1, 1><<<grid, 256, lds, s>>>(a);
-    else
-      k_tv_smsys_stream<1, 3><<<grid, 256, lds, s>>>(a);
-  }
-}
 void launch_tv_system(const TvArgs &a, hipStream_t s) {
   const dim3 grid(ceil_div(a.sp, 256), a.n);
   if (a.nop == 2) {
@@ -3456,6 +3382,8 @@ void launch_init_area(const InitArgs &a, hipStream_t s) {
 void launch_upsample(const UpArgs &a, hipStream_t s) {
   if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
     k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
+  else if (a.nop == 1 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
+    k_upsample_rows1<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
   else
     k_upsample<<<dim3(ceil_div(a.W0, 256), a.H0, a.n), 256, 0, s>>>(a);
 }

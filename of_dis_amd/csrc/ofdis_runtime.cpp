@@ -80,7 +80,6 @@ struct ofdis_context {
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
-  int opt_sstream = 1;         // tall levels: the streaming form of the fused launch (0: two launches, A/B)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
@@ -487,8 +486,6 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
         timed(c, 7, s, [&] {
           if (tv_smsys_ok(tv)) {
             launch_tv_smsys(tv, s);
-          } else if (c->opt_sstream && tv_smsys_stream_ok(tv)) {
-            launch_tv_smsys_stream(tv, s);
           } else {
             launch_tv_smooth(tv, s);
             launch_tv_system(tv, s);
@@ -1175,7 +1172,6 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
-      {"smsys_stream", &ofdis_context::opt_sstream, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
