@@ -43,6 +43,18 @@ __device__ __forceinline__ float ssemax(float a, float b) { return (a > b) ? a :
 
 inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
+// XCD-aware block order (T1 of the CDNA guide): the dispatcher deals workgroups to the 8 XCDs round robin by
+// linear id, each XCD with its own L2.  Linear id L runs block number L / 8 of the contiguous eighth of the
+// grid (frame-major) that L's XCD serves, so blocks that share data -- neighbouring rows of a skewed plane,
+// neighbouring tiles of a frame -- are L2 neighbours.  Bijective for any grid size; uniform (scalar) math.
+__device__ __forceinline__ uint3 xcd_block() {
+  const unsigned gx = gridDim.x, gy = gridDim.y, gxy = gx * gy, nwg = gxy * gridDim.z;
+  const unsigned orig = (blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x;
+  const unsigned q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const unsigned w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  return make_uint3(w % gx, (w / gx) % gy, w / gxy);
+}
+
 
 
 // ------------------------------------------------------------------------------------------------ pyramid
@@ -873,12 +885,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 // for the L1 and pseudo-Huber losses' square roots and division).
 template <int NOP, int P, int NOC, int MINW, int COST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchw(PatchArgs a) {
+  const uint3 xb = xcd_block();
   using S = PatchShape<P, NOC>;
   constexpr int PAIRS = S::PAIRS, ODD = S::ODD, V = S::V, RS = S::RS;
   extern __shared__ __attribute__((aligned(16))) float win_all[];
   const LevelGeom &g = a.g;
   const int s8 = threadIdx.x & 7;
-  const long gp = (long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const long gp = (long)xb.x * 32 + (threadIdx.x >> 3);
   const bool live = gp < (long)a.n * g.npatch;
   const long gq = live ? gp : 0;
   const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
@@ -1351,19 +1364,20 @@ __device__ __forceinline__ void aggregate_cg_one(const AggArgs &a, const CgPatch
 // With a complementary grid, its patches are staged through LDS 256 at a time (all of them, in id order:
 // an optimised position is arbitrary) and each pixel tests its reach.
 __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
+  const uint3 xb = xcd_block();
   __shared__ CgPatch cgs[256];
   const LevelGeom &g = a.g;
-  const int x = blockIdx.x * 64 + (threadIdx.x & 63), f = blockIdx.z;
+  const int x = xb.x * 64 + (threadIdx.x & 63), f = xb.z;
   float we[4], f0[4], f1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     we[r] = f0[r] = f1[r] = 0.0f;
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * r;
+    const int y = xb.y * 16 + (threadIdx.x >> 6) + 4 * r;
     if (x < g.w && y < g.h) aggregate_own(a, x, y, f, we[r], f0[r], f1[r]);
   }
   if (a.cg_p_iter) {
     const int hp = a.p / 2;
-    const int tx0 = blockIdx.x * 64, ty0 = blockIdx.y * 16;
+    const int tx0 = xb.x * 64, ty0 = xb.y * 16;
     const float *CPI = a.cg_p_iter + (long)f * g.npatch * a.nop;
     const float *CPW = a.cg_pweight + (long)f * g.npatch * a.novals;
     for (int c0 = 0; c0 < g.npatch; c0 += 256) {
@@ -1405,7 +1419,7 @@ __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
   const long plane = (long)g.w * g.h;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 6) + 4 * r;
+    const int y = xb.y * 16 + (threadIdx.x >> 6) + 4 * r;
     if (x >= g.w || y >= g.h) continue;
     float v0 = f0[r], v1 = f1[r];
     if (we[r] > 0) {
@@ -1484,9 +1498,10 @@ __device__ __forceinline__ void tv_prep_store(const TvArgs &a, int x, int y, int
 constexpr int kTileW = 64, kTileP = 66;
 template <int NP, int TH>
 __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
+  const uint3 xb = xcd_block();
   __shared__ float sm[NP][TH][kTileP];  // mask, wx, wy, t[noc], dt[noc]
   constexpr int TD = kTileW + TH - 1;
-  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
+  const int x0 = xb.x * kTileW, y0 = xb.y * TH, f = xb.z;
   const int tx = threadIdx.x & 63, np = NP;
   for (int yl = threadIdx.x >> 6; yl < TH; yl += 4) {
     const int x = x0 + tx, y = y0 + yl;
@@ -1563,12 +1578,14 @@ __device__ __forceinline__ void tv_deriv2_px(const TvArgs &a, long pl, int kk) {
 }
 
 __global__ __launch_bounds__(256) void k_tv_deriv1(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk < a.sp) tv_deriv1_px(a, blockIdx.y, kk);
+  const uint3 b = xcd_block();
+  const int kk = b.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_deriv1_px(a, b.y, kk);
 }
 __global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk < a.sp) tv_deriv2_px(a, blockIdx.y, kk);
+  const uint3 b = xcd_block();
+  const int kk = b.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_deriv2_px(a, b.y, kk);
 }
 
 #define DNORM (0.1f * 0.1f)
@@ -1950,13 +1967,15 @@ __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
 
 template <int NOP>
 __global__ __launch_bounds__(256) void k_tv_smooth(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk < a.sp) tv_smooth_px<NOP>(a, blockIdx.y, kk, a.first_iter != 0);
+  const uint3 b = xcd_block();
+  const int kk = b.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_smooth_px<NOP>(a, b.y, kk, a.first_iter != 0);
 }
 template <int NOP, int NOC>
 __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (kk < a.sp) tv_system_px<NOP, NOC>(a, blockIdx.y, kk);
+  const uint3 b = xcd_block();
+  const int kk = b.x * blockDim.x + threadIdx.x;
+  if (kk < a.sp) tv_system_px<NOP, NOC>(a, b.y, kk);
 }
 
 // ---- smoothness + system in one launch (compute_smoothness + the system of refine_variational.cpp:195-199)
@@ -2842,9 +2861,10 @@ __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
 
 template <int TH>
 __global__ __launch_bounds__(256) void k_tv_final(TvArgs a) {
+  const uint3 xb = xcd_block();
   __shared__ float sm[2][TH][kTileP];
   constexpr int TD = kTileW + TH - 1;
-  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
+  const int x0 = xb.x * kTileW, y0 = xb.y * TH, f = xb.z;
   for (int i = threadIdx.x; i < TD * TH; i += 256) {  // skewed side: diagonal segments
     const int yy = i & (TH - 1), dd = i / TH, xl = dd - yy;
     const int x = x0 + xl, y = y0 + yy;
