@@ -38,13 +38,16 @@ CONFIGS = {
     # 2048 pairs per GPU per step = two 1024-pair chunks on two streams (measured best: 1024 pairs 266k,
     # 1536 282k, 2048 298k, 3072 285k, 4096 293k MPix/s; profiles/r02/sweep3)
     "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 2048),
-    # op-point 3 as the config text states it ("finer scale, L1 cost"): op3 values with costfct = 1
-    "C": ("run_OF_RGB", 1920, 1080, 3, 1, 3, "6 2 16 16 0.05 0.95 0 12 0.75 0 1 1 1 10 10 5 1 3 1.6 2", 64),
+    # op-point 3 as the config text states it ("finer scale, L1 cost"): op3 values with costfct = 1.
+    # 512 pairs = two 256-pair chunks on two streams (64: 6.9k, 128: 7.4k, 256: 7.8k, 512: 8.1k, 1024: 8.2k
+    # MPix/s; profiles/r02/ab/ab_batch*)
+    "C": ("run_OF_RGB", 1920, 1080, 3, 1, 3, "6 2 16 16 0.05 0.95 0 12 0.75 0 1 1 1 10 10 5 1 3 1.6 2", 512),
     # op-point 3 as run_dense.cpp:248-253 defines it (costfct 0, L2); SURVEY §8(d): report both
-    "C2": ("run_OF_RGB", 1920, 1080, 3, 1, 3, None, 64),
+    "C2": ("run_OF_RGB", 1920, 1080, 3, 1, 3, None, 512),
     "D": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 32),
-    # op-point 4 values with tv_innerit = 10
-    "E": ("run_DE_INT", 3840, 2160, 1, 2, 4, "7 2 128 128 0.05 0.95 0 12 0.75 0 1 0 1 10 10 5 10 3 1.6 2", 256),
+    # op-point 4 values with tv_innerit = 10; 512 = two 256-pair chunks on two streams
+    # (256: 6.85k, 512: 7.57k, 1024: 7.54k MPix/s; profiles/r02/ab/ab_batch*)
+    "E": ("run_DE_INT", 3840, 2160, 1, 2, 4, "7 2 128 128 0.05 0.95 0 12 0.75 0 1 0 1 10 10 5 10 3 1.6 2", 512),
 }
 METRIC = "MPix/s (and frames/sec) 1080p op-point-2; avg EPE vs CPU ref"
 
