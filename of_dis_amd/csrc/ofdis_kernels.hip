@@ -887,6 +887,9 @@ template <int NOP, int P, int NOC, int MINW, int COST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchw(PatchArgs a) {
   const uint3 xb = xcd_block();
   using S = PatchShape<P, NOC>;
+  // a big shape (LEAN: samples read twice instead of kept) keeps its samples when compiled for one wave per
+  // SIMD (MINW 1): measured faster for the L2 cost, slower for the square-root costs (config C2 / C)
+  constexpr bool LEAN = S::LEAN && MINW > 1;
   constexpr int PAIRS = S::PAIRS, ODD = S::ODD, V = S::V, RS = S::RS;
   extern __shared__ __attribute__((aligned(16))) float win_all[];
   const LevelGeom &g = a.g;
@@ -910,7 +913,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   // PK: the per-value arithmetic of an evaluation on value pairs (k, k + 1) in packed fp32 -- every lane of a
   // v_pk_mul_f32 / v_pk_add_f32 rounds like the scalar instruction, so the pairs keep each value's operation
   // order; the taps of a pair come straight from one ds_read2_b32 into a register pair
-  constexpr bool PK = !S::LEAN && S::ODD == 0 && V % (2 * S::KP) == 0;
+  constexpr bool PK = !LEAN && S::ODD == 0 && V % (2 * S::KP) == 0;
   float *win = win_all + (threadIdx.x >> 3) * S::WIN;
   // value of slot k of this lane, and its D-tap offset in the window tile
   auto value = [&](int k) { return k < PAIRS ? s8 + 8 * k : 8 * PAIRS + (s8 & 3); };
@@ -1015,7 +1018,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   };
   const float *Bimg = a.img_b + f * fs;
   // window loads of this lane: float4 e = s8 + 8 j of the (P+1) x Q4 tile
-  constexpr int LPLK = S::LEAN ? 1 : S::LPL;
+  constexpr int LPLK = LEAN ? 1 : S::LPL;
   int gofs[LPLK], lofs[LPLK];
   auto woff = [&](int j, int &go, int &lo) {
     const int e = s8 + 8 * j, e2 = e < S::NQ ? e : S::NQ - 1;
@@ -1023,7 +1026,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     go = row * W * NOC + c4 * 4;
     lo = row * RS + c4 * 4;
   };
-  if (!S::LEAN) {
+  if (!LEAN) {
 #pragma unroll
     for (int j = 0; j < LPLK; ++j) woff(j, gofs[j], lofs[j]);
   }
@@ -1054,7 +1057,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     lpos0 = pos0;
     lpos1 = pos1;
     wave_lds_sync();  // the previous evaluation's tap reads are done before the tile is overwritten
-    if (S::LEAN) {  // in batches of 4 loads: bounded registers in flight
+    if (LEAN) {  // in batches of 4 loads: bounded registers in flight
 #pragma unroll
       for (int j0 = 0; j0 < S::LPL; j0 += 4) {
         float4_u t[4];
@@ -1087,8 +1090,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       const unsigned wb = (unsigned)(uintptr_t)win;
       f2p pd2[V2], q[2][4];
       auto issue = [&](auto jc) {  // the four taps of pair j (in flight: this pair and the next)
-        constexpr int j = decltype(jc)::value, i = j % KP, o = 2 * (j / KP) * PD;
-        const unsigned b = wb + 4u * (unsigned)dbase[i];
+        constexpr int j = decltype(jc)::value, i = j % KP, o0 = 2 * (j / KP) * PD;
+        constexpr bool imm = o0 + RS + NOC + PD <= 255;  // else the row offset goes into the address
+        constexpr int o = imm ? o0 : 0;
+        const unsigned b = wb + 4u * (unsigned)dbase[i] + (imm ? 0u : 4u * (unsigned)o0);
         q[j & 1][0] = lds_read2<o, o + PD>(b);                        // D
         q[j & 1][1] = lds_read2<o + NOC, o + NOC + PD>(b);            // C
         q[j & 1][2] = lds_read2<o + RS, o + RS + PD>(b);              // B
@@ -1159,15 +1164,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       const float D = t[0], C = t[NOC], Bv = t[RS], A = t[RS + NOC];
       return w0 * A + w1 * Bv + w2 * C + w3 * D;
     };
-    constexpr int VK = S::LEAN ? 1 : V;
+    constexpr int VK = LEAN ? 1 : V;
     float pd[VK];
     float mean = 0.0f;
-    if (a.patnorm > 0 || !S::LEAN) {
+    if (a.patnorm > 0 || !LEAN) {
       EigenAcc<PAIRS, ODD> m;
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const float x = sample(k);
-        if (!S::LEAN) pd[k] = x;
+        if (!LEAN) pd[k] = x;
         m.add(k, x);
       }
       if (a.patnorm > 0) mean = div_n(m.total());
@@ -1175,7 +1180,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     EigenAcc<PAIRS, ODD> ab, ex, ey;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const float x = (S::LEAN ? sample(k) : pd[k]) - mean;  // mean = 0 without normalisation: x - 0 == x
+      const float x = (LEAN ? sample(k) : pd[k]) - mean;  // mean = 0 without normalisation: x - 0 == x
       const float d = x - tmpv(k);
       float w, e;
       if (COST == 0) {
@@ -3181,14 +3186,16 @@ static void patch8(const PatchArgs &a, hipStream_t s) {
     k_patch8<1, PAIRS, ODD><<<ceil_div(patches, 32), 256, 0, s>>>(a);
 }
 // MINW1 / MINW2: waves per SIMD for the depth (nop 1) / flow (nop 2) forms, chosen so that nothing spills
-template <int P, int NOC, int MINW1, int MINW2>
+// MINW0: waves per SIMD of the L2-cost (costfct 0) instances
+template <int P, int NOC, int MINW1, int MINW2, int MINW0 = 0>
 static void patchw(const PatchArgs &a, hipStream_t s) {
   const long patches = (long)a.n * a.g.npatch;
   const size_t lds = sizeof(float) * 32 * PatchShape<P, NOC>::WIN;
   const dim3 grid(ceil_div(patches, 32));
+  constexpr int M01 = MINW0 ? MINW0 : MINW1, M02 = MINW0 ? MINW0 : MINW2;
   switch (a.costfct * 2 + (a.nop == 2 ? 1 : 0)) {
-    case 0: k_patchw<1, P, NOC, MINW1, 0><<<grid, 256, lds, s>>>(a); return;
-    case 1: k_patchw<2, P, NOC, MINW2, 0><<<grid, 256, lds, s>>>(a); return;
+    case 0: k_patchw<1, P, NOC, M01, 0><<<grid, 256, lds, s>>>(a); return;
+    case 1: k_patchw<2, P, NOC, M02, 0><<<grid, 256, lds, s>>>(a); return;
     case 2: k_patchw<1, P, NOC, MINW1, 1><<<grid, 256, lds, s>>>(a); return;
     case 3: k_patchw<2, P, NOC, MINW2, 1><<<grid, 256, lds, s>>>(a); return;
     case 4: k_patchw<1, P, NOC, MINW1, 2><<<grid, 256, lds, s>>>(a); return;
@@ -3201,7 +3208,7 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
       case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
       case 8 * 4 + 3: patchw<8, 3, 2, 2>(a, s); return;
-      case 12 * 4 + 3: patchw<12, 3, 2, 2>(a, s); return;
+      case 12 * 4 + 3: patchw<12, 3, 2, 2, 1>(a, s); return;  // L2 cost: samples kept, one wave per SIMD
     }
   }
   if (!a.wave_per_patch) {

@@ -53,6 +53,7 @@ CASES = [
     (160, 120, 1, 1, 2, {"patnorm": 0, "tv_innerit": 2, "tv_solverit": 4, "tv_sor": 1.3}),
     (240, 120, 1, 2, 4, {"max_iter": 16, "min_iter": 16}),    # depth from stereo, op4
     (240, 120, 3, 2, 2, {}),                                  # RGB depth
+    (240, 120, 3, 2, 4, {"max_iter": 16, "min_iter": 16}),    # RGB depth, p = 12 (samples kept, L2 cost)
     (160, 120, 1, 1, 2, {"usefbcon": 1}),                     # forward-backward merging (patchgrid.cpp:277-375)
     (200, 150, 1, 1, 1, {"usefbcon": 1}),                     # ... without TV refinement
     (192, 128, 3, 1, 3, {"usefbcon": 1, "costfct": 1}),       # ... RGB (weight-pointer quirk, bounds [1, w-1))
