@@ -16,6 +16,6 @@ step prof_default 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_default -o r
 step prof_serial 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_serial -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-latency --no-kernel-timing --streams 1 --chunk 1024
 BENCH_BATCH=2048 bash tools/pmc_session.sh ${1:-round}/pmc_B || exit $?
 bash tools/bench_configs.sh ${1:-round}/configs A C C2 D E || exit $?
-bash tools/pmc_config.sh ${1:-round}/pmc_C C 64 || exit $?
-bash tools/pmc_config.sh ${1:-round}/pmc_E E 256 || exit $?
+bash tools/pmc_config.sh ${1:-round}/pmc_C C 512 || exit $?
+bash tools/pmc_config.sh ${1:-round}/pmc_E E 512 || exit $?
 echo "== session done"
