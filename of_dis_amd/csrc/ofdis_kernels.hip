@@ -1451,6 +1451,11 @@ __device__ __forceinline__ long skw(int x, int y, int h, int w, int wrap) {
 // skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
 // image_warp (opticalflow_aux.c:31-75) + the t / It inputs of get_derivatives (:77-132) for pixel (x, y):
 // v = {mask, wx, wy, t[0..noc), dt[0..noc)}.
+// image_warp's mask (opticalflow_aux.c:47): 1 where the warped position (x + wx, y + wy) lies inside the level.
+__device__ __forceinline__ float warp_mask(int x, int y, float wx, float wy, int w, int h) {
+  const float xx = (float)x + wx, yy = (float)y + wy;
+  return (xx >= 0 && xx <= (float)(w - 1) && yy >= 0 && yy <= (float)(h - 1)) ? 1.0f : 0.0f;
+}
 __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, int f, float *v) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
@@ -1459,7 +1464,7 @@ __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, in
   const float xx = (float)x + wx, yy = (float)y + wy;
   const int xi = (int)floorf(xx), yi = (int)floorf(yy);
   const float dx = xx - (float)xi, dy = yy - (float)yi;
-  v[0] = (xx >= 0 && xx <= (float)(a.w - 1) && yy >= 0 && yy <= (float)(a.h - 1)) ? 1.0f : 0.0f;
+  v[0] = warp_mask(x, y, wx, wy, a.w, a.h);
   v[1] = wx;
   v[2] = wy;
   const int x1 = clampi(xi, 0, a.w - 1), x2 = clampi(xi + 1, 0, a.w - 1);
@@ -1476,10 +1481,11 @@ __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, in
   }
 #undef SB
 }
-// The values of pixel (x, y) into the skewed planes (du = dv = 0: the increment starts at zero).
+// The values of pixel (x, y) into the skewed planes (du = dv = 0: the increment starts at zero).  The mask
+// is not stored: it is a function of (x, y, wx, wy), which the system kernels recompute (warp_mask) from the
+// skewed flow copies they read anyway -- 4 bytes per pixel and inner iteration less.
 __device__ __forceinline__ void tv_prep_store(const TvArgs &a, int x, int y, int f, const float *v) {
   const long sk = skw(x, y, a.h, a.w, a.wrap), fk = (long)f * a.sp + sk;
-  a.mask[fk] = v[0];
   a.wxs[fk] = v[1];
   a.du[fk] = 0.0f;
   if (a.nop == 2) {
@@ -1949,7 +1955,8 @@ __device__ __forceinline__ void tv_system_px(const TvArgs &a, long fr, int kk) {
     X5[k] = ldu(a.wxs, i5[k]);
     Y5[k] = NOP == 2 ? ldu(a.wys, i5[k]) : 0.0f;
   }
-  const float m = ldu(a.mask, ui), u = ldu(a.du, ui), v = NOP == 2 ? ldu(a.dv, ui) : 0.0f;
+  const float u = ldu(a.du, ui), v = NOP == 2 ? ldu(a.dv, ui) : 0.0f;
+  const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
   const unsigned q = (unsigned)(fr * NOC * a.sp + kk);
   float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
 #pragma unroll
@@ -2073,7 +2080,109 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
     }
     const float4 qc = st[cs];
     const long idx = f0 + (long)rr * h + y;
-    const float m = a.mask[idx];
+    const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
+    const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)rr * h + y);
+    float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
+#pragma unroll
+    for (int ch = 0; ch < NOC; ++ch) {
+      const unsigned o = qd + (unsigned)(ch * a.sp);
+      lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
+      lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
+    }
+    float4 c0, c1;
+    sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, qc.z, NOP == 2 ? qc.w : 0.0f, lIx, lIy, lIz, lIxx, lIxy, lIyy,
+                          lIxz, lIyz, c0, c1);
+    if (NOP == 2) {
+      float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
+      C[0] = c0;
+      C[1] = c1;
+    } else {
+      reinterpret_cast<float4 *>(a.coef)[idx] = c0;
+    }
+  }
+}
+
+// The same launch on 2-D tiles of the skewed plane for tall levels (h > 256), where whole-row blocks would
+// stage RB + 4 rows for RB < 4 computed ones.  A workgroup takes rows r0 .. r0+RB-1 and columns
+// y0 .. y0+CB-1; its 4-neighbours lie at (r -+ 1, y) and (r -+ 1, y -+ 1), so it stages (wx, wy, du, dv) of
+// rows r0-2 .. r0+RB+1 x columns y0-2 .. y0+CB+1 ((RB+4)(CB+4) for RB CB: 1.33x at 16 x 64) and s of rows
+// r0-1 .. r0+RB x columns y0-1 .. y0+CB in LDS.  Against the two launches (smoothness, then system) it
+// skips the s round trip and the second read of (wx, du): same functions, same bits.  blockIdx.x is the
+// frame, so the tiles of a frame land on one XCD.
+constexpr int kS2R = 16, kS2C = 64, kS2CS = kS2C + 4, kS2SS = kS2C + 2;
+template <int NOP, int NOC>
+__global__ __launch_bounds__(256) void k_tv_smsys2d(TvArgs a) {
+  __shared__ float4 st[(kS2R + 4) * kS2CS];  // (wx, wy, du, dv)
+  __shared__ float sl[(kS2R + 2) * kS2SS];   // s
+  const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
+  const int f = blockIdx.x, r0 = blockIdx.y * kS2R, y0 = blockIdx.z * kS2C;
+  const long f0 = (long)f * a.sp;
+  const bool first = a.first_iter != 0;
+  auto prow = [&](int r) { return a.wrap ? (r < 0 ? r + w : (r >= w ? r - w : r)) : (r < 0 || r >= rows ? -1 : r); };
+  auto pix = [&](int r, int y, int &x) {  // plane (row, column) -> pixel x; false outside the level
+    if (r < 0 || y < 0 || y >= h) return false;
+    x = r - y;
+    if (a.wrap) {
+      if (x < 0) x += w;
+      return true;
+    }
+    return x >= 0 && x < w;
+  };
+  // ---- phase 0: stage
+  for (int i = threadIdx.x; i < (kS2R + 4) * kS2CS; i += blockDim.x) {
+    const int ri = i / kS2CS, y = y0 - 2 + (i - ri * kS2CS);
+    const int r = prow(r0 - 2 + ri);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= 0 && y >= 0 && y < h) {
+      const long o = f0 + (long)r * h + y;
+      v.x = a.wxs[o];
+      v.z = a.du[o];
+      if (NOP == 2) {
+        v.y = a.wys[o];
+        v.w = a.dv[o];
+      }
+    }
+    st[i] = v;
+  }
+  __syncthreads();
+  // ---- phase 1: s of rows r0 - 1 .. r0 + RB, columns y0 - 1 .. y0 + CB
+  for (int i = threadIdx.x; i < (kS2R + 2) * kS2SS; i += blockDim.x) {
+    const int ri = i / kS2SS, yl = i - ri * kS2SS, y = y0 - 1 + yl;  // s (ri, yl) <-> staged (ri + 1, yl + 1)
+    int x;
+    float sv = 0.0f;
+    if (pix(prow(r0 - 1 + ri), y, x)) {
+      const int c = (ri + 1) * kS2CS + yl + 1;
+      const int cl = x > 0 ? c - kS2CS : c, cr = x < w - 1 ? c + kS2CS : c;
+      const int cu = y > 0 ? c - kS2CS - 1 : c, cd = y < h - 1 ? c + kS2CS + 1 : c;
+      const float4 q0 = st[c], q1 = st[cl], q2 = st[cr], q3 = st[cu], q4 = st[cd];
+      const float wx5[5] = {q0.x, q1.x, q2.x, q3.x, q4.x}, du5[5] = {q0.z, q1.z, q2.z, q3.z, q4.z};
+      const float wy5[5] = {q0.y, q1.y, q2.y, q3.y, q4.y}, dv5[5] = {q0.w, q1.w, q2.w, q3.w, q4.w};
+      sv = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
+    }
+    sl[i] = sv;
+  }
+  __syncthreads();
+  // ---- phase 2: the system of rows r0 .. r0 + RB - 1, columns y0 .. y0 + CB - 1
+  for (int i = threadIdx.x; i < kS2R * kS2C; i += blockDim.x) {
+    const int ri = i / kS2C, yl = i - ri * kS2C, y = y0 + yl;
+    const int rr = r0 + ri;
+    int x;
+    if (rr >= rows || !pix(rr, y, x)) continue;
+    const int c = (ri + 1) * kS2SS + yl + 1, cs = (ri + 2) * kS2CS + yl + 2;  // s index, staged index
+    const int yu = y > 0 ? -1 : 0, yd = y < h - 1 ? 1 : 0;  // clamped columns; absent neighbours are discarded
+    const int s5[5] = {c, c - kS2SS, c + kS2SS, c - kS2SS + yu, c + kS2SS + yd};
+    const int t5[5] = {cs, cs - kS2CS, cs + kS2CS, cs - kS2CS + yu, cs + kS2CS + yd};
+    float S5[5], X5[5], Y5[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      S5[k] = sl[s5[k]];
+      const float4 q = st[t5[k]];
+      X5[k] = q.x;
+      Y5[k] = NOP == 2 ? q.y : 0.0f;
+    }
+    const float4 qc = st[cs];
+    const long idx = f0 + (long)rr * h + y;
+    const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
     const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)rr * h + y);
     float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
 #pragma unroll
@@ -3253,8 +3362,22 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
 }
 // The fused form stages RB + 4 rows for RB computed ones: below RB = 4 (h > 256) the halo re-reads cost
 // more than the smoothness round trip saves (config E, h = 544 / 272: 518 vs 299 us per launch).
-bool tv_smsys_ok(const TvArgs &a) { return a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024; }
+// Tall levels take the 2-D tiled form (k_tv_smsys2d) unless a.smsys2d = 0 (A/B: two launches there).
+bool tv_smsys_ok(const TvArgs &a) {
+  return a.smsys && ((smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) || a.smsys2d);
+}
 void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
+  if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) {
+    const dim3 g2(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), kS2R), ceil_div(a.h, kS2C));
+    if (a.nop == 2) {
+      if (a.noc == 1) k_tv_smsys2d<2, 1><<<g2, 256, 0, s>>>(a);
+      else k_tv_smsys2d<2, 3><<<g2, 256, 0, s>>>(a);
+    } else {
+      if (a.noc == 1) k_tv_smsys2d<1, 1><<<g2, 256, 0, s>>>(a);
+      else k_tv_smsys2d<1, 3><<<g2, 256, 0, s>>>(a);
+    }
+    return;
+  }
   const dim3 grid(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), smsys_rb(a.h)));
   const size_t lds = smsys_lds(a.h);
   if (a.nop == 2) {

@@ -80,6 +80,13 @@ struct ofdis_context {
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
+  // the fused launch on 2-D tiles for tall levels: 1 on, 0 off (two launches there), 2 auto = on for calls of
+  // fewer than 512 pairs (one stream).  Measured at config E: alone on the GPU it cuts the system time 10 %
+  // (580 vs 603 ms per 512 pairs on one stream), but beside a second chain (two streams) the LDS-holding
+  // fused kernel overlaps worse with the other lane's patch kernel than the two plain launches (561 vs
+  // 544-551 ms per step) -- profiles/r02/ab/ab_smsys2d.
+  int opt_smsys2d = 2;
+  int call_frames = 1;         // pairs of the current call (auto options)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
@@ -474,6 +481,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_cring = c->opt_sor_cring;
       tv.smsys = c->opt_smsys;
+      tv.smsys2d = c->opt_smsys2d == 2 ? c->call_frames < 512 : c->opt_smsys2d;
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
@@ -794,6 +802,7 @@ struct CallPlan {
 int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int height, bool init, bool capturing,
             CallPlan &cp) {
   cp.n = n;
+  c->call_frames = n;
   cp.width = width;
   cp.height = height;
   cp.init = init;
@@ -998,6 +1007,7 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
 int run_verbose(ofdis_context *c, const uint8_t *img_a, const uint8_t *img_b, const float *init, int width,
                 int height, const ofdis_params *p, float *flow_out) {
   hipStream_t s = c->stream;
+  c->call_frames = 1;
   auto t0 = std::chrono::steady_clock::now();
   Plan P = batch_plan(p, 1, width, height, init != nullptr);
   int rc = ensure_ws(c, P.total);
@@ -1172,7 +1182,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
-      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
+      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
@@ -1303,6 +1313,7 @@ int ofdis_oflow_compute(const float *const *im_ao, const float *const *im_ao_dx,
     if (nb) HIP_OK(hipMemcpyAsync(dinit, initflow, nb, hipMemcpyHostToDevice, s));
   }
   std::vector<StageTimes> times;
+  c->call_frames = 1;
   rc = run_levels(c, c->ws, P, p, s, dinit, p->verbosity > 1 ? &times : nullptr);
   if (rc == OFDIS_OK) {
     const LevelGeom &g = P.lv[0];
