@@ -104,6 +104,7 @@ struct TvArgs {
   int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
   int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
   int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3)
+  int sor_rows2;               // lean SOR with two rows per lane for levels of 321..640 rows (else the pipeline)
   int smsys;                   // smoothness + system in one launch (k_tv_smsys)
   int smsys2d;                 // ... and on 2-D tiles for tall levels (k_tv_smsys2d; 0: two launches there, A/B)
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)

@@ -2738,7 +2738,11 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // coefficients once and passes them to the later sweeps through LDS (slot = diagonal mod 6: a diagonal
 // lives from sweep 0's step to sweep S-1's, 2 (S - 1) + 1 <= 6 steps for S <= 3), which also supplies the
 // upper pixel's sv; CRN = 0: every sweep loads its own coefficients and keeps an sv ring.
-template <int S, int MODE, int SI, int NB, int CRN>
+// R: rows per lane.  Wave (g, s) owns rows 64 R g .. 64 R g + 64 R - 1; lane i runs rows y + 64 r (r < R), one
+// pixel each per step -- the rows of one step are independent (their top neighbours ran at step t-1 and are in
+// the ring), so R = 2 runs levels of up to 640 rows with S <= 3 in 16 waves (E's 544-row level) where R = 1
+// would need 27.  Every per-row ring / coefficient-ring offset is a compile-time multiple of 64 entries.
+template <int S, int MODE, int SI, int NB, int CRN, int R = 1>
 struct SorLane {
   static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
   static_assert(CRN == 0 || S <= 3, "coefficient ring depth 6 needs S <= 3");
@@ -2746,8 +2750,8 @@ struct SorLane {
   static constexpr int U = NB % 3 == 0 ? (NB < 6 ? 6 : NB) : 3 * NB;  // multiple of 3 (ring) and NB
   static constexpr int CW = MODE == 0 ? 2 : 1;                         // float4s of coefficients per pixel
   struct Ld {
-    float4 c0, c1;
-    f2v o, b;   // sweep 0: old (u, v) of the pixel and of the one below (the right one: next step's o)
+    float4 c0[R], c1[R];
+    f2v o[R], b[R];  // sweep 0: old (u, v) of the pixel and of the one below (the right one: next step's o)
   };
   Ld L0, L1, L2, L3, L4, L5;  // buffers as named members (no array: keeps them in registers)
   template <int I>
@@ -2760,8 +2764,8 @@ struct SorLane {
     else if constexpr (I == 4) return L4;
     else return L5;
   }
-  f2v pp;      // own (u, v) of step t-1 (left neighbour)
-  float phr;   // own sh of step t-1 (left neighbour's sh)
+  f2v pp[R];      // own (u, v) of step t-1 (left neighbour)
+  float phr[R];   // own sh of step t-1 (left neighbour's sh)
   const float4 *C;
   const float *du_r, *dv_r;
   float *du, *dv;
@@ -2770,28 +2774,32 @@ struct SorLane {
   float *sv_s;        // [NR][3] this sweep's sv (row y's sv at entry y + 1) (CRN = 0)
   float4 *cr;         // [6][CW][CRN] coefficient ring, lane base = entry y + 1 (CRN > 0)
   int w, h, y, s, lim, rmax, hplane;
-  bool border, notop;
+  bool border[R], notop[R];
   float omega;
 
   __device__ __forceinline__ void load(int t, Ld &B) {
     const int d = t - 2 * s;
     const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
-    if (FIRST || CRN == 0) {
-      const float4 *cp = C + (size_t)r0 * CW;
-      B.c0 = cp[(unsigned)y * CW];
-      if (MODE == 0) B.c1 = cp[(unsigned)y * CW + 1];
-    }
-    if (FIRST) {
-      const unsigned r1 = (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane;
-      const float *u0 = du_r + r0, *u1 = du_r + r1;
-      float ov = 0.0f, bv = 0.0f;
-      if (MODE == 0) {
-        const float *v0 = dv_r + r0, *v1 = dv_r + r1;
-        ov = v0[(unsigned)y];
-        bv = v1[(unsigned)y + 1];
+    const unsigned r1 = FIRST ? (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane : 0u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned yr = (unsigned)(y + 64 * r);
+      if (FIRST || CRN == 0) {
+        const float4 *cp = C + (size_t)r0 * CW;
+        B.c0[r] = cp[yr * CW];
+        if (MODE == 0) B.c1[r] = cp[yr * CW + 1];
       }
-      B.o = f2v{u0[(unsigned)y], ov};
-      B.b = f2v{u1[(unsigned)y + 1], bv};
+      if (FIRST) {
+        const float *u0 = du_r + r0, *u1 = du_r + r1;
+        float ov = 0.0f, bv = 0.0f;
+        if (MODE == 0) {
+          const float *v0 = dv_r + r0, *v1 = dv_r + r1;
+          ov = v0[yr];
+          bv = v1[yr + 1];
+        }
+        B.o[r] = f2v{u0[yr], ov};
+        B.b[r] = f2v{u1[yr + 1], bv};
+      }
     }
   }
 
@@ -2802,75 +2810,80 @@ struct SorLane {
     const Ld &Bn = buf<(Q + 1) % NB>();
     load(t + PD, buf<(Q + PD) % NB>());  // beyond the last step too: sor_row keeps every address in the plane
     const int d = t - 2 * s;
-    const int xp = d - y;
-    const bool hasl = xp > 0, hasr = xp < w - 1;
-    f2v o, r, bt;
-    if (FIRST) {
-      o = B.o; r = Bn.o; bt = B.b;
-    } else {
-      o = ring_p[m2]; r = ring_p[m1]; bt = ring_p[3 + m1];
-    }
-    const f2v tp = ring_s[m1 - 3];  // row y - 1 at step t-1
-    // coefficients of this pixel and sv of the one above (entry 0, row -1, stays zero)
-    constexpr int cs = ((Q - 2 * SI) % 6 + 6) % 6, ct = (cs + 5) % 6;  // slots of diagonals d, d - 1
-    float4 c0, c1;
-    float tsv;
-    if (CRN > 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      constexpr int RO = 64 * 3;  // ring entries of the row 64 below, in f2v / float
+      const int yr = y + 64 * r;
+      const int xp = d - yr;
+      const bool hasl = xp > 0, hasr = xp < w - 1;
+      f2v o, rgt, bt;
       if (FIRST) {
-        c0 = B.c0;
-        c1 = MODE == 0 ? B.c1 : B.c0;
-        cr[cs * CW * CRN] = c0;
-        if (MODE == 0) cr[(cs * CW + 1) * CRN] = c1;
+        o = B.o[r]; rgt = Bn.o[r]; bt = B.b[r];
       } else {
-        c0 = cr[cs * CW * CRN];
-        c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN] : c0;
+        o = ring_p[r * RO + m2]; rgt = ring_p[r * RO + m1]; bt = ring_p[r * RO + 3 + m1];
       }
-      tsv = cr[(ct * CW + CW - 1) * CRN - 1].w;
-    } else {
-      c0 = B.c0;
-      c1 = MODE == 0 ? B.c1 : B.c0;
-      tsv = sv_s[m1 - 3];
-    }
-    f2v nw;
-    float vv;
-    if (MODE == 0) {
-      const float hr = c1.z;
-      vv = c1.w;
-      const f2v bb = f2v{c1.x, c1.y};
-      const f2v rr = hasr ? r : f2v{0.0f, 0.0f};
-      const f2v X = hr * rr, Y = tsv * tp, Z = vv * bt;
-      // solver.c's three border expression trees (see sor_rhs), lane-constant operand selects
-      const f2v l = X + (border ? bb : Y);
-      const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Y) : Z);
-      const f2v sr = l + rg;
-      const f2v Bv = hasl ? phr * pp + sr : sr;
-      const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;  // (i11,i12), (i12,i22)
-      nw = o + omega * ((m_1 + m_2) - o);
-      phr = hr;
-    } else {
-      const float a11 = c0.x, b1 = c0.y, hr = c0.z;
-      vv = c0.w;
-      const bool has_top = !notop, has_bot = !(border && has_top);
-      const float tu = tp.x, ur = hasr ? r.x : 0.0f, hl = phr;
-      float su = 0.0f, sd = 0.0f;
-      su = has_top ? su - tsv * tu : su;   sd = has_top ? sd + tsv : sd;
-      su = hasl ? su - hl * pp.x : su;     sd = hasl ? sd + hl : sd;
-      su = has_bot ? su - vv * bt.x : su;  sd = has_bot ? sd + vv : sd;
-      su = hasr ? su - hr * ur : su;       sd = hasr ? sd + hr : sd;
-      const float A = a11 + sd, Bq = b1 - su;
-      nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
-      phr = hr;
-    }
-    ring_s[m0] = nw;
-    if (CRN == 0) sv_s[m0] = vv;
-    if (LAST) {
-      if ((unsigned)xp < (unsigned)w && y < h) {
-        const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
-        du[r0 + (unsigned)y] = nw.x;
-        if (MODE == 0) dv[r0 + (unsigned)y] = nw.y;
+      const f2v tp = ring_s[r * RO + m1 - 3];  // row y - 1 at step t-1
+      // coefficients of this pixel and sv of the one above (entry 0, row -1, stays zero)
+      constexpr int cs = ((Q - 2 * SI) % 6 + 6) % 6, ct = (cs + 5) % 6;  // slots of diagonals d, d - 1
+      float4 c0, c1;
+      float tsv;
+      if (CRN > 0) {
+        if (FIRST) {
+          c0 = B.c0[r];
+          c1 = MODE == 0 ? B.c1[r] : B.c0[r];
+          cr[cs * CW * CRN + 64 * r] = c0;
+          if (MODE == 0) cr[(cs * CW + 1) * CRN + 64 * r] = c1;
+        } else {
+          c0 = cr[cs * CW * CRN + 64 * r];
+          c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN + 64 * r] : c0;
+        }
+        tsv = cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w;
+      } else {
+        c0 = B.c0[r];
+        c1 = MODE == 0 ? B.c1[r] : B.c0[r];
+        tsv = sv_s[r * RO + m1 - 3];
       }
+      f2v nw;
+      float vv;
+      if (MODE == 0) {
+        const float hr = c1.z;
+        vv = c1.w;
+        const f2v bb = f2v{c1.x, c1.y};
+        const f2v rr = hasr ? rgt : f2v{0.0f, 0.0f};
+        const f2v X = hr * rr, Y = tsv * tp, Z = vv * bt;
+        // solver.c's three border expression trees (see sor_rhs), lane-constant operand selects
+        const f2v l = X + (border[r] ? bb : Y);
+        const f2v rg = (border[r] ? f2v{-0.0f, -0.0f} : bb) + (border[r] ? (notop[r] ? Z : Y) : Z);
+        const f2v sr = l + rg;
+        const f2v Bv = hasl ? phr[r] * pp[r] + sr : sr;
+        const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;  // (i11,i12), (i12,i22)
+        nw = o + omega * ((m_1 + m_2) - o);
+        phr[r] = hr;
+      } else {
+        const float a11 = c0.x, b1 = c0.y, hr = c0.z;
+        vv = c0.w;
+        const bool has_top = !notop[r], has_bot = !(border[r] && has_top);
+        const float tu = tp.x, ur = hasr ? rgt.x : 0.0f, hl = phr[r];
+        float su = 0.0f, sd = 0.0f;
+        su = has_top ? su - tsv * tu : su;   sd = has_top ? sd + tsv : sd;
+        su = hasl ? su - hl * pp[r].x : su;  sd = hasl ? sd + hl : sd;
+        su = has_bot ? su - vv * bt.x : su;  sd = has_bot ? sd + vv : sd;
+        su = hasr ? su - hr * ur : su;       sd = hasr ? sd + hr : sd;
+        const float A = a11 + sd, Bq = b1 - su;
+        nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
+        phr[r] = hr;
+      }
+      ring_s[r * RO + m0] = nw;
+      if (CRN == 0) sv_s[r * RO + m0] = vv;
+      if (LAST) {
+        if ((unsigned)xp < (unsigned)w && yr < h) {
+          const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
+          du[r0 + (unsigned)yr] = nw.x;
+          if (MODE == 0) dv[r0 + (unsigned)yr] = nw.y;
+        }
+      }
+      pp[r] = nw;
     }
-    pp = nw;
     __syncthreads();
   }
 
@@ -2888,8 +2901,11 @@ struct SorLane {
   // Steps [0, T), T a multiple of U.  The wave's rows y0..ymax are inside the frame for diagonals
   // d = t - 2s in [y0, ymax + w - 1]; blocks wholly outside that range only join the barriers.
   __device__ __forceinline__ void run(int T, int y0, int ymax) {
-    pp = f2v{0.0f, 0.0f};
-    phr = 0.0f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      pp[r] = f2v{0.0f, 0.0f};
+      phr[r] = 0.0f;
+    }
     const int ta = max(0, (y0 + 2 * SI) / U * U);
     const int tb = min(T, (ymax + w - 1 + 2 * SI) / U * U + U);
     for (int t = 0; t < ta; ++t) __syncthreads();
@@ -2899,24 +2915,28 @@ struct SorLane {
   }
 };
 
+constexpr size_t kSorLds = 160 * 1024;  // LDS per workgroup (gfx950: 160 KB per CU)
 // Entries per slot of the coefficient ring: the most rows a workgroup of MAXT threads holds, + 2 halos
 // (a compile-time constant, so every ring offset is an immediate); 0 = no coefficient ring (S > 3).
-__host__ __device__ constexpr int sor_crn(int S, int MAXT) { return S <= 3 ? 64 * (MAXT / (64 * S)) + 2 : 0; }
+__host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
+  return S <= 3 ? 64 * R * (MAXT / (64 * S)) + 2 : 0;
+}
 
-// LDS of the lean SOR: S (u, v) rings of NR = 64 G + 2 entries x 3 slots of float2, then S sv rings
+// LDS of the lean SOR: S (u, v) rings of NR = 64 R G + 2 entries x 3 slots of float2, then S sv rings
 // (CRN = 0) or the [6][CW][CRN] coefficient ring (16-byte aligned).
-__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw) {
-  const size_t uv = sizeof(float) * 2 * 3 * (size_t)S * (((h + 63) / 64) * 64 + 2);
-  if (crn == 0) return uv + sizeof(float) * 3 * (size_t)S * (((h + 63) / 64) * 64 + 2);
+__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1) {
+  const size_t nr = (size_t)((h + 64 * R - 1) / (64 * R)) * 64 * R + 2;
+  const size_t uv = sizeof(float) * 2 * 3 * (size_t)S * nr;
+  if (crn == 0) return uv + sizeof(float) * 3 * (size_t)S * nr;
   return (uv + 15) / 16 * 16 + sizeof(float4) * 6 * cw * (size_t)crn;
 }
 
-// One frame's SOR call, lean form (R = 1): 64 * G * S threads.
-template <int S, int MODE, int NB, int CRN>
+// One frame's SOR call, lean form: 64 * G * S threads, R rows per lane.
+template <int S, int MODE, int NB, int CRN, int R>
 __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
   constexpr int CW = MODE == 0 ? 2 : 1;
-  const int G = (a.h + 63) / 64;
-  const int NR = G * 64 + 2;
+  const int G = (a.h + 64 * R - 1) / (64 * R);
+  const int NR = G * 64 * R + 2;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = wid / S, s = wid - g * S;
   float *svr = reinterpret_cast<float *>(ring + S * 3 * NR);
@@ -2929,9 +2949,9 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     for (int i = threadIdx.x; i < 6 * CW * CRN; i += blockDim.x) crr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   const long fo = (long)frame * a.sp;
-  constexpr int U = SorLane<S, MODE, 0, NB, CRN>::U;
+  constexpr int U = SorLane<S, MODE, 0, NB, CRN, R>::U;
   const int T = ((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1 + U - 1) / U * U;
-  const int y0 = g * 64, ymax = min(y0 + 63, a.h - 1);
+  const int y0 = g * 64 * R, ymax = min(y0 + 64 * R - 1, a.h - 1);
   auto setup = [&](auto &st) {
     st.C = reinterpret_cast<const float4 *>(a.coef) + fo * (MODE == 0 ? 2 : 1);
     st.du_r = a.du + fo;
@@ -2947,30 +2967,34 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.lim = a.wrap ? a.w : 1 << 30;
     st.rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
     st.hplane = a.h;
-    st.notop = y == 0;
-    st.border = y == 0 || y >= a.h - 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int yr = y + 64 * r;
+      st.notop[r] = yr == 0;
+      st.border[r] = yr == 0 || yr >= a.h - 1;
+    }
     st.omega = a.omega;
     st.run(T, y0, ymax);
   };
   if (s == 0) {
-    SorLane<S, MODE, 0, NB, CRN> st;
+    SorLane<S, MODE, 0, NB, CRN, R> st;
     setup(st);
   } else if (s == 1) {
-    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN> st;
+    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R> st;
     setup(st);
   } else if (s == 2) {
-    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN> st;
+    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R> st;
     setup(st);
   } else {
-    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN> st;
+    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R> st;
     setup(st);
   }
 }
 
-template <int S, int MODE, int NB, int MAXT, bool CRING>
+template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
-  sor_lanes_frame<S, MODE, NB, CRING ? sor_crn(S, MAXT) : 0>(a, blockIdx.x, ring_uv);
+  sor_lanes_frame<S, MODE, NB, CRING ? sor_crn(S, MAXT, R) : 0, R>(a, blockIdx.x, ring_uv);
 }
 
 template <int TH>
@@ -3426,29 +3450,33 @@ static void sor_pipe(const TvArgs &a, hipStream_t s) {
       k_tv_sor_pipe<S, 2, 1024><<<a.n, threads, 0, s>>>(a);
   }
 }
-// Sweep-per-wave SOR (k_tv_sor_lanes): 64 * ceil(h / 64) * S threads, one workgroup per frame.  With S <= 3
-// sweep 0 hands the coefficients to the later sweeps through an LDS ring (option sor_cring, default on).
-template <int S, int MAXT>
+// Sweep-per-wave SOR (k_tv_sor_lanes): 64 * ceil(h / (64 R)) * S threads, one workgroup per frame.  With S <= 3
+// sweep 0 hands the coefficients to the later sweeps through an LDS ring (option sor_cring, default on) while
+// it fits the LDS.
+template <int S, int MAXT, int R>
 static void sor_lanes(const TvArgs &a, hipStream_t s) {
-  const int G = (a.h + 63) / 64;
-  constexpr int crn = sor_crn(S, MAXT);
-  const bool cring = crn > 0 && a.sor_cring;
-  const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, a.nop == 2 ? 2 : 1);
+  const int G = (a.h + 64 * R - 1) / (64 * R);
+  constexpr int crn = sor_crn(S, MAXT, R);
+  const int cw = a.nop == 2 ? 2 : 1;
+  const bool cring = crn > 0 && a.sor_cring && sor_lanes_lds(S, a.h, crn, cw, R) <= kSorLds;
+  const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, cw, R);
   const int th = 64 * G * S;
   if (cring) {
-    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
-    else k_tv_sor_lanes<S, 2, 3, MAXT, true><<<a.n, th, lds, s>>>(a);
+    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true, R><<<a.n, th, lds, s>>>(a);
+    else k_tv_sor_lanes<S, 2, 3, MAXT, true, R><<<a.n, th, lds, s>>>(a);
   } else {
-    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
-    else k_tv_sor_lanes<S, 2, 3, MAXT, false><<<a.n, th, lds, s>>>(a);
+    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, false, R><<<a.n, th, lds, s>>>(a);
+    else k_tv_sor_lanes<S, 2, 3, MAXT, false, R><<<a.n, th, lds, s>>>(a);
   }
 }
 template <int S>
 static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
   if (64 * S * ((a.h + 63) / 64) <= 512)
-    sor_lanes<S, 512>(a, s);
+    sor_lanes<S, 512, 1>(a, s);
+  else if (64 * S * ((a.h + 63) / 64) <= 1024)
+    sor_lanes<S, 1024, 1>(a, s);
   else
-    sor_lanes<S, 1024>(a, s);
+    sor_lanes<S, 1024, 2>(a, s);
 }
 // Exact-order SOR dispatch: the sweep-per-wave form while its S * ceil(h / 64) waves fit one workgroup,
 // the register pipeline (one wave per row group runs all sweeps) for taller levels, the generic
@@ -3471,8 +3499,9 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
     }
     return;
   }
-  const int G = (a.h + 63) / 64;
-  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && G * a.solverit <= 16) {
+  const int G = (a.h + 63) / 64, G2 = (a.h + 127) / 128;  // row groups at one / two rows per lane
+  const bool lanes_fit = G * a.solverit <= 16 || (a.solverit <= 3 && G2 * a.solverit <= 16 && a.sor_rows2);
+  if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && lanes_fit) {
     switch (a.solverit) {
       case 2: sor_lanes_s<2>(a, s); return;
       case 3: sor_lanes_s<3>(a, s); return;

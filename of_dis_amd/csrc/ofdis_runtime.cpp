@@ -88,6 +88,7 @@ struct ofdis_context {
   int opt_smsys2d = 2;
   int call_frames = 1;         // pairs of the current call (auto options)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
+  int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
@@ -480,6 +481,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_generic = c->opt_sor_generic;
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_cring = c->opt_sor_cring;
+      tv.sor_rows2 = c->opt_sor_rows2;
       tv.smsys = c->opt_smsys;
       tv.smsys2d = c->opt_smsys2d == 2 ? c->call_frames < 512 : c->opt_smsys2d;
       tv.sor_redblack = c->opt_sor_mode == 1;
@@ -1182,7 +1184,8 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
-      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
+      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
+      {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
