@@ -63,6 +63,8 @@ struct PatchArgs {
   int n, nop, noc, p, novals, steps;
   int costfct, patnorm, max_iter, min_iter;
   float dp_thresh_sq, dr_thresh, res_thresh, outlierthresh;
+  float outlier_sq;                           // largest s with sqrt_rn(s) <= outlierthresh: the outlier test
+                                              // sqrt(ex^2 + ey^2) > thresh (patch.cpp:197) without the sqrt
   int camlr;
   int wave_per_patch;                         // 1: force the one-wave-per-patch kernel (A/B testing)
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one

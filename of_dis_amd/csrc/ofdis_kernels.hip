@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
     pt0 = ptr0 + p0;
     if (NOP == 2) pt1 = ptr1 + p1;
     const float ex = st0 - pt0, ey = st1 - pt1;
-    if (sqrt_nonneg(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+    if (ex * ex + ey * ey > a.outlier_sq || oob(pt0, pt1)) {
       p0 = pin0;
       p1 = pin1;
       pt0 = ptr0 + p0;
@@ -750,7 +750,7 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
     pt0 = ptr0 + p0;
     if (NOP == 2) pt1 = ptr1 + p1;
     const float ex = st0 - pt0, ey = st1 - pt1;
-    if (sqrt_nonneg(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+    if (ex * ex + ey * ey > a.outlier_sq || oob(pt0, pt1)) {
       p0 = pin0;
       p1 = pin1;
       pt0 = ptr0 + p0;
@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         pt0 = ptr0 + p0;
         if (NOP == 2) pt1 = ptr1 + p1;
         const float ex = st0 - pt0, ey = st1 - pt1;
-        if (sqrt_nonneg(ex * ex + ey * ey) > a.outlierthresh || oob(pt0, pt1)) {
+        if (ex * ex + ey * ey > a.outlier_sq || oob(pt0, pt1)) {
           p0 = pin0;
           p1 = pin1;
           pt0 = ptr0 + p0;

@@ -320,6 +320,17 @@ struct StageTimes {
 
 // The coarse-to-fine loop (oflow.cpp:182-330) over device pyramids already in the workspace.
 // init: optional coarse initial flow (device, interleaved, (w_f/2)*(h_f/2)*nop per frame).
+// The largest float s with sqrtf(s) <= t.  A correctly rounded square root is monotone, so for every float s
+// (NaN and inf included) sqrtf(s) > t <=> s > sqrt_le_bound(t): the patch kernels' outlier test compares the
+// squared distance against it, bit-for-bit the reference's norm() > outlierthresh without a square root.
+static float sqrt_le_bound(float t) {
+  if (!(t >= 0.0f) || std::isinf(t)) return t * t;
+  float s = t * t;
+  while (std::sqrt(std::nextafter(s, INFINITY)) <= t) s = std::nextafter(s, INFINITY);
+  while (s > 0.0f && std::sqrt(s) > t) s = std::nextafter(s, -INFINITY);
+  return s;
+}
+
 int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, hipStream_t s, const float *init,
                std::vector<StageTimes> *times) {
   const int nop = P.nop, noc = P.noc, n = P.n;
@@ -373,6 +384,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.dr_thresh = p->dr_thresh;
     pa.res_thresh = p->res_thresh;
     pa.outlierthresh = (float)p->p_samp_s / 2;
+    pa.outlier_sq = sqrt_le_bound(pa.outlierthresh);
     pa.camlr = 0;
     pa.wave_per_patch = c->opt_wave_per_patch;
     pa.window = c->opt_patch_window;
