@@ -2766,6 +2766,12 @@ struct SorLane {
   }
   f2v pp[R];      // own (u, v) of step t-1 (left neighbour)
   float phr[R];   // own sh of step t-1 (left neighbour's sh)
+  float pvv[R];   // own sv of step t-1 (the lower pixel's upper sv)
+  f2v prv[R];     // previous sweep's (u, v) of this row at step t-2: the right neighbour read at step t-1
+  // DPT: the upper neighbour's (u, v) and sv come from lane y-1's registers (DPP) instead of the LDS rings;
+  // only lane 0 of a row group below the first reads them there (the row above is another wave's)
+  static constexpr bool DPT = R == 1;
+  bool top_lds;   // DPT: this lane reads its upper neighbour from LDS (lane 0, row group > 0)
   const float4 *C;
   const float *du_r, *dv_r;
   float *du, *dv;
@@ -2819,14 +2825,13 @@ struct SorLane {
       f2v o, rgt, bt;
       if (FIRST) {
         o = B.o[r]; rgt = Bn.o[r]; bt = B.b[r];
-      } else {
-        o = ring_p[r * RO + m2]; rgt = ring_p[r * RO + m1]; bt = ring_p[r * RO + 3 + m1];
+      } else {  // own value after the previous sweep (step t-2) = the right neighbour read at step t-1
+        o = prv[r]; rgt = ring_p[r * RO + m1]; bt = ring_p[r * RO + 3 + m1];
+        prv[r] = rgt;
       }
-      const f2v tp = ring_s[r * RO + m1 - 3];  // row y - 1 at step t-1
       // coefficients of this pixel and sv of the one above (entry 0, row -1, stays zero)
       constexpr int cs = ((Q - 2 * SI) % 6 + 6) % 6, ct = (cs + 5) % 6;  // slots of diagonals d, d - 1
       float4 c0, c1;
-      float tsv;
       if (CRN > 0) {
         if (FIRST) {
           c0 = B.c0[r];
@@ -2837,11 +2842,23 @@ struct SorLane {
           c0 = cr[cs * CW * CRN + 64 * r];
           c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN + 64 * r] : c0;
         }
-        tsv = cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w;
       } else {
         c0 = B.c0[r];
         c1 = MODE == 0 ? B.c1[r] : B.c0[r];
-        tsv = sv_s[r * RO + m1 - 3];
+      }
+      // row y - 1 at step t-1: its (u, v) and its sv
+      f2v tp;
+      float tsv;
+      if (DPT) {
+        tp = f2v{dpp_from_prev_lane(pp[r].x), MODE == 0 ? dpp_from_prev_lane(pp[r].y) : 0.0f};
+        tsv = dpp_from_prev_lane(pvv[r]);
+        if (top_lds) {
+          tp = ring_s[r * RO + m1 - 3];
+          tsv = CRN > 0 ? cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w : sv_s[r * RO + m1 - 3];
+        }
+      } else {
+        tp = ring_s[r * RO + m1 - 3];
+        tsv = CRN > 0 ? cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w : sv_s[r * RO + m1 - 3];
       }
       f2v nw;
       float vv;
@@ -2875,6 +2892,7 @@ struct SorLane {
       }
       ring_s[r * RO + m0] = nw;
       if (CRN == 0) sv_s[r * RO + m0] = vv;
+      pvv[r] = vv;
       if (LAST) {
         if ((unsigned)xp < (unsigned)w && yr < h) {
           const unsigned r0 = (unsigned)sor_row2(d, lim, rmax) * (unsigned)hplane;
@@ -2905,10 +2923,16 @@ struct SorLane {
     for (int r = 0; r < R; ++r) {
       pp[r] = f2v{0.0f, 0.0f};
       phr[r] = 0.0f;
+      pvv[r] = 0.0f;
     }
     const int ta = max(0, (y0 + 2 * SI) / U * U);
     const int tb = min(T, (ymax + w - 1 + 2 * SI) / U * U + U);
     for (int t = 0; t < ta; ++t) __syncthreads();
+    // the previous sweep's value at step ta - 2 (written before the barrier of step ta - 1; zero before t = 0)
+    if (!FIRST) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) prv[r] = ta >= 2 ? ring_p[64 * 3 * r + (ta - 2) % 3] : f2v{0.0f, 0.0f};
+    }
     prologue<0>(ta);
     for (int t = ta; t < tb; t += U) block<0>(t);
     for (int t = tb; t < T; ++t) __syncthreads();
@@ -2967,6 +2991,7 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.lim = a.wrap ? a.w : 1 << 30;
     st.rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
     st.hplane = a.h;
+    st.top_lds = lane == 0 && y0 > 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int yr = y + 64 * r;
