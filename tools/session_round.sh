@@ -18,4 +18,5 @@ BENCH_BATCH=2048 bash tools/pmc_session.sh ${1:-round}/pmc_B || exit $?
 bash tools/bench_configs.sh ${1:-round}/configs A C C2 D E || exit $?
 bash tools/pmc_config.sh ${1:-round}/pmc_C C 512 || exit $?
 bash tools/pmc_config.sh ${1:-round}/pmc_E E 512 || exit $?
+bash tools/pmc_sq2.sh ${1:-round}/pmc_Bsq B 2048 || exit $?
 echo "== session done"
