@@ -108,6 +108,7 @@ struct TvArgs {
   int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3)
   int sor_rows2;               // lean SOR with two rows per lane for levels of 321..640 rows (else the pipeline)
   int smsys;                   // smoothness + system in one launch (k_tv_smsys)
+  int prepd;                   // prep + derivatives in one launch (k_tv_prepd, intensity images; 0: three launches)
   int smsys2d;                 // ... and on 2-D tiles for tall levels (k_tv_smsys2d; 0: two launches there, A/B)
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)
 };
@@ -138,6 +139,8 @@ void launch_aggregate(const AggArgs &a, hipStream_t s);
 void launch_tv_prep(const TvArgs &a, hipStream_t s);
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s);
 void launch_tv_deriv2(const TvArgs &a, hipStream_t s);
+bool tv_prepd_ok(const TvArgs &a);
+void launch_tv_prepd(const TvArgs &a, hipStream_t s);
 void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
 bool tv_smsys_ok(const TvArgs &a);

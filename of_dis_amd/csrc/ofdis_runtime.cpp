@@ -88,6 +88,7 @@ struct ofdis_context {
   int opt_smsys2d = 2;
   int call_frames = 1;         // pairs of the current call (auto options)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
+  int opt_prepd = 1;           // prep + derivatives in one launch for intensity images (0: three launches, A/B)
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
@@ -498,11 +499,16 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.smsys2d = c->opt_smsys2d == 2 ? c->call_frames < 512 : c->opt_smsys2d;
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
-      timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
-      timed(c, 6, s, [&] {
-        launch_tv_deriv1(tv, s);
-        launch_tv_deriv2(tv, s);
-      });
+      tv.prepd = c->opt_prepd;
+      if (tv_prepd_ok(tv)) {
+        timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
+      } else {
+        timed(c, 5, s, [&] { launch_tv_prep(tv, s); });
+        timed(c, 6, s, [&] {
+          launch_tv_deriv1(tv, s);
+          launch_tv_deriv2(tv, s);
+        });
+      }
       for (int it = 0; it < n_inner; ++it) {
         tv.first_iter = it == 0;
         timed(c, 7, s, [&] {
@@ -1197,7 +1203,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
-      {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
+      {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},

@@ -107,7 +107,8 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_cring", 0, 1),       # sweep-per-wave SOR without the LDS coefficient ring
     ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
-    ("smsys2d", 0, 2),         # tall levels: two launches instead of the 2-D tiled fused one (auto: on below 512 pairs)
+    ("smsys2d", 0, 2),
+    ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)         # tall levels: two launches instead of the 2-D tiled fused one (auto: on below 512 pairs)
 ]
 
 
