@@ -55,8 +55,10 @@ METRIC = "MPix/s (and frames/sec) 1080p op-point-2; avg EPE vs CPU ref"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first (the clocks and the caches settle: 3 left the first timed steps of a "
+                         "fresh process up to 4 %% slower)")
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="frame pairs per GPU per step (0 = the config's)")
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
