@@ -157,7 +157,13 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        instead of the sweep-per-wave SOR;
  *   "sor_cring" (0/1, default 1): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
  *                        hands them to the later sweeps through LDS (solverit <= 3);
+ *   "sor_rows2" (0/1, default 1): levels of 321..640 rows run the sweep-per-wave SOR with two rows per lane
+ *                        (else the register pipeline);
  *   "smsys" (0/1, default 1): smoothness and system of a TV iteration in one launch;
+ *   "smsys2d" (0/1/2, default 2): the fused launch on 2-D tiles for levels taller than 256 rows (0: two
+ *                        launches there; 2 = automatic: on for calls of fewer than 512 pairs);
+ *   "prepd" (0/1, default 1): for intensity images, image warp, temporal images and the derivative filters
+ *                        of a level in one launch (0: three launches);
  *   "sor_mode" (0/1, default 0): 0 = sor_coupled's exact lexicographic order (the reference's bits);
  *                        1 = red-black order (SURVEY §7 4(ii) throughput mode: every half-sweep fully
  *                        parallel; a different iteration -- NOT the reference's bits, end-point error
