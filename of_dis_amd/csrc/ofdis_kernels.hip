@@ -152,9 +152,13 @@ __global__ __launch_bounds__(256) void k_pyr_base_gray(PyrBaseArgs a) {
   a.out[t] = (float)sum * scale;
 }
 
+// One thread per output value over the flattened [2n][h][w * noc] range (full waves on narrow levels).
 __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a) {
-  const int xc = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-  if (xc >= a.w * a.noc) return;
+  const int rw = a.w * a.noc;
+  const long total = (long)a.n2 * a.h * rw;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const long r = t / rw;
+  const int xc = (int)(t - r * rw), y = (int)(r % a.h), f = (int)(r / a.h);
   const int x = xc / a.noc, c = xc - x * a.noc;
   const long idx = (((long)f * a.h + y) * a.w + x) * a.noc + c;
   const int sw = 2 * a.w;
@@ -162,6 +166,7 @@ __global__ __launch_bounds__(256) void k_pyr_down(PyrDownArgs a) {
   const float p = s[((2 * y) * sw + 2 * x) * a.noc + c], q = s[((2 * y) * sw + 2 * x + 1) * a.noc + c];
   const float u = s[((2 * y + 1) * sw + 2 * x) * a.noc + c], v = s[((2 * y + 1) * sw + 2 * x + 1) * a.noc + c];
   a.dst[idx] = ((p + q) + (u + v)) * 0.25f;
+  }
 }
 
 __device__ __forceinline__ int reflect101(int i, int n) {
@@ -192,10 +197,14 @@ __global__ __launch_bounds__(256) void k_pyr_gradmag(PyrGradmagArgs a) {
   a.out[((long)f * a.Hp + Y) * a.Wp + X] = sqrtf(dx * dx + dy * dy);
 }
 
+// One thread per padded pixel over the flattened [2n][H][W] range (full waves on narrow levels: a 136-wide
+// padded 1080p level 4 filled 53 % of a row-per-block launch's lanes).
 __global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
   const int W = a.w + 2 * a.pad, H = a.h + 2 * a.pad;
-  const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y, f = blockIdx.z;
-  if (X >= W) return;
+  const long total = (long)a.n2 * H * W;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const long r = t / W;
+  const int X = (int)(t - r * W), Y = (int)(r % H), f = (int)(r / H);
   const long idx = ((long)f * H + Y) * W + X;
   const int sx = X - a.pad, sy = Y - a.pad;
   const int noc = a.noc, w = a.w;
@@ -221,6 +230,7 @@ __global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
       a.dx[o] = 0.0f;
       a.dy[o] = 0.0f;
     }
+  }
   }
 }
 
@@ -3396,10 +3406,11 @@ void launch_pyr_gradmag(const PyrGradmagArgs &a, hipStream_t s) {
   k_pyr_gradmag<<<dim3(ceil_div(a.Wp, 256), a.Hp, 2 * a.n), 256, 0, s>>>(a);
 }
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {
-  k_pyr_down<<<dim3(ceil_div((long)a.w * a.noc, 256), a.h, a.n2), 256, 0, s>>>(a);
+  k_pyr_down<<<std::min(ceil_div((long)a.n2 * a.h * a.w * a.noc, 256), 1u << 22), 256, 0, s>>>(a);  // grid-stride beyond
 }
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s) {
-  k_pyr_pad_grad<<<dim3(ceil_div(a.w + 2 * a.pad, 256), a.h + 2 * a.pad, a.n2), 256, 0, s>>>(a);
+  k_pyr_pad_grad<<<std::min(ceil_div((long)a.n2 * (a.h + 2 * a.pad) * (a.w + 2 * a.pad), 256), 1u << 22), 256, 0,
+                   s>>>(a);  // grid-stride beyond 2^22 workgroups
 }
 template <int JM>
 static void patch_jm(const PatchArgs &a, hipStream_t s) {
