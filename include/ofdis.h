@@ -148,7 +148,9 @@ int ofdis_pyramid_u8_host(ofdis_context *ctx, const uint8_t *img, int width, int
 
 /* Per-stage capture for parity tests: when set, the next run copies frame 0's flow at scale s after
  * patch aggregation (dis_flow[s]) and after variational refinement (tv_flow[s]), each
- * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL). */
+ * w_s*h_s*nop interleaved floats, into these host arrays (entries may be NULL).  A capturing run issues
+ * the whole batch as one launch on one stream whatever the "streams" / "chunk" options; a batch larger
+ * than ofdis_max_frames_per_launch() returns OFDIS_ERR_UNSUPPORTED while a capture is set. */
 int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, float *const *tv_flow, int nscales);
 
 /* Tuning / A-B switches:
@@ -168,7 +170,12 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        1 = red-black order (SURVEY §7 4(ii) throughput mode: every half-sweep fully
  *                        parallel; a different iteration -- NOT the reference's bits, end-point error
  *                        gated against the exact path; the one option that changes results);
- *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch;
+ *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (patches of at most
+ *                        448 values; larger ones always run the any-shape kernel);
+ *   "patch_window" (0/1, default 1): p = 8 / 12 patches read their bilinear taps from an LDS copy of the
+ *                        sample window (0: eight-lane patches gathering the taps from the L1 cache);
+ *   "patch_generic" (0/1, default 0): every patch shape on the any-shape kernel (runtime value loops: the
+ *                        default for p*p*noc > 448, e.g. RGB p >= 14, gray p >= 22);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
  *   "graph" (0/1/2/3, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
  *                        parameters repeat (re-captured when they change); 1 captures single-stream
@@ -189,7 +196,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);
 
 /* Largest number of frame pairs one launch of the refinement kernels takes at this size (their plane groups
- * are addressed with 32-bit offsets: frames * noc * plane < 2^30 floats); larger batches are chunked. */
+ * are addressed with 32-bit offsets: frames * noc * plane < 2^30 floats); larger batches are chunked.
+ * A size at which one frame alone exceeds that (e.g. ~20k x 20k RGB with sc_l 0) returns
+ * OFDIS_ERR_INVALID_ARGUMENT here and from every run entry point. */
 int ofdis_max_frames_per_launch(const ofdis_params *p, int width, int height, int *frames);
 
 /* HIP-event timing of individual kernels on the launch stream (used by bench.py for the roofline). */
@@ -222,6 +231,10 @@ int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height,
 /* Deterministic synthetic frame pair: band-limited texture + noise, frame b is frame
  * a moved along a known smooth flow (OF) or a horizontal disparity (DE).  Host buffers [h][w][noc]. */
 int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, int mode);
+/* The same texture and noise, frame b a pure translation of frame a: b(x, y) = a(x - sx, y - sy), i.e. the
+ * true flow is (sx, sy) at every pixel (the known-answer setups of SURVEY §4). */
+int ofdis_synth_shift_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, float sx,
+                              float sy);
 
 #ifdef __cplusplus
 }

@@ -118,6 +118,7 @@ def lib():
         "ofdis_read_pnm": ([C.c_char_p, vp, C.POINTER(i), C.POINTER(i), C.POINTER(i), C.c_size_t], i),
         "ofdis_read_image": ([C.c_char_p, vp, C.POINTER(i), C.POINTER(i), i, C.c_size_t], i),
         "ofdis_synth_pair_u8": ([vp, vp, i, i, i, i, i], i),
+        "ofdis_synth_shift_pair_u8": ([vp, vp, i, i, i, i, C.c_float, C.c_float], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -106,7 +106,6 @@ int ofdis_params_validate(const ofdis_params *p, int width, int height, int imgp
   if (p->gradmag && p->noc != 1) return OFDIS_ERR_INVALID_ARGUMENT;  // SELECTCHANNEL 2 is single-channel
   if (p->p_samp_s < 2 || (p->p_samp_s & 1)) return OFDIS_ERR_INVALID_ARGUMENT;
   if ((p->p_samp_s * p->p_samp_s * p->noc) % 4) return OFDIS_ERR_INVALID_ARGUMENT;
-  if (p->p_samp_s * p->p_samp_s * p->noc > 448) return OFDIS_ERR_UNSUPPORTED;  // 7 values per lane
   if (p->sc_l < 0 || p->sc_f < p->sc_l || p->sc_f > 16) return OFDIS_ERR_INVALID_ARGUMENT;
   if (p->sc_l > 8) return OFDIS_ERR_UNSUPPORTED;  // exact box-mean pyramid
   if (p->costfct < 0 || p->costfct > 2) return OFDIS_ERR_UNSUPPORTED;  // 10 (NCC) unimplemented upstream
@@ -253,7 +252,10 @@ static inline uint8_t to_u8(double v) {
 // Frame a: band-limited texture + N(0,2) noise.  Frame b samples the same texture at x - u(x,y):
 // OF: u = global shift (6.5, 2.25) + rotation <= 0.5 deg + zoom <= 1 % about the centre, varying with
 // `frame`; DE: a pure horizontal disparity of -6.5 px.  Noise is independent per frame.
-int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, int mode) {
+// kind 0: the motion of `mode` above; kind 1: a pure translation by (sx, sy) (the known-answer setups of
+// b(x, y) = a(x - sx, y - sy), so the true flow is (sx, sy) everywhere).
+static int synth_pair(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, int mode,
+                      int kind, double sx, double sy) {
   if (!img_a || !img_b || width <= 0 || height <= 0 || (noc != 1 && noc != 3)) return OFDIS_ERR_INVALID_ARGUMENT;
   uint64_t sa = 1234ull + (uint64_t)frame * 2ull, sb = 1235ull + (uint64_t)frame * 2ull;
   const double cx = 0.5 * width, cy = 0.5 * height;
@@ -272,7 +274,10 @@ int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, i
     for (int y = y0; y < y1; ++y)
       for (int x = 0; x < width; ++x) {
         double bx, by;
-        if (mode == OFDIS_MODE_DE) {
+        if (kind == 1) {
+          bx = x - sx;
+          by = y - sy;
+        } else if (mode == OFDIS_MODE_DE) {
           bx = x + 6.5;  // b(x) = a(x + 6.5): disparity -6.5
           by = y;
         } else {
@@ -295,6 +300,15 @@ int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, i
   rows(0, (int)((long)height / nt));
   for (auto &t : th) t.join();
   return OFDIS_OK;
+}
+
+int ofdis_synth_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, int mode) {
+  return synth_pair(img_a, img_b, width, height, noc, frame, mode, 0, 0.0, 0.0);
+}
+
+int ofdis_synth_shift_pair_u8(uint8_t *img_a, uint8_t *img_b, int width, int height, int noc, int frame, float sx,
+                              float sy) {
+  return synth_pair(img_a, img_b, width, height, noc, frame, OFDIS_MODE_OF, 1, sx, sy);
 }
 
 }  // extern "C"

@@ -67,6 +67,7 @@ struct PatchArgs {
                                               // sqrt(ex^2 + ey^2) > thresh (patch.cpp:197) without the sqrt
   int camlr;
   int wave_per_patch;                         // 1: force the one-wave-per-patch kernel (A/B testing)
+  int generic;                                // 1: force the any-shape kernel k_patchg (parity testing)
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)

@@ -778,6 +778,247 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
   if (ODD && s8 < 4) pwo[8 * PAIRS + s8] = pw[PAIRS];
 }
 
+// ---------------------------------------------------------------- DIS patches, any shape (eight lanes per patch)
+// k_patch8's lane layout and reduction trees with the values walked by a runtime loop instead of held in
+// registers, so every p^2 noc the reference accepts (a multiple of 4, patch.cpp:230) runs, however large:
+// lane s of a patch visits v = s + 8k in k order -- exactly Eigen's packet-accumulator chain s -- and then
+// its value of the odd trailing packet.  Nothing per value lives in registers or LDS: template, gradients
+// and target samples are re-read per pass from the cache-resident pyramid.  The normalised template value
+// is the same single subtraction A - mean as InitializePatch's (patch.cpp:341-342), so recomputing it
+// gives the stored bits; the bilinear sample is recomputed for the pass after the mean (same bits).
+struct ChainAcc {  // one Eigen packet-accumulator chain per lane + the lane's tail-packet value
+  float acc = 0.0f, tail = 0.0f;
+  __device__ __forceinline__ void add(int k, int pairs, float x) {
+    if (k < pairs)
+      acc = k == 0 ? x : acc + x;
+    else
+      tail = x;
+  }
+  // res0 + res1, odd packet, (l0 + l2) + (l1 + l3): grp_eigen_sum's tree
+  __device__ __forceinline__ float total(int pairs, int odd) const {
+    float r;
+    if (pairs > 0) {
+      r = acc + grp_xor4(acc);
+      if (odd) r = r + tail;
+    } else {
+      r = tail;
+    }
+    r = r + grp_xor2(r);
+    return r + grp_xor1(r);
+  }
+};
+
+// Calls fn(k, off) for chain s8's values in k order (k == pairs: the tail-packet value 8 pairs + (s8 & 3)),
+// off = the value's float offset inside a patch window of rows of pn = p * noc floats, rowstep apart.
+template <class F>
+__device__ __forceinline__ void chain_walk(int s8, int pairs, int odd, int pn, long rowstep, F &&fn) {
+  int r = 0, c = s8;
+  while (c >= pn) {
+    c -= pn;
+    ++r;
+  }
+  for (int k = 0; k < pairs; ++k) {
+    fn(k, (long)r * rowstep + c);
+    c += 8;
+    while (c >= pn) {
+      c -= pn;
+      ++r;
+    }
+  }
+  if (odd) {
+    const int v = 8 * pairs + (s8 & 3);
+    fn(pairs, (long)(v / pn) * rowstep + v % pn);
+  }
+}
+
+template <int NOP>
+__global__ __launch_bounds__(256) void k_patchg(PatchArgs a) {
+  const LevelGeom &g = a.g;
+  const int s8 = threadIdx.x & 7;
+  const long gp = (long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const bool live = gp < (long)a.n * g.npatch;
+  const long gq = live ? gp : 0;
+  const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
+  const int pxi = ip / g.noph, pyi = ip % g.noph;
+  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+  const long fs = (long)g.W * g.H * a.noc;
+  const int noc = a.noc, P = a.p, W = g.W, pn = P * noc;
+  const int pairs = a.novals >> 3, odd = (a.novals >> 2) & 1;
+  const long rowstep = (long)W * noc;
+  const float inv_n = 1.0f / (float)a.novals;
+  const bool pow2 = (a.novals & (a.novals - 1)) == 0;  // x / n == x * (1/n) exactly for n = 2^k
+  auto div_n = [&](float x) { return pow2 ? x * inv_n : x / (float)a.novals; };
+  // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
+  const int rpx = (int)roundf(ptr0) + g.pad, rpy = (int)roundf(ptr1) + g.pad;
+  const long rbase = (long)f * fs + ((long)(rpy - P / 2) * W + (rpx - P / 2)) * noc;
+  const float *A = a.img_a + rbase, *DX = a.dx_a + rbase, *DY = a.dy_a + rbase;
+  float tmean = 0.0f;
+  if (a.patnorm > 0) {
+    ChainAcc m;
+    chain_walk(s8, pairs, odd, pn, rowstep, [&](int k, long o) { m.add(k, pairs, A[o]); });
+    tmean = div_n(m.total(pairs, odd));
+  }
+  // ---- ComputeHessian (patch.cpp:69-86)
+  float H00, H01 = 0.0f, H11 = 0.0f;
+  {
+    ChainAcc q0, q1, q2;
+    chain_walk(s8, pairs, odd, pn, rowstep, [&](int k, long o) {
+      const float gx = DX[o], gy = DY[o];
+      q0.add(k, pairs, gx * gx);
+      q1.add(k, pairs, gx * gy);
+      q2.add(k, pairs, gy * gy);
+    });
+    H00 = q0.total(pairs, odd);
+    if (NOP == 2) {
+      H01 = q1.total(pairs, odd);
+      H11 = q2.total(pairs, odd);
+      if (H00 * H11 - H01 * H01 == 0.0f) {
+        H00 = (float)((double)H00 + 1e-10);
+        H11 = (float)((double)H11 + 1e-10);
+      }
+    } else if (H00 == 0.0f) {
+      H00 = (float)((double)H00 + 1e-10);
+    }
+  }
+  const Llt2 fac = llt2_factor(H00, H01, H11);
+  const float fac1 = llt1_factor(H00);
+  const float tlast = A[0] - tmean;  // keeps the template work alive in the diagnostics below
+  if (a.stage == 1) {  // timing diagnostic "pconst": construction only
+    if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tlast;
+    return;
+  }
+  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
+  float pin0 = 0.0f, pin1 = 0.0f;
+  if (a.prev) {
+    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
+    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
+    pin0 = pv[0] * 2;
+    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  if (a.stage == 2) {  // "pconst + pinit"
+    if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tlast + pin0 + pin1;
+    return;
+  }
+  const float *Bimg = a.img_b + (long)f * fs;
+  // getPatchStaticBil + mean + LossComputeErrorImage (patch.cpp:221-273,345-413) at (x, y): the Eigen sums
+  // of |w|, dx e (, dy e); with pwo, the loss weights w are written instead
+  auto eval = [&](float x, float y, float &r0, float &e0, float &e1, float *pwo) {
+    const int pos0 = (int)ceilf(x + 0.00001f) + g.pad;
+    const int pos1 = (int)ceilf(y + 0.00001f) + g.pad;
+    const int pos2 = (int)floorf(x), pos3 = (int)floorf(y);
+    const float rx = x - (float)pos2, ry = y - (float)pos3;
+    const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+    const float *Q = Bimg + ((long)(pos1 - P / 2) * W + (pos0 - P / 2)) * noc;
+    auto sample = [&](long o) {
+      const float *q = Q + o;
+      return w0 * q[0] + w1 * q[-noc] + w2 * q[-rowstep] + w3 * q[-rowstep - noc];
+    };
+    float mean = 0.0f;
+    if (a.patnorm > 0) {
+      ChainAcc m;
+      chain_walk(s8, pairs, odd, pn, rowstep, [&](int k, long o) { m.add(k, pairs, sample(o)); });
+      mean = div_n(m.total(pairs, odd));
+    }
+    ChainAcc sa, sx, sy;
+    chain_walk(s8, pairs, odd, pn, rowstep, [&](int k, long o) {
+      float pd = sample(o);
+      if (a.patnorm > 0) pd = pd - mean;
+      const float tmp = a.patnorm > 0 ? A[o] - tmean : A[o];
+      const float d = pd - tmp;
+      float w, e;
+      if (a.costfct == 0) {
+        e = d;
+        w = fabsf(d);
+      } else if (a.costfct == 1) {
+        w = sqrt_nonneg(fabsf(d));
+        e = copysignf(w, d);
+      } else {
+        w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        e = copysignf(w, d);
+      }
+      if (pwo) {
+        const int v = k < pairs ? s8 + 8 * k : 8 * pairs + (s8 & 3);
+        if (k < pairs || s8 < 4) pwo[v] = w;
+      } else {
+        sa.add(k, pairs, fabsf(w));
+        sx.add(k, pairs, DX[o] * e);
+        if (NOP == 2) sy.add(k, pairs, DY[o] * e);
+      }
+    });
+    if (!pwo) {
+      r0 = sa.total(pairs, odd);
+      e0 = sx.total(pairs, odd);
+      if (NOP == 2) e1 = sy.total(pairs, odd);
+    }
+  };
+  // ---- OptimizeStart (patch.cpp:117-154)
+  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
+  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
+  const float st0 = pt0, st1 = pt1;
+  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
+  int cnt = 0;
+  bool converged = !live, start_oob = false;
+  float b0 = 0.0f, b1 = 0.0f;
+  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  auto err = [&]() {  // OptimizeComputeErrImg (patch.cpp:275-295)
+    float r0 = 0.0f;
+    eval(pt0, pt1, r0, b0, b1, nullptr);
+    sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+    if (cnt == 1) sq_init = sq;
+    mares_old = mares;
+    mares = div_n(r0);
+    const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) &
+                      ((cnt < a.min_iter) | (sq / sq_init >= a.dp_thresh_sq)) &
+                      ((cnt < a.min_iter) | (mares / mares_old <= a.dr_thresh));
+    if (!keep) converged = true;
+  };
+  if (!converged) {
+    if (oob(pt0, pt1)) {
+      converged = start_oob = true;  // pweight never written upstream: defined as 0
+    } else {
+      mares = 1e5f;
+      err();
+    }
+  }
+  // ---- OptimizeIter loop (patch.cpp:156-210)
+  while (!converged) {
+    ++cnt;
+    if (NOP == 2) {
+      llt2_solve(fac, b0, b1, d0, d1);
+      p0 = p0 - d0;
+      p1 = p1 - d1;
+    } else {
+      d0 = llt1_solve(fac1, b0);
+      p0 = p0 - d0;
+      p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+    }
+    pt0 = ptr0 + p0;
+    if (NOP == 2) pt1 = ptr1 + p1;
+    const float ex = st0 - pt0, ey = st1 - pt1;
+    if (ex * ex + ey * ey > a.outlier_sq || oob(pt0, pt1)) {
+      p0 = pin0;
+      p1 = pin1;
+      pt0 = ptr0 + p0;
+      if (NOP == 2) pt1 = ptr1 + p1;
+      converged = true;
+    }
+    err();
+  }
+  // ---- outputs: the loss weights of the last evaluation, i.e. at the final position (a pure function of it)
+  if (!live) return;
+  if (s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
+  float *pwo = a.pweight + gp * a.novals;
+  if (start_oob) {
+    chain_walk(s8, pairs, odd, pn, rowstep, [&](int k, long) {
+      const int v = k < pairs ? s8 + 8 * k : 8 * pairs + (s8 & 3);
+      if (k < pairs || s8 < 4) pwo[v] = 0.0f;
+    });
+  } else {
+    float r0, e0, e1;
+    eval(pt0, pt1, r0, e0, e1, pwo);
+  }
+}
+
 // ---------------------------------------------------------------- DIS patches, windowed (eight lanes per patch)
 // Same lane layout, reduction trees and per-patch arithmetic as k_patch8, but the bilinear taps come from
 // LDS: per iteration the eight lanes of a patch copy its (p+1) x (p+1) x noc sample window (rows of
@@ -3448,7 +3689,7 @@ static void patchw(const PatchArgs &a, hipStream_t s) {
   }
 }
 void launch_patch(const PatchArgs &a, hipStream_t s) {
-  if (a.window && !a.wave_per_patch) {  // LDS-windowed eight-lane form for the shapes of the op-points
+  if (a.window && !a.wave_per_patch && !a.generic) {  // LDS-windowed eight-lane form for the shapes of the op-points
     switch (a.p * 4 + a.noc) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;
       case 12 * 4 + 1: patchw<12, 1, 4, 3>(a, s); return;
@@ -3456,7 +3697,7 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
       case 12 * 4 + 3: patchw<12, 3, 2, 2, 1>(a, s); return;  // L2 cost: samples kept, one wave per SIMD
     }
   }
-  if (!a.wave_per_patch) {
+  if (!a.wave_per_patch && !a.generic) {
     switch (a.novals) {  // eight lanes per patch for the common shapes
       case 64: patch8<8, 0>(a, s); return;    // p 8, gray
       case 144: patch8<18, 0>(a, s); return;  // p 12, gray
@@ -3468,6 +3709,14 @@ void launch_patch(const PatchArgs &a, hipStream_t s) {
     }
   }
   const int J = (a.novals + 63) / 64;
+  if (a.generic || J > 7) {  // any shape: runtime value loops (p^2 noc > 448, or forced by option patch_generic)
+    const unsigned grid = ceil_div((long)a.n * a.g.npatch, 32);
+    if (a.nop == 2)
+      k_patchg<2><<<grid, 256, 0, s>>>(a);
+    else
+      k_patchg<1><<<grid, 256, 0, s>>>(a);
+    return;
+  }
   if (J <= 1)
     patch_jm<1>(a, s);
   else if (J <= 3)

@@ -93,6 +93,7 @@ struct ofdis_context {
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
+  int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
@@ -389,6 +390,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.camlr = 0;
     pa.wave_per_patch = c->opt_wave_per_patch;
     pa.window = c->opt_patch_window;
+    pa.generic = c->opt_patch_generic;
     pa.g = g;
     if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
       PatchArgs pd = pa;
@@ -805,7 +807,7 @@ int tv_frame_cap(const ofdis_params *p, int width, int height) {
   if (!p->usetvref) return 1 << 30;
   const Plan P1 = batch_plan(p, 1, width, height);
   const long per = (long)P1.noc * (long)P1.tv_plane;
-  return (int)std::max(1L, std::min((long)(1 << 30), ((1L << 30) - 1) / per));
+  return (int)std::min((long)(1 << 30), ((1L << 30) - 1) / per);  // 0: one frame alone is too large
 }
 
 // How one call is issued: the whole batch on one stream and workspace (single), chunks round-robin over
@@ -826,12 +828,15 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
   cp.width = width;
   cp.height = height;
   cp.init = init;
-  const int nstreams = stream_count(c, n);
-  int chunk = c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : (n + nstreams - 1) / nstreams;
+  // a stage capture (frame 0's per-scale flow) runs the batch as one launch on one stream, whatever the
+  // stream / chunk options; it is refused only for batches beyond the launch-size cap
+  const int nstreams = capturing ? 1 : stream_count(c, n);
+  int chunk = capturing ? n : c->opt_chunk > 0 ? std::min(c->opt_chunk, n) : (n + nstreams - 1) / nstreams;
   chunk = std::min(chunk, tv_frame_cap(p, width, height));
+  if (chunk < 1) return OFDIS_ERR_INVALID_ARGUMENT;
   cp.chunk = chunk;
   cp.nchunks = (n + chunk - 1) / chunk;
-  if (cp.nchunks > 1 && capturing) return OFDIS_ERR_UNSUPPORTED;  // stage capture reads frame 0 of one launch
+  if (cp.nchunks > 1 && capturing) return OFDIS_ERR_UNSUPPORTED;
   if (cp.nchunks == 1) {
     cp.kind = CallPlan::kSingle;
     cp.whole = batch_plan(p, n, width, height, init);
@@ -967,7 +972,10 @@ int validate_call(const ofdis_params *p, int width, int height, bool init) {
   int rc = ofdis_params_validate(p, -1, -1, -1);
   if (rc) return rc;
   Plan P = batch_plan(p, 1, width, height, init);
-  return ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
+  rc = ofdis_params_validate(p, P.Wp, P.Hp, P.pad);
+  if (rc) return rc;
+  // one frame's TV plane group must stay below 2^30 floats (32-bit byte offsets in the system kernels)
+  return tv_frame_cap(p, width, height) >= 1 ? OFDIS_OK : OFDIS_ERR_INVALID_ARGUMENT;
 }
 
 // The whole-batch device path on stream s (call ordering done by the caller).
@@ -1205,7 +1213,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
-      {"patch_window", &ofdis_context::opt_patch_window, 0, 1},
+      {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
@@ -1357,7 +1365,7 @@ int ofdis_max_frames_per_launch(const ofdis_params *p, int width, int height, in
   const int rc = ofdis_params_validate(p, -1, -1, -1);
   if (rc) return rc;
   *frames = tv_frame_cap(p, width, height);
-  return OFDIS_OK;
+  return *frames >= 1 ? OFDIS_OK : OFDIS_ERR_INVALID_ARGUMENT;
 }
 
 }  // extern "C"

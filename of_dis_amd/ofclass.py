@@ -51,6 +51,15 @@ def synth_pair(width: int, height: int, noc: int = 1, frame: int = 0, mode: int 
     return a, b
 
 
+def synth_shift_pair(width: int, height: int, shift, noc: int = 1, frame: int = 0):
+    """The synth_pair texture with frame b a pure translation of frame a by shift = (sx, sy) (true flow)."""
+    a = np.empty((height, width, noc), np.uint8)
+    b = np.empty((height, width, noc), np.uint8)
+    check(lib().ofdis_synth_shift_pair_u8(a.ctypes.data, b.ctypes.data, width, height, noc, frame,
+                                          float(shift[0]), float(shift[1])), "synth")
+    return a, b
+
+
 def write_flo(path: str, flow: np.ndarray) -> None:
     """SaveFlowFile (run_dense.cpp:17-58)."""
     flow = np.ascontiguousarray(flow, _f32)
@@ -257,7 +266,7 @@ def algorithmic_bytes(p: Params, width: int, height: int, kernel: str) -> float:
     return v.value
 
 
-__all__ = ["OFClass", "Context", "Params", "oppoint", "params_from_strings", "validate", "synth_pair",
+__all__ = ["OFClass", "Context", "Params", "oppoint", "params_from_strings", "validate", "synth_pair", "synth_shift_pair",
            "write_flo", "write_pfm", "read_flo", "read_image", "auto_first_scale", "kernel_names", "algorithmic_bytes",
            "max_frames_per_launch",
            "MODE_OF", "MODE_DE"]

@@ -59,7 +59,10 @@ CASES = [
     (192, 128, 3, 1, 3, {"usefbcon": 1, "costfct": 1}),       # ... RGB (weight-pointer quirk, bounds [1, w-1))
     (240, 120, 1, 2, 4, {"usefbcon": 1, "max_iter": 16, "min_iter": 16}),  # ... depth (right camera clamp)
     (400, 300, 1, 1, 2, {"sc_l": 0, "sc_f": 2}),              # 300 rows: 5 row groups x 3 sweep waves
-    (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows: register pipeline, 1024 threads
+    (320, 600, 1, 2, 2, {"sc_l": 0, "sc_f": 1}),              # 600 rows, 3 sweeps: two rows per lane (R = 2)
+    (320, 600, 1, 1, 2, {"sc_l": 0, "sc_f": 1, "tv_solverit": 2}),  # 2 sweeps, 513..1024 rows: R = 2, 1024 threads
+    (256, 1000, 1, 2, 2, {"sc_l": 0, "sc_f": 1, "tv_solverit": 2}),  # ... depth, 1000 rows (8 row-pair groups)
+    (256, 704, 1, 1, 2, {"sc_l": 0, "sc_f": 1}),              # 3 sweeps, 641..1024 rows: register pipeline
     (300, 280, 3, 1, 2, {"sc_l": 0, "sc_f": 1}),              # RGB, 280 rows: streaming smoothness + system
     (200, 300, 3, 2, 2, {"sc_l": 0, "sc_f": 1}),              # ... RGB depth, tall (unfolded) layout
     (160, 120, 1, 1, 2, {"omp_build": 1}),                    # USE_OPENMP build: point SOR (solver.c:34-78)
@@ -107,8 +110,9 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_cring", 0, 1),       # sweep-per-wave SOR without the LDS coefficient ring
     ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
-    ("smsys2d", 0, 2),
-    ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)         # tall levels: two launches instead of the 2-D tiled fused one (auto: on below 512 pairs)
+    ("smsys2d", 0, 2),         # tall levels: two launches instead of the 2-D tiled fused one (auto: on below 512 pairs)
+    ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
+    ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
 ]
 
 
@@ -371,3 +375,35 @@ def test_cli_stdout_timers(od, tmp_path):
         assert int(m.group(1)) == s
         ws, hs = w >> s, h >> s
         assert int(m.group(2)) == -(-ws // 4) * -(-hs // 4)  # nopw * noph, steps 4 (patchgrid.cpp:43-46)
+
+
+def test_capture_on_large_batch(oracle, od, ctx):
+    """A stage capture on a batch that would be chunked over two streams (>= 512 pairs, and with explicit
+    stream / chunk options) runs as one launch and captures frame 0 exactly."""
+    import torch
+    w, h, n = 96, 64, 520
+    pa, pb = od.synth_pair(w, h, 1, 0, 1)
+    a = torch.from_numpy(np.stack([pa] * n)).cuda()
+    b = torch.from_numpy(np.stack([pb] * n)).cuda()
+    p = od.oppoint(2, w, 1, 1)
+    q = oracle.oppoint(2, w, 1, 1)
+    ref, cap_d, cap_t = oracle.run_u8(pa, pb, q, capture=True)
+    for streams, chunk in ((0, 0), (3, 100)):
+        dis = {s: np.zeros_like(v) for s, v in cap_d.items()}
+        tv = {s: np.zeros_like(v) for s, v in cap_t.items()}
+        ctx.set_option("streams", streams)
+        ctx.set_option("chunk", chunk)
+        ctx.set_capture(dis, tv)
+        try:
+            out = ctx.run(a, b, p)
+            torch.cuda.synchronize()
+        finally:
+            ctx.set_capture(None, None)
+            ctx.set_option("streams", 0)
+            ctx.set_option("chunk", 0)
+        for s in cap_d:
+            assert_bitexact(dis[s], cap_d[s], f"streams={streams} chunk={chunk}: scale {s} after aggregation")
+            assert_bitexact(tv[s], cap_t[s], f"streams={streams} chunk={chunk}: scale {s} after TV refinement")
+        o = out.cpu().numpy()
+        assert_bitexact(o[0], ref, "frame 0")
+        assert_bitexact(o[n - 1], ref, "last frame")

@@ -99,7 +99,6 @@ def test_params_from_strings_matches_readme_order():
 @pytest.mark.parametrize("change,code", [
     ({"p_samp_s": 7}, _lib.ERR_INVALID_ARGUMENT),      # odd patch
     ({"p_samp_s": 0}, _lib.ERR_INVALID_ARGUMENT),
-    ({"p_samp_s": 22}, _lib.ERR_UNSUPPORTED),          # > 448 values per patch
     ({"sc_l": 7}, _lib.ERR_INVALID_ARGUMENT),          # sc_l > sc_f
     ({"costfct": 10}, _lib.ERR_UNSUPPORTED),           # NCC: unimplemented upstream too
     ({"patove": 1.0}, _lib.ERR_INVALID_ARGUMENT),
@@ -109,6 +108,18 @@ def test_params_from_strings_matches_readme_order():
 def test_validation_rejects(change, code):
     p = od.oppoint(2, 1920).copy(**change)
     assert od.validate(p, 1920, 1088, 8) == code
+
+
+@pytest.mark.parametrize("noc", [1, 3])
+def test_every_even_patch_size_accepted(noc):
+    """The reference takes any even p with p*p*noc a multiple of 4 (run_dense.cpp:280, patch.cpp:230): every
+    such shape up to 32 validates; odd sizes do not."""
+    for p_s in range(2, 34, 2):
+        p = od.oppoint(2, 1920, od.MODE_OF, noc).copy(p_samp_s=p_s)
+        assert od.validate(p, 1920, 1088, p_s) == 0, p_s
+        assert od.validate(p, 1920, 1088, p_s + 6) == 0, p_s  # imgpadding > p
+    for p_s in (3, 9, 15):
+        assert od.validate(od.oppoint(2, 1920, od.MODE_OF, noc).copy(p_samp_s=p_s)) == _lib.ERR_INVALID_ARGUMENT
 
 
 def test_validation_geometry():
