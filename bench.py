@@ -5,8 +5,8 @@ Default workload (BASELINE configs[1], "B"): run_OF_INT 1920x1080 grayscale, ope
 overlap 0.4, TV on), batches of synthetic frame pairs resident in HBM.  One step = the whole hot path
 (pad + pyramid + DIS + aggregation + TV + upsample + crop) over one batch of `--batch` pairs per GPU.
 `--config A|C|C2|D|E` runs the other BASELINE configs (640x480 op2; 1080p RGB op3 with the L1 cost / as
-op-point 3 defines it (L2); B at 32 pairs per GPU = 256 over 8 GPUs; 4K stereo depth op4 with 10 TV outer
-iterations).
+op-point 3 defines it (L2); D = a batch of 256 1080p op2 pairs per step sharded over the GPUs (strong
+scaling: 256 on one GPU, 32 per GPU on 8); 4K stereo depth op4 with 10 TV outer iterations).
 
 Multi-GPU: `--gpus N` (N > 1) without a torch.distributed environment re-launches this script as N ranks
 (`python -m torch.distributed.run --nproc-per-node N`, a child process -- this parent never touches a GPU)
@@ -44,12 +44,15 @@ CONFIGS = {
     "C": ("run_OF_RGB", 1920, 1080, 3, 1, 3, "6 2 16 16 0.05 0.95 0 12 0.75 0 1 1 1 10 10 5 1 3 1.6 2", 512),
     # op-point 3 as run_dense.cpp:248-253 defines it (costfct 0, L2); SURVEY §8(d): report both
     "C2": ("run_OF_RGB", 1920, 1080, 3, 1, 3, None, 512),
-    "D": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 32),
+    # BASELINE configs[3]: 256 pairs per step in total, sharded over the GPUs (strong scaling, STRONG below)
+    "D": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 256),
     # op-point 4 values with tv_innerit = 10; 512 = two 256-pair chunks on two streams
     # (256: 6.85k, 512: 7.57k, 1024: 7.54k MPix/s; profiles/r02/ab/ab_batch*)
     "E": ("run_DE_INT", 3840, 2160, 1, 2, 4, "7 2 128 128 0.05 0.95 0 12 0.75 0 1 0 1 10 10 5 10 3 1.6 2", 512),
 }
 METRIC = "MPix/s (and frames/sec) 1080p op-point-2; avg EPE vs CPU ref"
+# configs whose batch is the whole job's (sharded over the ranks) rather than each GPU's
+STRONG = {"D"}
 
 
 def parse():
@@ -61,6 +64,9 @@ def parse():
                          "fresh process up to 4 %% slower)")
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="frame pairs per GPU per step (0 = the config's)")
+    ap.add_argument("--total", type=int, default=0,
+                    help="frame pairs per step over ALL GPUs, sharded over the ranks (strong scaling; 0 = the "
+                         "config's: D 256, the others weak scaling at --batch per GPU)")
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample per leg (1 core, all cores; 0 = skip)")
@@ -162,25 +168,35 @@ def host_cores() -> int:
     return max(1, min(aff, share) if share > 0 else aff)
 
 
+def cpu_quota():
+    """CPUs this process may use by its cgroup quota (cgroup v2 cpu.max), or None when unlimited."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(O, q, pairs, W, H, seconds, binary, cfg_name):
     """The oracle port (oracle/ofdis_oracle.c, -O3 -msse4.1 -ffp-contract=off; the reference's default
     build semantics: lexicographic block SOR, no OpenMP) timed over whole pairs (pad + pyramid + OFClass
-    + upsample, the reference's verbosity-2 timer scope): one core, then one single-threaded worker per
-    host core, frame-parallel (ctypes releases the GIL inside the oracle)."""
+    + upsample, the reference's verbosity-2 timer scope): one core (with the stage breakdown), one
+    single-threaded worker per core of this process's CPU share, and one per host CPU of the node (nproc;
+    the cgroup quota is reported beside it -- on a shared box it caps that leg), frame-parallel (ctypes
+    releases the GIL inside the oracle)."""
     from concurrent.futures import ThreadPoolExecutor
     nd = len(pairs)
     t0 = time.perf_counter()
     done = 0
+    stages = []
     while True:
-        O.run_u8(pairs[done % nd][0], pairs[done % nd][1], q)
+        stages.append(O.run_u8_stages(pairs[done % nd][0], pairs[done % nd][1], q)[1])
         done += 1
         if time.perf_counter() - t0 > seconds:
             break
     t1 = time.perf_counter() - t0
-    cores = host_cores()
-    done_all = 0
-    t_all = 0.0
-    if cores > 1:
+
+    def parallel(workers):
         deadline = time.perf_counter() + seconds
 
         def worker(k):
@@ -191,9 +207,14 @@ def cpu_baseline(O, q, pairs, W, H, seconds, binary, cfg_name):
                 if time.perf_counter() > deadline:
                     return n
         t0 = time.perf_counter()
-        with ThreadPoolExecutor(cores) as ex:
-            done_all = sum(ex.map(worker, range(cores)))
-        t_all = time.perf_counter() - t0
+        with ThreadPoolExecutor(workers) as ex:
+            n = sum(ex.map(worker, range(workers)))
+        return n, time.perf_counter() - t0
+
+    cores = host_cores()
+    done_all, t_all = parallel(cores) if cores > 1 else (0, 0.0)
+    node = os.cpu_count() or 1
+    done_node, t_node = parallel(node) if node > cores else (0, 0.0)
     fair = None
     ff = os.path.join(ROOT, "profiles", "cpu_fairness.json")
     if os.path.exists(ff):
@@ -205,13 +226,53 @@ def cpu_baseline(O, q, pairs, W, H, seconds, binary, cfg_name):
            "frames_per_sec": round(done / t1, 3),
            "sample": f"{done} synthetic {W}x{H} {binary} pairs (config {cfg_name}), oracle/ofdis_oracle.c -O3 "
                      f"-msse4.1, 1 thread (pad+pyramid+OFClass+upsample), {t1:.1f} s",
-           "cores_all": cores, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "cores_all": cores, "nproc": os.cpu_count(), "cpu_quota": cpu_quota(), "cpu_model": cpu_model(),
+           "stages_ms_1core_median": {k: round(float(np.median([s_[k] for s_ in stages])) * 1e3, 3)
+                                      for k in stages[0]},
            "fairness_vs_reference": fair}
+    st = out["stages_ms_1core_median"]
+    out["pyramid_upsample_share"] = round((st["pyramid"] + st["upsample"]) / sum(st.values()), 3)
+    probe = os.path.join(ROOT, "profiles", "r03", "cpu_core_vs_probe.json")
+    if os.path.exists(probe):  # the port's OFClass core against SURVEY's probe of the reference (container)
+        try:
+            ent = json.load(open(probe))["configs"].get(cfg_name)
+            if ent:
+                out["dis_core_ratio_vs_reference_probe"] = {
+                    "ratio": ent["ofclass_ratio_vs_probe"], "port_ofclass_ms": ent["stages_min_ms"]["ofclass"],
+                    "reference_probe_ms": ent["probe_ofclass_ms"], "where": "survey container, 1 thread",
+                    "source": "tools/cpu_core_probe.py -> profiles/r03/cpu_core_vs_probe.json (BASELINE.md:30-34)"}
+        except Exception:
+            pass
     if done_all:
         out["value_all_cores"] = round(W * H * done_all / t_all / 1e6, 3)
         out["frames_per_sec_all_cores"] = round(done_all / t_all, 3)
         out["sample_all_cores"] = f"{done_all} pairs over {cores} worker threads, {t_all:.1f} s"
+    if done_node:
+        out["value_node"] = round(W * H * done_node / t_node / 1e6, 3)
+        out["frames_per_sec_node"] = round(done_node / t_node, 3)
+        out["cores_node"] = node
+        out["sample_node"] = f"{done_node} pairs over {node} worker threads (nproc), {t_node:.1f} s"
     return out
+
+
+def plan_shards(args, cfg, world, rank):
+    """This rank's [first, stop) of the step's pairs, the whole job's pairs per step and the scaling kind:
+    strong (--total, or config D's 256 pairs) shards one batch over the ranks; weak gives every rank
+    --batch pairs of its own."""
+    total = args.total or (cfg[7] if args.config in STRONG and not args.batch else 0)
+    if total:
+        if total < world:
+            raise SystemExit(f"bench.py: --total {total} < {world} ranks")
+        first, stop = shard_range_of(total, rank, world)
+        return first, stop, total, "strong"
+    B = args.batch or cfg[7]
+    first, stop = shard_range_of(B * world, rank, world)
+    return first, stop, B * world, "weak"
+
+
+def shard_range_of(n, rank, world):
+    from of_dis_amd.distributed import shard_range
+    return shard_range(n, rank, world)
 
 
 def dry_run(args, cfg):
@@ -222,8 +283,8 @@ def dry_run(args, cfg):
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    B = args.batch or cfg[7]
-    shard = odd.shard_range(B * world, rank, world)
+    first, stop, total, scaling = plan_shards(args, cfg, world, rank)
+    shard = (first, stop)
     t0 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))
     elapsed = time.perf_counter() - t0
@@ -236,9 +297,9 @@ def dry_run(args, cfg):
     if rank == 0:
         if world != args.gpus:
             raise SystemExit(f"world size {world} != --gpus {args.gpus}")
-        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": args.steps,
-                          "config": {"name": args.config, "batch_per_gpu": B}, "shards": shards,
-                          "frames": int(frames), "elapsed_max_s": elapsed}))
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "ranks": world, "steps": args.steps,
+                          "scaling": scaling, "config": {"name": args.config, "pairs_per_step": total},
+                          "shards": shards, "frames": int(frames), "elapsed_max_s": elapsed}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -263,6 +324,8 @@ def main():
     # the GPUs round robin and the control collectives go over gloo (RCCL refuses two ranks on one GPU)
     rehearsal = os.environ.get("OFDIS_BENCH_REHEARSAL") == "1"
     gpu = local % max(1, torch.cuda.device_count()) if rehearsal else local
+    # physical devices in use (a rehearsal's ranks share them); one GPU per rank otherwise
+    n_devices = min(world, max(1, torch.cuda.device_count())) if rehearsal else world
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(gpu)
@@ -278,7 +341,8 @@ def main():
     from of_dis_amd import distributed as odd
 
     binary, W, H, noc, mode, op, explicit, default_batch = cfg
-    B = args.batch or default_batch
+    first, stop, total, scaling = plan_shards(args, cfg, world, rank)
+    B = stop - first  # this rank's pairs per step
     p = params_of(od, cfg)
     p.verbosity = 0
     if world > 1:  # one configuration for every shard
@@ -295,7 +359,6 @@ def main():
         ctx.set_option(k, int(v))
 
     # synthetic inputs, resident in HBM before timing: this rank's shard of frames, distinct pairs tiled
-    first = odd.shard_range(B * world, rank, world)[0]
     nd = max(1, min(args.distinct, B))
     pairs = [od.synth_pair(W, H, noc, first + k, mode) for k in range(nd)]
     a = torch.empty((B, H, W, noc), dtype=torch.uint8, device=dev)
@@ -336,7 +399,7 @@ def main():
     # the timed pass's output of the distinct pairs, for the parity check below
     timed_out = out[:nd].cpu().numpy()
 
-    frames = B * world * args.steps
+    frames = total * args.steps
     mpix = W * H * frames / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -422,17 +485,20 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC,
-            "value": round(mpix, 2), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
+            "value": round(mpix, 2), "unit": "MPix/s", "n_gpus": n_devices, "ranks": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "frames_per_sec": round(frames / elapsed, 2),
-            "per_gpu_mpix_s": round(mpix / world, 2),
+            "per_gpu_mpix_s": round(mpix / n_devices, 2),
             "config": {"workload": f"{binary} {W}x{H} op-point {op}" + (f" ({explicit})" if explicit else "")
-                                   + f", {B} pairs/GPU/step", "name": args.config,
+                                   + (f", {total} pairs/step over {world} GPU(s)" if scaling == "strong"
+                                      else f", {B} pairs/GPU/step"), "name": args.config,
                        "width": W, "height": H, "channels": noc, "oppoint": op, "batch_per_gpu": B,
+                       "pairs_per_step": total,
                        "streams": streams_eff, "pairs_per_launch": chunk_eff,
                        "options": args.option,
-                       "parallelism": f"frame-sharded x{world}"},
+                       "parallelism": f"frame-sharded x{world}" + (" (rehearsal: ranks share the GPU)"
+                                                                   if rehearsal else "")},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,
             "latency": latency, "host_io": host_io, "kernels": kernels,
         }
@@ -440,6 +506,8 @@ def main():
             line["speedup_vs_cpu_1core"] = round(mpix / cpu["value"], 1)
             if cpu.get("value_all_cores"):
                 line["speedup_vs_cpu_all_cores"] = round(mpix / cpu["value_all_cores"], 1)
+            if cpu.get("value_node"):
+                line["speedup_vs_cpu_node"] = round(mpix / cpu["value_node"], 1)
         print(json.dumps(line))
     ctx.close()
     if world > 1:

@@ -11,6 +11,8 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <smmintrin.h>
+#include <time.h>
 
 /* ------------------------------------------------------------------ helpers */
 
@@ -25,28 +27,39 @@ static inline float ssemax(float a, float b) { return (a > b) ? a : b; }
 /* Eigen::DenseBase::sum() for a dynamic float vector with SSE packets (redux_impl,
  * LinearVectorizedTraversal, NoUnrolling; aligned start 0): two 4-lane packet accumulators over
  * packet pairs, res0+res1, odd trailing packet, predux = (l0+l2)+(l1+l3), scalar tail. */
+static float eigen_dot(const float *x, const float *b, int n);
+
 float ofo_eigen_sum(const float *x, int n) {
+  return eigen_dot(x, NULL, n);
+}
+
+/* Eigen's vectorised redux as the SSE build runs it, on 4-float packets (every _mm_add_ps / _mm_mul_ps lane
+ * rounds like the scalar operation: the same bits as the scalar restatement, at the reference's speed).
+ * b == NULL: sum of x; else the sum of the packet products x * b -- what Eigen evaluates for
+ * (x.array() * b.array()).sum(): the product packet is formed, then accumulated (no fused multiply-add). */
+static float eigen_dot(const float *x, const float *b, int n) {
   const int aligned = (n / 4) * 4, aligned2 = (n / 8) * 8;
+#define PK(i) (b ? _mm_mul_ps(_mm_loadu_ps(x + (i)), _mm_loadu_ps(b + (i))) : _mm_loadu_ps(x + (i)))
   if (aligned == 0) {
-    float r = x[0];
-    for (int i = 1; i < n; ++i) r = r + x[i];
+    float r = b ? x[0] * b[0] : x[0];
+    for (int i = 1; i < n; ++i) r = r + (b ? x[i] * b[i] : x[i]);
     return r;
   }
-  float r0[4], r1[4];
-  for (int l = 0; l < 4; ++l) r0[l] = x[l];
+  __m128 r0 = PK(0);
   if (aligned > 4) {
-    for (int l = 0; l < 4; ++l) r1[l] = x[4 + l];
-    for (int i = 8; i < aligned2; i += 8)
-      for (int l = 0; l < 4; ++l) {
-        r0[l] = r0[l] + x[i + l];
-        r1[l] = r1[l] + x[i + 4 + l];
-      }
-    for (int l = 0; l < 4; ++l) r0[l] = r0[l] + r1[l];
-    if (aligned > aligned2)
-      for (int l = 0; l < 4; ++l) r0[l] = r0[l] + x[aligned2 + l];
+    __m128 r1 = PK(4);
+    for (int i = 8; i < aligned2; i += 8) {
+      r0 = _mm_add_ps(r0, PK(i));
+      r1 = _mm_add_ps(r1, PK(i + 4));
+    }
+    r0 = _mm_add_ps(r0, r1);
+    if (aligned > aligned2) r0 = _mm_add_ps(r0, PK(aligned2));
   }
-  float res = (r0[0] + r0[2]) + (r0[1] + r0[3]);
-  for (int i = aligned; i < n; ++i) res = res + x[i];
+#undef PK
+  /* predux: (l0 + l2) + (l1 + l3) */
+  const __m128 t = _mm_add_ps(r0, _mm_movehl_ps(r0, r0));
+  float res = _mm_cvtss_f32(_mm_add_ss(t, _mm_shuffle_ps(t, t, 1)));
+  for (int i = aligned; i < n; ++i) res = res + (b ? x[i] * b[i] : x[i]);
   return res;
 }
 
@@ -294,20 +307,15 @@ static void patch_sample_bil(const cam_t *c, const opt_t *o, const float *img, c
   float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
   pos0 += c->pad;
   pos1 += c->pad;
-  const int p = o->p, noc = o->noc;
-  int k = 0;
+  const int p = o->p, noc = o->noc, pn = p * noc;
+  /* row pointers as in the reference (img_a / img_b = a - noc / img_c = a - row / img_d = c - noc): a patch
+   * row is pn contiguous floats, so the value loop is a plain elementwise expression */
   for (int iy = 0; iy < p; ++iy) {
-    int row = pos1 - p / 2 + iy;
-    for (int ix = 0; ix < p; ++ix) {
-      int col = pos0 - p / 2 + ix;
-      for (int ch = 0; ch < noc; ++ch, ++k) {
-        float A = img[((size_t)row * c->tmp_w + col) * noc + ch];
-        float B = img[((size_t)row * c->tmp_w + col - 1) * noc + ch];
-        float C = img[((size_t)(row - 1) * c->tmp_w + col) * noc + ch];
-        float D = img[((size_t)(row - 1) * c->tmp_w + col - 1) * noc + ch];
-        out[k] = w0 * A + w1 * B + w2 * C + w3 * D;
-      }
-    }
+    const int row = pos1 - p / 2 + iy;
+    const float *a = img + ((size_t)row * c->tmp_w + pos0 - p / 2) * noc;
+    const float *cc = a - (size_t)c->tmp_w * noc;
+    float *dst = out + (size_t)iy * pn;
+    for (int i = 0; i < pn; ++i) dst[i] = w0 * a[i] + w1 * a[i - noc] + w2 * cc[i] + w3 * cc[i - noc];
   }
   if (o->patnorm > 0) {
     float mean = ofo_eigen_sum(out, o->novals) / (float)o->novals;
@@ -341,7 +349,7 @@ typedef struct {
   float sq, sq_init, mares, mares_old;
   int cnt, converged;
   float H00, H01, H11;
-  float *tmp, *dxx, *dyy, *pdiff, *pweight;
+  float *tmp, *dxx, *dyy, *pdiff, *pweight, *scratch;
 } patch_t;
 
 /* OptimizeComputeErrImg (patch.cpp:275-295) */
@@ -354,11 +362,9 @@ static void patch_err(const cam_t *c, const opt_t *o, const float *im_b, patch_t
     P->sq = P->delta_p[0] * P->delta_p[0];
   if (P->cnt == 1) P->sq_init = P->sq;
   P->mares_old = P->mares;
-  /* lpNorm<1> = cwiseAbs().sum() */
-  float *ab = (float *)malloc(sizeof(float) * o->novals);
-  for (int i = 0; i < o->novals; ++i) ab[i] = fabsf(P->pweight[i]);
-  P->mares = ofo_eigen_sum(ab, o->novals) / (float)o->novals;
-  free(ab);
+  /* lpNorm<1> = cwiseAbs().sum() (into the pdiff-sized scratch, no allocation per iteration) */
+  for (int i = 0; i < o->novals; ++i) P->scratch[i] = fabsf(P->pweight[i]);
+  P->mares = ofo_eigen_sum(P->scratch, o->novals) / (float)o->novals;
   int keep = (P->cnt < o->max_iter) & (P->mares > o->res_thresh) &
              ((P->cnt < o->min_iter) | (P->sq / P->sq_init >= o->dp_thresh_sq)) &
              ((P->cnt < o->min_iter) | (P->mares / P->mares_old <= o->dr_thresh));
@@ -407,15 +413,11 @@ static void patch_run(const cam_t *c, const opt_t *o, const float *im_a, const f
     float mean = ofo_eigen_sum(P->tmp, nv) / (float)nv;
     for (int i = 0; i < nv; ++i) P->tmp[i] = P->tmp[i] - mean;
   }
-  /* ComputeHessian (patch.cpp:69-86) */
-  float *prod = (float *)malloc(sizeof(float) * nv);
-  for (int i = 0; i < nv; ++i) prod[i] = P->dxx[i] * P->dxx[i];
-  P->H00 = ofo_eigen_sum(prod, nv);
+  /* ComputeHessian (patch.cpp:69-86): (dxx.array() * dxx.array()).sum() etc. */
+  P->H00 = eigen_dot(P->dxx, P->dxx, nv);
   if (o->nop == 2) {
-    for (int i = 0; i < nv; ++i) prod[i] = P->dxx[i] * P->dyy[i];
-    P->H01 = ofo_eigen_sum(prod, nv);
-    for (int i = 0; i < nv; ++i) prod[i] = P->dyy[i] * P->dyy[i];
-    P->H11 = ofo_eigen_sum(prod, nv);
+    P->H01 = eigen_dot(P->dxx, P->dyy, nv);
+    P->H11 = eigen_dot(P->dyy, P->dyy, nv);
     if (P->H00 * P->H11 - P->H01 * P->H01 == 0.0f) {
       P->H00 = (float)((double)P->H00 + 1e-10);
       P->H11 = (float)((double)P->H11 + 1e-10);
@@ -445,11 +447,9 @@ static void patch_run(const cam_t *c, const opt_t *o, const float *im_a, const f
   /* OptimizeIter loop */
   while (!P->converged) {
     P->cnt++;
-    for (int i = 0; i < nv; ++i) prod[i] = P->dxx[i] * P->pdiff[i];
-    float b0 = ofo_eigen_sum(prod, nv);
+    float b0 = eigen_dot(P->dxx, P->pdiff, nv);  /* (dxx.array() * pdiff.array()).sum() (patch.cpp:170-171) */
     if (o->nop == 2) {
-      for (int i = 0; i < nv; ++i) prod[i] = P->dyy[i] * P->pdiff[i];
-      float b1 = ofo_eigen_sum(prod, nv);
+      float b1 = eigen_dot(P->dyy, P->pdiff, nv);
       llt2_solve(P->H00, P->H01, P->H11, b0, b1, &P->delta_p[0], &P->delta_p[1]);
       P->p_iter[0] = P->p_iter[0] - P->delta_p[0];
       P->p_iter[1] = P->p_iter[1] - P->delta_p[1];
@@ -471,7 +471,6 @@ static void patch_run(const cam_t *c, const opt_t *o, const float *im_a, const f
     }
     patch_err(c, o, im_b, P);
   }
-  free(prod);
 }
 
 /* ------------------------------------------------------------------ grid (patchgrid.cpp) */
@@ -1142,14 +1141,16 @@ static void fill_cam(const ofdis_params *p, int width, int height, int imgpaddin
 static patch_t *run_grid(const cam_t *c, const opt_t *o, const grid_t *g, const float *im_a, const float *im_a_dx,
                          const float *im_a_dy, const float *im_b, const float *prev, float **store_out) {
   patch_t *pats = (patch_t *)calloc(g->nopatches, sizeof(patch_t));
-  float *store = (float *)malloc(sizeof(float) * (size_t)g->nopatches * o->novals * 5);
+  /* five arrays per patch + one scratch array shared by the grid's (sequential) patches */
+  float *store = (float *)malloc(sizeof(float) * ((size_t)g->nopatches * o->novals * 5 + o->novals));
+  float *scratch = store + (size_t)g->nopatches * o->novals * 5;
   for (int x = 0, i = 0; x < g->nopw; ++x)
     for (int y = 0; y < g->noph; ++y, ++i) {
       pats[i].pt_ref[0] = (float)(x * g->steps + g->offw);
       pats[i].pt_ref[1] = (float)(y * g->steps + g->offh);
       float *s = store + (size_t)i * o->novals * 5;
       pats[i].tmp = s; pats[i].dxx = s + o->novals; pats[i].dyy = s + 2 * o->novals;
-      pats[i].pdiff = s + 3 * o->novals; pats[i].pweight = s + 4 * o->novals;
+      pats[i].pdiff = s + 3 * o->novals; pats[i].pweight = s + 4 * o->novals; pats[i].scratch = scratch;
     }
   for (int i = 0; i < g->nopatches; ++i) {
     float pin[2] = {0.0f, 0.0f};
@@ -1333,8 +1334,23 @@ int ofo_run_u8(const uint8_t *img_a, const uint8_t *img_b, int width, int height
   return ofo_run_u8_init(img_a, img_b, NULL, width, height, p, flow_out, cap_dis, cap_tv);
 }
 
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
 int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *init, int width, int height,
                     const ofdis_params *p, float *flow_out, float *const *cap_dis, float *const *cap_tv) {
+  return ofo_run_u8_stages(img_a, img_b, init, width, height, p, flow_out, cap_dis, cap_tv, NULL);
+}
+
+/* The same with the wall time of each stage (CPU-baseline breakdown): stage_s[0] divisibility padding,
+ * [1] pyramid + gradients (both frames), [2] OFClass, [3] upsample + crop. */
+int ofo_run_u8_stages(const uint8_t *img_a, const uint8_t *img_b, const float *init, int width, int height,
+                      const ofdis_params *p, float *flow_out, float *const *cap_dis, float *const *cap_tv,
+                      double *stage_s) {
+  double t0 = stage_s ? now_s() : 0.0;
   const int noc = p->noc, nop = p->mode == OFDIS_MODE_OF ? 2 : 1, pad = p->p_samp_s;
   int padw, padh;
   ofo_divisibility_pad(width, height, p->sc_f + (init ? 1 : 0), &padw, &padh);  /* run_dense.cpp:302 */
@@ -1360,8 +1376,18 @@ int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *ini
     size_t n = (size_t)((Wp >> s) + 2 * pad) * ((Hp >> s) + 2 * pad) * noc;
     for (int k = 0; k < 6; ++k) pyr[k][s] = (float *)malloc(sizeof(float) * n);
   }
+  if (stage_s) {
+    const double t = now_s();
+    stage_s[0] = t - t0;
+    t0 = t;
+  }
   rc = ofo_build_pyramid_ex(pa, Wp, Hp, noc, p->sc_f, p->sc_l, pad, p->gradmag, pyr[0], pyr[1], pyr[2]);
   if (!rc) rc = ofo_build_pyramid_ex(pb, Wp, Hp, noc, p->sc_f, p->sc_l, pad, p->gradmag, pyr[3], pyr[4], pyr[5]);
+  if (stage_s) {
+    const double t = now_s();
+    stage_s[1] = t - t0;
+    t0 = t;
+  }
   const int wl = Wp >> p->sc_l, hl = Hp >> p->sc_l;
   float *fl = (float *)malloc(sizeof(float) * (size_t)wl * hl * nop);
   float *ini = NULL;
@@ -1373,7 +1399,13 @@ int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *ini
     rc = ofo_oflow((const float *const *)pyr[0], (const float *const *)pyr[1], (const float *const *)pyr[2],
                    (const float *const *)pyr[3], (const float *const *)pyr[4], (const float *const *)pyr[5], pad, fl,
                    ini, Wp, Hp, p, cap_dis, cap_tv);
+  if (stage_s) {
+    const double t = now_s();
+    stage_s[2] = t - t0;
+    t0 = t;
+  }
   if (!rc) rc = ofo_upsample_crop(fl, wl, hl, nop, p->sc_l, padw, padh, width, height, flow_out);
+  if (stage_s) stage_s[3] = now_s() - t0;
   free(fl);
   free(ini);
   for (int s = p->sc_l; s <= p->sc_f; ++s)

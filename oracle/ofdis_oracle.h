@@ -60,6 +60,9 @@ int ofo_run_u8(const uint8_t *img_a, const uint8_t *img_b, int width, int height
  * divisibility 2^(sc_f+1), replicate pad, x 2^-(sc_f+1), INTER_AREA down to the coarsest scale - 1). */
 int ofo_run_u8_init(const uint8_t *img_a, const uint8_t *img_b, const float *init, int width, int height,
                     const ofdis_params *p, float *flow_out, float *const *cap_dis, float *const *cap_tv);
+int ofo_run_u8_stages(const uint8_t *img_a, const uint8_t *img_b, const float *init, int width, int height,
+                      const ofdis_params *p, float *flow_out, float *const *cap_dis, float *const *cap_tv,
+                      double *stage_s);
 void ofo_init_flow_area(const float *init, int width, int height, int nop, int padw, int padh, int sc_f,
                         float *out);
 

@@ -70,6 +70,8 @@ def lib():
                                         C.c_int, C.c_int, _f32p]
         L.ofo_run_u8.argtypes = [_u8p, _u8p, C.c_int, C.c_int, C.POINTER(Params), _f32p, vp, vp]
         L.ofo_run_u8_init.argtypes = [_u8p, _u8p, vp, C.c_int, C.c_int, C.POINTER(Params), _f32p, vp, vp]
+        L.ofo_run_u8_stages.argtypes = [_u8p, _u8p, vp, C.c_int, C.c_int, C.POINTER(Params), _f32p, vp, vp,
+                                        C.POINTER(C.c_double)]
         L.ofo_init_flow_area.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _f32p]
         L.ofo_refine_level.argtypes = [_f32p, _f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Params), _f32p]
         L.ofo_image_warp.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, C.c_int, C.c_int]
@@ -165,6 +167,18 @@ def run_u8(a: np.ndarray, b: np.ndarray, p: Params, capture=False, init=None):
     if rc != 0:
         raise RuntimeError(f"ofo_run_u8 failed: {rc}")
     return (out, cap_d, cap_t) if capture else out
+
+
+def run_u8_stages(a: np.ndarray, b: np.ndarray, p: Params):
+    """run_u8 plus the wall time (s) of its stages: pad, pyramid (both frames), OFClass, upsample + crop."""
+    h, w = a.shape[:2]
+    out = np.zeros((h, w, nop_of(p)), np.float32)
+    st = (C.c_double * 4)()
+    rc = lib().ofo_run_u8_stages(np.ascontiguousarray(a, np.uint8), np.ascontiguousarray(b, np.uint8), None, w, h,
+                                 C.byref(p), out, None, None, st)
+    if rc != 0:
+        raise RuntimeError(f"ofo_run_u8_stages failed: {rc}")
+    return out, {"pad": st[0], "pyramid": st[1], "ofclass": st[2], "upsample": st[3]}
 
 
 # --------------------------------------------------------------------------- reference FDF1.0.1 (_ref)

@@ -73,7 +73,7 @@ def test_gloo_world2_control_collectives():
 def test_bench_launcher_dry_run_two_ranks():
     """`bench.py --gpus 2` outside torchrun re-launches itself as 2 ranks (a child torch.distributed.run
     job); with --dry-run the ranks run on gloo without a GPU and rank 0 reports n_gpus 2 and the disjoint
-    shards of config D (32 pairs per GPU)."""
+    shards of config D: BASELINE configs[3]'s 256-pair batch split over the ranks (strong scaling)."""
     import json
     import subprocess
     import sys
@@ -85,9 +85,28 @@ def test_bench_launcher_dry_run_two_ranks():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["dry_run"]
-    assert d["shards"] == [[0, 32], [32, 64]]
-    assert d["frames"] == 64
+    assert d["n_gpus"] == 2 and d["dry_run"] and d["scaling"] == "strong"
+    assert d["shards"] == [[0, 128], [128, 256]]
+    assert d["frames"] == 256
+
+
+@pytest.mark.parametrize("argv,world,shards,scaling", [
+    (["--config", "B", "--batch", "4"], 2, [[0, 4], [4, 8]], "weak"),          # weak: --batch per GPU
+    (["--config", "B", "--total", "10"], 3, [[0, 4], [4, 7], [7, 10]], "strong"),  # ragged strong shards
+    (["--config", "D"], 4, [[0, 64], [64, 128], [128, 192], [192, 256]], "strong"),
+])
+def test_bench_shard_plans(argv, world, shards, scaling):
+    """Shard plans of bench.py at several world sizes: every pair of the step owned by exactly one rank."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run"] + argv,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["shards"] == shards and d["scaling"] == scaling and d["frames"] == shards[-1][1]
 
 
 def test_bench_rejects_world_mismatch():
