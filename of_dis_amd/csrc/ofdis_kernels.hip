@@ -2624,6 +2624,15 @@ __device__ __forceinline__ float dpp_from_next_lane(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
 }
 
+#ifdef OFDIS_SOR_PROBE
+// Step-timing probe of the sweep-per-wave SOR (a separate build, tools/sor_probe.py; never in libofdis.so):
+// frame 0 of every launch records, per wave and wavefront step, the shader clock (s_memtime) after the
+// previous step's barrier, after the step's LDS reads have arrived, after its update is written to LDS, and
+// after the step's barrier.  Layout: [0] launch counter, then [launch < 64][wave < 16][step < 1024][4].
+__device__ unsigned *g_sor_probe;
+__device__ __forceinline__ unsigned probe_clock() { return (unsigned)__builtin_amdgcn_s_memtime(); }
+#endif
+
 // Per-pixel data that sweep 0 loads / derives and sweeps 1..S-1 reuse 2s steps later (register ring).
 struct SorPix {
   float i11, i12, i22, b1, b2, hl, hr, vv, vt;
@@ -3109,6 +3118,9 @@ struct SorLane {
   int w, h, y, s, lim, rmax, hplane;
   bool border[R], notop[R];
   float omega;
+#ifdef OFDIS_SOR_PROBE
+  unsigned *probe = nullptr;  // this wave's [step][4] records (frame 0 only)
+#endif
 
   __device__ __forceinline__ void load(int t, Ld &B) {
     const int d = t - 2 * s;
@@ -3139,6 +3151,10 @@ struct SorLane {
   template <int Q>
   __device__ __forceinline__ void step(const int t) {
     constexpr int m0 = Q % 3, m1 = (Q + 2) % 3;  // ring slots of steps t, t-1
+#ifdef OFDIS_SOR_PROBE
+    const unsigned pt0 = probe_clock();
+    unsigned pt1 = 0, pt2 = 0;
+#endif
     Ld &B = buf<Q % NB>();
     const Ld &Bn = buf<(Q + 1) % NB>();
     load(t + PD, buf<(Q + PD) % NB>());  // beyond the last step too: sor_row keeps every address in the plane
@@ -3189,6 +3205,13 @@ struct SorLane {
       }
       f2v nw;
       float vv;
+#ifdef OFDIS_SOR_PROBE
+      {  // the step's LDS operands arrived (a use of each forces the wait): take the clock
+        const float dep = ((c0.x + c1.x) + (tp.x + tsv)) + (rgt.x + bt.x);
+        asm volatile("; probe use %0" ::"v"(dep) : "memory");
+        pt1 = probe_clock();
+      }
+#endif
       if (MODE == 0) {
         const float hr = c1.z;
         vv = c1.w;
@@ -3229,7 +3252,15 @@ struct SorLane {
       }
       pp[r] = nw;
     }
+#ifdef OFDIS_SOR_PROBE
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pt2 = probe_clock();
+#endif
     __syncthreads();
+#ifdef OFDIS_SOR_PROBE
+    if (probe && (threadIdx.x & 63) == 0 && t < 1024)
+      *reinterpret_cast<uint4 *>(probe + 4 * t) = make_uint4(pt0, pt1, pt2, probe_clock());
+#endif
   }
 
   template <int J>
@@ -3299,6 +3330,11 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
   if (CRN > 0)
     for (int i = threadIdx.x; i < 6 * CW * CRN; i += blockDim.x) crr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
+#ifdef OFDIS_SOR_PROBE
+  __shared__ unsigned probe_slot;
+  if (threadIdx.x == 0 && frame == 0) probe_slot = g_sor_probe ? atomicAdd(g_sor_probe, 1u) : 64u;
+  __syncthreads();
+#endif
   const long fo = (long)frame * a.sp;
   constexpr int U = SorLane<S, MODE, 0, NB, CRN, R>::U;
   const int T = ((a.w - 1) + (a.h - 1) + 2 * (S - 1) + 1 + U - 1) / U * U;
@@ -3326,6 +3362,10 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
       st.border[r] = yr == 0 || yr >= a.h - 1;
     }
     st.omega = a.omega;
+#ifdef OFDIS_SOR_PROBE
+    if (frame == 0 && probe_slot < 64u && wid < 16)
+      st.probe = g_sor_probe + 4 + ((size_t)probe_slot * 16 + wid) * 1024 * 4;
+#endif
     st.run(T, y0, ymax);
   };
   if (s == 0) {
@@ -3933,3 +3973,10 @@ void launch_upsample(const UpArgs &a, hipStream_t s) {
 }
 
 }  // namespace ofdis
+
+#ifdef OFDIS_SOR_PROBE
+// Probe build only: point the SOR step probe at a device buffer of 4 + 64 * 16 * 1024 * 4 uints (NULL: off).
+extern "C" int ofdis_sor_probe_attach(void *dev_buffer) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(ofdis::g_sor_probe), &dev_buffer, sizeof(dev_buffer)) == hipSuccess ? 0 : -1;
+}
+#endif
