@@ -69,6 +69,7 @@ struct PatchArgs {
   int wave_per_patch;                         // 1: force the one-wave-per-patch kernel (A/B testing)
   int generic;                                // 1: force the any-shape kernel k_patchg (parity testing)
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
+  int quad;                                   // four lanes per patch (k_patchq) where the shape has that form
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;

@@ -1527,6 +1527,337 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   if (live && s8 < NOP) a.p_iter[gp * NOP + s8] = s8 == 0 ? p0 : p1;
 }
 
+// ------------------------------------------------------------------ DIS patches, four lanes per patch (round 3)
+// k_patchw replicates the per-patch scalar work of an iteration (bilinear weights, the LLT solve's correctly
+// rounded divisions, the stopping tests, the three DPP reductions) on all eight lanes of a patch: at p = 12
+// gray that is ~40 % of the VALU instructions of an iteration.  Here four lanes share a patch (sixteen patches
+// per wave), so the same per-patch work is spread over twice the values.  Lane s holds Eigen's packet slots s
+// and s + 4 -- the values v = s + 8k and v + 4 of every 8-value block k -- as one register pair, so every
+// per-value operation is packed fp32 on the pair (v, v + 4) INCLUDING the Eigen chains: the pair of slot
+// accumulators (acc_s, acc_{s+4}) takes one v_pk_add_f32 per block, and res0 + res1 is the pair's own
+// .x + .y; then (l0 + l2) + (l1 + l3) by two DPP butterflies inside the quad.  Same additions, same order:
+// bit-identical to k_patchw (and to the oracle).  With p * noc a multiple of 4 every tap of lane s sits at
+// s + (a compile-time offset) in the window tile, so a pair's taps are one ds_read2_b32 off a single base
+// address.  Shapes: p * p * noc a multiple of 8 with the pairs' registers in budget (gray p = 8 / 12).
+template <int P, int NOC>
+struct QuadShape {
+  static constexpr int NV = P * P * NOC;
+  static constexpr int ROWV = P * NOC;
+  static constexpr int K = NV / 8;           // 8-value blocks: lane s holds pair k = (s + 8k, s + 4 + 8k)
+  static constexpr int WR = (P + 1) * NOC;   // window row (floats)
+  static constexpr int Q4 = (WR + 3) / 4;    // 16-byte loads per window row
+  // LDS row stride (floats): the row rounded up to an even count only (8-byte stores): at RS = Q4 * 4 the
+  // 64 windows of a workgroup took 53 KB and three workgroups did not fit a CU (the quad form then ran at
+  // two thirds of its register occupancy: no faster than the eight-lane form at p = 12)
+  static constexpr int RS = (WR + 1) & ~1;
+  // windows at a stride of 4 (mod 8) dwords: the 8 patches of a 32-lane half then start on 8 distinct 4-bank
+  // groups, and their lanes' 4 consecutive dwords never share a bank
+  static constexpr int WIN = (P + 1) * RS + ((4 - ((P + 1) * RS) % 8) + 8) % 8;
+  static constexpr int NQ = (P + 1) * Q4;    // 16-byte loads per window
+  static constexpr int LPL = (NQ + 3) / 4;   // ... per lane
+  static_assert(NV % 8 == 0 && ROWV % 4 == 0, "quad form: p * noc a multiple of 4, p * p * noc of 8");
+  // window offset (floats, lane s excluded) of the D tap of value 8k + h (h = 0 or 4)
+  static constexpr int dtap(int k, int h) { return ((8 * k + h) / ROWV) * RS + (8 * k + h) % ROWV; }
+  // frame offset (floats, lane s excluded) of value 8k + h relative to the patch's top-left pixel
+  static constexpr int frow(int k, int h) { return (8 * k + h) / ROWV; }
+  static constexpr int fcol(int k, int h) { return (8 * k + h) % ROWV; }
+};
+
+// Eigen's total of the quad's slot pairs: res0 + res1 (the pair), then (l0 + l2) + (l1 + l3).
+__device__ __forceinline__ float quad_total(f2p acc) {
+  float r = acc.x + acc.y;
+  r = r + grp_xor2(r);
+  return r + grp_xor1(r);
+}
+
+template <int NOP, int P, int NOC, int MINW, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchq(PatchArgs a) {
+  const uint3 xb = xcd_block();
+  using S = QuadShape<P, NOC>;
+  constexpr int K = S::K, RS = S::RS;
+  extern __shared__ __attribute__((aligned(16))) float win_all[];
+  const LevelGeom &g = a.g;
+  const int s4 = threadIdx.x & 3;
+  const long gp = (long)xb.x * 64 + (threadIdx.x >> 2);
+  const bool live = gp < (long)a.n * g.npatch;
+  const long gq = live ? gp : 0;
+  const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
+  const int pxi = ip / g.noph, pyi = ip % g.noph;
+  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+  const long fs = (long)g.W * g.H * NOC;
+  const int W = g.W;
+  constexpr float inv_n = 1.0f / (float)S::NV;
+  constexpr bool pow2 = (S::NV & (S::NV - 1)) == 0;
+  auto div_n = [&](float x) {
+    if constexpr (pow2)
+      return x * inv_n;
+    else
+      return div_by_const<S::NV>(x);
+  };
+  float *win = win_all + (threadIdx.x >> 2) * S::WIN;
+  // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
+  f2p tmp2[K], gx2[K], gy2[NOP == 2 ? K : 1];
+  {
+    const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
+    const long base = ((long)(py - P / 2) * W + (px - P / 2)) * NOC + s4;
+    const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
+    const long rw = (long)W * NOC;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const long o0 = S::frow(k, 0) * rw + S::fcol(k, 0), o1 = S::frow(k, 4) * rw + S::fcol(k, 4);
+      tmp2[k] = f2p{A[o0], A[o1]};
+      gx2[k] = f2p{DX[o0], DX[o1]};
+      if constexpr (NOP == 2) gy2[k] = f2p{DY[o0], DY[o1]};
+    }
+  }
+  if (a.patnorm > 0) {
+    f2p m = tmp2[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) m = m + tmp2[k];
+    const float mean = div_n(quad_total(m));
+#pragma unroll
+    for (int k = 0; k < K; ++k) tmp2[k] = tmp2[k] - mean;
+  }
+  // ---- ComputeHessian (patch.cpp:69-86)
+  float H00, H01 = 0.0f, H11 = 0.0f;
+  {
+    f2p h0 = gx2[0] * gx2[0], h1 = {0.0f, 0.0f}, h2 = {0.0f, 0.0f};
+    if constexpr (NOP == 2) {
+      h1 = gx2[0] * gy2[0];
+      h2 = gy2[0] * gy2[0];
+    }
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+      h0 = h0 + gx2[k] * gx2[k];
+      if constexpr (NOP == 2) {
+        h1 = h1 + gx2[k] * gy2[k];
+        h2 = h2 + gy2[k] * gy2[k];
+      }
+    }
+    H00 = quad_total(h0);
+    if (NOP == 2) {
+      H01 = quad_total(h1);
+      H11 = quad_total(h2);
+      if (H00 * H11 - H01 * H01 == 0.0f) {
+        H00 = (float)((double)H00 + 1e-10);
+        H11 = (float)((double)H11 + 1e-10);
+      }
+    } else if (H00 == 0.0f) {
+      H00 = (float)((double)H00 + 1e-10);
+    }
+  }
+  const Llt2 fac = llt2_factor(H00, H01, H11);
+  const float fac1 = llt1_factor(H00);
+  if (a.stage == 1) {  // timing diagnostic "pconst"
+    if (live && s4 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp2[K - 1].y;
+    return;
+  }
+  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
+  float pin0 = 0.0f, pin1 = 0.0f;
+  if (a.prev) {
+    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
+    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
+    pin0 = pv[0] * 2;
+    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  if (a.stage == 2) {  // "pconst + pinit"
+    if (live && s4 == 0)
+      a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp2[K - 1].y + pin0 + pin1;
+    return;
+  }
+  const float *Bimg = a.img_b + f * fs;
+  // ---- OptimizeStart (patch.cpp:117-154)
+  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
+  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
+  const float st0 = pt0, st1 = pt1;
+  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
+  int cnt = 0;
+  bool converged = false;
+  float b0 = 0.0f, b1 = 0.0f;
+  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  int lpos0 = -0x7fffffff, lpos1 = 0;
+  const unsigned wb = (unsigned)(uintptr_t)win + 4u * (unsigned)s4;  // lane s's taps: wb + 4 * (constant)
+  // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
+  auto evaluate = [&](float &r0, float *out, auto store_t) {
+    constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
+    const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
+    const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
+    const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
+    const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
+    const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+    const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
+    if (__builtin_amdgcn_ballot_w64(pos0 != lpos0 || pos1 != lpos1) != 0) {
+      lpos0 = pos0;
+      lpos1 = pos1;
+      wave_lds_sync();
+      // every load of the tile in flight at once: one round trip to L2 per reload (the 8-lane kernel's count)
+      constexpr int NB = S::LPL;
+#pragma unroll
+      for (int j0 = 0; j0 < S::LPL; j0 += NB) {
+        float4_u t[NB];
+        int lo[NB];
+#pragma unroll
+        for (int j = j0; j < j0 + NB && j < S::LPL; ++j) {
+          const int e = s4 + 4 * j, e2 = e < S::NQ ? e : S::NQ - 1;
+          const int row = e2 / S::Q4, c4 = e2 % S::Q4;
+          lo[j - j0] = row * RS + c4 * 4;
+          t[j - j0] = *reinterpret_cast<const float4_u *>(Q + row * W * NOC + c4 * 4);
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + NB && j < S::LPL; ++j) {  // two 8-byte stores: columns < RS only
+          const int e = s4 + 4 * j;
+          if (e < S::NQ) {
+            f2p *d = reinterpret_cast<f2p *>(win + lo[j - j0]);
+            d[0] = f2p{t[j - j0].x, t[j - j0].y};
+            if (4 * (e % S::Q4) + 2 < RS) d[1] = f2p{t[j - j0].z, t[j - j0].w};
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+    // taps of pair k: one ds_read2_b32 per tap (D, C, B, A), the next pair's reads in flight
+    f2p pd2[K], q[2][4];
+    auto issue = [&](auto kc) {
+      constexpr int k = decltype(kc)::value, c0 = S::dtap(k, 0), c1 = S::dtap(k, 4);
+      constexpr int mx = (c0 > c1 ? c0 : c1) + RS + NOC;
+      constexpr int b = mx <= 255 ? 0 : (c0 < c1 ? c0 : c1);  // else part of the offset goes into the address
+      const unsigned ad = wb + 4u * (unsigned)b;
+      q[k & 1][0] = lds_read2<c0 - b, c1 - b>(ad);                        // D
+      q[k & 1][1] = lds_read2<c0 - b + NOC, c1 - b + NOC>(ad);            // C
+      q[k & 1][2] = lds_read2<c0 - b + RS, c1 - b + RS>(ad);              // B
+      q[k & 1][3] = lds_read2<c0 - b + RS + NOC, c1 - b + RS + NOC>(ad);  // A
+    };
+    issue(std::integral_constant<int, 0>{});
+    f2p macc;
+    static_for<K>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k + 1 < K) {
+        issue(std::integral_constant<int, k + 1>{});
+        lds_wait<4>();
+      } else {
+        lds_wait<0>();
+      }
+      f2p *t = q[k & 1];
+      static_for<4>([&](auto ic) { reg_fence(t[decltype(ic)::value]); });
+      f2p x = t[3] * w0 + t[2] * w1;
+      x = x + t[1] * w2;
+      x = x + t[0] * w3;
+      pd2[k] = x;
+      if constexpr (k == 0) macc = x;
+      else macc = macc + x;
+    });
+    const float mean = a.patnorm > 0 ? div_n(quad_total(macc)) : 0.0f;
+    float abl = 0.0f, abh = 0.0f;
+    f2p ex, ey;
+    static_for<K>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const f2p d = (pd2[k] - mean) - tmp2[k];
+      f2p wv, e;
+      if (COST == 0) {
+        wv = d;
+        e = d;
+      } else {
+        float w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float dh = h ? d.y : d.x;
+          w[h] = COST == 1 ? sqrt_nonneg(fabsf(dh))
+                           : sqrt_nonneg((sqrt_nonneg(1.0f + (dh * dh) / 25.0f) - 1.0f) * 50.0f);
+        }
+        wv = f2p{w[0], w[1]};
+        e = f2p{copysignf(w[0], d.x), copysignf(w[1], d.y)};
+      }
+      if constexpr (STORE == 0) {
+        const f2p qx = gx2[k] * e;
+        f2p qy;
+        if constexpr (NOP == 2) qy = gy2[k] * e;
+        if constexpr (k == 0) {
+          abl = fabsf(wv.x);
+          abh = fabsf(wv.y);
+          ex = qx;
+          if (NOP == 2) ey = qy;
+        } else {
+          abl = abl + fabsf(wv.x);
+          abh = abh + fabsf(wv.y);
+          // two scalar adds with |.| source modifiers; left to itself the compiler packs this chain pair
+          // (v_pk_add_f32 after two v_and_b32: three instructions instead of two)
+          asm volatile("" : "+v"(abl), "+v"(abh));
+          ex = ex + qx;
+          if (NOP == 2) ey = ey + qy;
+        }
+      } else {
+        const float wl = COST == 0 ? fabsf(wv.x) : wv.x, wh = COST == 0 ? fabsf(wv.y) : wv.y;
+        out[s4 + 8 * k] = wl;
+        out[s4 + 4 + 8 * k] = wh;
+      }
+    });
+    if constexpr (STORE == 0) {
+      r0 = quad_total(f2p{abl, abh});
+      b0 = quad_total(ex);
+      if (NOP == 2) b1 = quad_total(ey);
+    }
+  };
+  float *pwo = a.pweight + gq * S::NV;
+  bool start_oob = false, first = true;
+  converged = !live;
+  if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      pwo[s4 + 8 * k] = 0.0f;
+      pwo[s4 + 4 + 8 * k] = 0.0f;
+    }
+    converged = true;
+    start_oob = true;
+  } else {
+    mares = 1e5f;
+  }
+  for (;;) {
+    if (__builtin_amdgcn_ballot_w64(!converged) == 0) break;
+    if (!converged) {
+      if (!first) {
+        ++cnt;
+        if (NOP == 2) {
+          llt2_solve(fac, b0, b1, d0, d1);
+          p0 = p0 - d0;
+          p1 = p1 - d1;
+        } else {
+          d0 = llt1_solve(fac1, b0);
+          p0 = p0 - d0;
+          p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+        }
+        pt0 = ptr0 + p0;
+        if (NOP == 2) pt1 = ptr1 + p1;
+        const float ex = st0 - pt0, ey = st1 - pt1;
+        if (ex * ex + ey * ey > a.outlier_sq || oob(pt0, pt1)) {
+          p0 = pin0;
+          p1 = pin1;
+          pt0 = ptr0 + p0;
+          if (NOP == 2) pt1 = ptr1 + p1;
+          converged = true;
+        }
+      }
+      float r0 = 0.0f;
+      evaluate(r0, nullptr, std::integral_constant<int, 0>());
+      // OptimizeComputeErrImg (patch.cpp:275-295)
+      sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+      if (cnt == 1) sq_init = sq;
+      mares_old = mares;
+      mares = div_n(r0);
+      bool rates = true;
+      if (__builtin_amdgcn_ballot_w64(cnt >= a.min_iter) != 0)
+        rates = (cnt < a.min_iter) | ((sq / sq_init >= a.dp_thresh_sq) & (mares / mares_old <= a.dr_thresh));
+      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) & rates;
+      if (!keep) converged = true;
+    }
+    first = false;
+  }
+  if (live && !start_oob) {
+    float r0;
+    evaluate(r0, pwo, std::integral_constant<int, 1>());
+  }
+  if (live && s4 < NOP) a.p_iter[gp * NOP + s4] = s4 == 0 ? p0 : p1;
+}
+
 // ------------------------------------------------------------------------------------------------ aggregation
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -3728,7 +4059,27 @@ static void patchw(const PatchArgs &a, hipStream_t s) {
     default: k_patchw<2, P, NOC, MINW2, 2><<<grid, 256, lds, s>>>(a); return;
   }
 }
+template <int P, int NOC, int MINW1, int MINW2>
+static void patchq(const PatchArgs &a, hipStream_t s) {
+  const long patches = (long)a.n * a.g.npatch;
+  const size_t lds = sizeof(float) * 64 * QuadShape<P, NOC>::WIN;
+  const dim3 grid(ceil_div(patches, 64));
+  switch (a.costfct * 2 + (a.nop == 2 ? 1 : 0)) {
+    case 0: k_patchq<1, P, NOC, MINW1, 0><<<grid, 256, lds, s>>>(a); return;
+    case 1: k_patchq<2, P, NOC, MINW2, 0><<<grid, 256, lds, s>>>(a); return;
+    case 2: k_patchq<1, P, NOC, MINW1, 1><<<grid, 256, lds, s>>>(a); return;
+    case 3: k_patchq<2, P, NOC, MINW2, 1><<<grid, 256, lds, s>>>(a); return;
+    case 4: k_patchq<1, P, NOC, MINW1, 2><<<grid, 256, lds, s>>>(a); return;
+    default: k_patchq<2, P, NOC, MINW2, 2><<<grid, 256, lds, s>>>(a); return;
+  }
+}
 void launch_patch(const PatchArgs &a, hipStream_t s) {
+  if (a.window && a.quad && !a.wave_per_patch && !a.generic) {  // four lanes per patch: gray p = 8 / 12
+    switch (a.p * 4 + a.noc) {
+      case 8 * 4 + 1: patchq<8, 1, 4, 3>(a, s); return;
+      case 12 * 4 + 1: patchq<12, 1, 3, 2>(a, s); return;
+    }
+  }
   if (a.window && !a.wave_per_patch && !a.generic) {  // LDS-windowed eight-lane form for the shapes of the op-points
     switch (a.p * 4 + a.noc) {
       case 8 * 4 + 1: patchw<8, 1, 4, 4>(a, s); return;

@@ -93,6 +93,7 @@ struct ofdis_context {
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
+  int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
@@ -390,6 +391,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.camlr = 0;
     pa.wave_per_patch = c->opt_wave_per_patch;
     pa.window = c->opt_patch_window;
+    pa.quad = c->opt_patch_quad;
     pa.generic = c->opt_patch_generic;
     pa.g = g;
     if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
@@ -1213,7 +1215,8 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 1},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
-      {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1},
+      {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
+      {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1},
       {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };

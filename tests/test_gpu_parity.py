@@ -48,6 +48,9 @@ CASES = [
     (173, 97, 1, 1, 2, {}),                                   # divisibility padding on both axes
     (192, 128, 3, 1, 3, {}),                                  # RGB op3 (p = 12, L2 as defined)
     (192, 128, 3, 1, 3, {"costfct": 1}),                      # RGB op3 with the L1 cost of BASELINE config C
+    (192, 128, 1, 1, 3, {}),                                  # gray op3: p = 12 flow on four lanes per patch
+    (192, 128, 1, 1, 4, {"costfct": 1, "max_iter": 16, "min_iter": 16}),  # ... L1 cost
+    (240, 120, 1, 2, 4, {"costfct": 2, "max_iter": 16, "min_iter": 16}),  # depth p = 12, pseudo-Huber
     (160, 120, 1, 1, 2, {"costfct": 2}),                      # pseudo-Huber
     (160, 120, 1, 1, 2, {"min_iter": 2, "dp_thresh": 0.3, "dr_thresh": 0.9}),  # early stopping active
     (160, 120, 1, 1, 2, {"patnorm": 0, "tv_innerit": 2, "tv_solverit": 4, "tv_sor": 1.3}),
@@ -113,6 +116,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("smsys2d", 0, 2),         # tall levels: two launches instead of the 2-D tiled fused one (auto: on below 512 pairs)
     ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
     ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
+    ("patch_quad", 0, 1),      # gray p = 8 / 12 on eight lanes per patch (k_patchw) instead of four (k_patchq)
 ]
 
 
