@@ -2477,19 +2477,28 @@ __device__ __forceinline__ void data_de(int noc, long plane, float u, float m, c
 
 // s of one pixel from (wx, du, wy, dv) of the pixel and its clamped 4-neighbourhood (centre, left, right,
 // up, down): the arithmetic of compute_smoothness (opticalflow_aux.c:138-160) on uu = wx + du.
+// uu (and vv) of one pixel: wx on the first inner iteration, else wx + du (DE: clamped to the camera side)
+template <int NOP>
+__device__ __forceinline__ float smooth_uu(const TvArgs &a, bool first, float wx, float du) {
+  if (NOP == 2) return first ? wx : wx + du;
+  return first ? wx : (a.camlr == 0 ? ssemin(wx + du, 0.0f) : ssemax(wx + du, 0.0f));
+}
+template <int NOP>
+__device__ __forceinline__ float smooth_from_uu(const TvArgs &a, const float (&uu5)[5], const float (&vv5)[5]);
 template <int NOP>
 __device__ __forceinline__ float smooth_compute(const TvArgs &a, bool first, const float (&wx5)[5],
                                              const float (&du5)[5], const float (&wy5)[5], const float (&dv5)[5]) {
   float uu5[5], vv5[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    if (NOP == 2) {
-      uu5[i] = first ? wx5[i] : wx5[i] + du5[i];
-      vv5[i] = first ? wy5[i] : wy5[i] + dv5[i];
-    } else {
-      uu5[i] = first ? wx5[i] : (a.camlr == 0 ? ssemin(wx5[i] + du5[i], 0.0f) : ssemax(wx5[i] + du5[i], 0.0f));
-    }
+    uu5[i] = smooth_uu<NOP>(a, first, wx5[i], du5[i]);
+    vv5[i] = NOP == 2 ? smooth_uu<2>(a, first, wy5[i], dv5[i]) : 0.0f;
   }
+  return smooth_from_uu<NOP>(a, uu5, vv5);
+}
+// the rest of compute_smoothness from the clamped 5-neighbourhood of uu (centre, left, right, up, down)
+template <int NOP>
+__device__ __forceinline__ float smooth_from_uu(const TvArgs &a, const float (&uu5)[5], const float (&vv5)[5]) {
   const float uc = uu5[0];
   const float ux = kK3[0] * uu5[1] + (kK3[1] * uc + kK3[2] * uu5[2]);
   const float uy = kK3[0] * uu5[3] + (kK3[1] * uc + kK3[2] * uu5[4]);
@@ -2757,6 +2766,144 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
     } else {
       reinterpret_cast<float4 *>(a.coef)[idx] = c0;
     }
+  }
+}
+
+// ---- smoothness + system as a register march (tall levels, h > 256; round 3)
+// One wave takes 64 consecutive columns (y0 - 2 .. y0 + 61) of one frame's skewed plane and walks a segment of
+// kMR rows.  A row-r pixel's 4-neighbours lie in rows r -+ 1 (left / right: same column; up / down: column
+// -+ 1), so with the rows r - 1 .. r + 2 of (wx, du, wy, dv) and the rows r - 1 .. r + 1 of s in registers, a
+// step loads row r + 2, computes s of row r + 1 and the system of row r; the column -+ 1 operands come from the
+// neighbouring lanes (DPP wave shifts).  s is valid on lanes 1 .. 62 and the system on lanes 2 .. 61 (60
+// columns per wave).  Everything streams once (plus 4 halo rows per kMR and 4 halo columns per 60): no LDS,
+// no barrier, no s round trip; the same functions as k_tv_smooth / k_tv_system, so the same bits.
+constexpr int kMR = 64, kMC = 60;
+__device__ __forceinline__ float wave_from_prev(float v) {  // lane i <- lane i - 1 (lane 0: its own value)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                                0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_from_next(float v) {  // lane i <- lane i + 1 (lane 63: its own value)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                                0x130, 0xF, 0xF, false));
+}
+__host__ __device__ __forceinline__ int march_segments(int rows) { return (rows + kMR - 1) / kMR; }
+__host__ __device__ __forceinline__ int march_strips(int h) { return (h + kMC - 1) / kMC; }
+
+template <int NOP, int NOC>
+__global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
+  const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
+  const int nstrip = march_strips(h), nseg = march_segments(rows);
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (frame, segment, strip), strip fastest
+  if (task >= (long)a.n * nseg * nstrip) return;
+  const int strip = (int)(task % nstrip), seg = (int)((task / nstrip) % nseg), f = (int)(task / ((long)nstrip * nseg));
+  const int lane = threadIdx.x & 63;
+  const int y = strip * kMC - 2 + lane;
+  const bool ycol = y >= 0 && y < h;
+  const bool out_lane = lane >= 2 && lane < 2 + kMC && ycol;
+  const int R0 = seg * kMR, R1 = R0 + kMR < rows ? R0 + kMR : rows;
+  const unsigned f0 = (unsigned)((long)f * a.sp);
+  const bool first = a.first_iter != 0;
+  // plane row of row r (-1: not in the plane), pixel x of (r, y) (false: no pixel)
+  auto prow = [&](int r) { return a.wrap ? (r < 0 ? r + w : (r >= w ? r - w : r)) : (r < 0 || r >= rows ? -1 : r); };
+  auto pix = [&](int r, int &x) {
+    const int pr = prow(r);
+    if (pr < 0 || !ycol) return false;
+    x = pr - y;
+    if (a.wrap) {
+      if (x < 0) x += w;
+      return true;
+    }
+    return x >= 0 && x < w;
+  };
+  struct Row {
+    float wx, du, wy, dv;
+  };
+  auto load_row = [&](int r) {
+    Row q{0.f, 0.f, 0.f, 0.f};
+    const int pr = prow(r);
+    if (pr >= 0 && ycol) {
+      const unsigned o = f0 + (unsigned)(pr * h + y);
+      q.wx = ldu(a.wxs, o);
+      q.du = ldu(a.du, o);
+      if (NOP == 2) {
+        q.wy = ldu(a.wys, o);
+        q.dv = ldu(a.dv, o);
+      }
+    }
+    return q;
+  };
+  // s of row r from rows r - 1 (U0), r (U1), r + 1 (U2): tv_smooth_px's clamped neighbourhood
+  auto smooth_row = [&](int r, const Row &U0, const Row &U1, const Row &U2) {
+    const float uu0 = smooth_uu<NOP>(a, first, U0.wx, U0.du), uu1 = smooth_uu<NOP>(a, first, U1.wx, U1.du);
+    const float uu2 = smooth_uu<NOP>(a, first, U2.wx, U2.du);
+    const float uup = wave_from_prev(uu0), uun = wave_from_next(uu2);
+    float vv0 = 0.f, vv1 = 0.f, vv2 = 0.f, vvp = 0.f, vvn = 0.f;
+    if (NOP == 2) {
+      vv0 = smooth_uu<2>(a, first, U0.wy, U0.dv);
+      vv1 = smooth_uu<2>(a, first, U1.wy, U1.dv);
+      vv2 = smooth_uu<2>(a, first, U2.wy, U2.dv);
+      vvp = wave_from_prev(vv0);
+      vvn = wave_from_next(vv2);
+    }
+    int x;
+    if (!pix(r, x)) return 0.0f;
+    const bool l = x > 0, rr = x < w - 1, u = y > 0, d = y < h - 1;
+    const float uu5[5] = {uu1, l ? uu0 : uu1, rr ? uu2 : uu1, u ? uup : uu1, d ? uun : uu1};
+    const float vv5[5] = {vv1, l ? vv0 : vv1, rr ? vv2 : vv1, u ? vvp : vv1, d ? vvn : vv1};
+    return smooth_from_uu<NOP>(a, uu5, vv5);
+  };
+  Row Um = load_row(R0 - 1), U0 = load_row(R0), U1 = load_row(R0 + 1);
+  float Sm = smooth_row(R0 - 1, load_row(R0 - 2), Um, U0);
+  float S0 = smooth_row(R0, Um, U0, U1);
+  for (int r = R0; r < R1; ++r) {
+    // the derivative images of row r (issued first: in flight while s of row r + 1 is computed)
+    int x;
+    const bool has = pix(r, x);
+    float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
+    const int pr = prow(r);
+    const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)(pr < 0 ? 0 : pr) * h + (ycol ? y : 0));
+#pragma unroll
+    for (int ch = 0; ch < NOC; ++ch) {
+      const unsigned o = qd + (unsigned)(ch * a.sp);
+      if (has) {
+        lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
+        lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
+      } else {
+        lIx[ch] = lIy[ch] = lIz[ch] = lIxx[ch] = lIxy[ch] = lIyy[ch] = lIxz[ch] = lIyz[ch] = 0.0f;
+      }
+    }
+    const Row U2 = load_row(r + 2);
+    const float S1 = smooth_row(r + 1, U0, U1, U2);
+    // the system of row r: s, wx, wy of the pixel and its 4-neighbourhood (centre, left, right, up, down)
+    const float Sp = wave_from_prev(Sm), Sn = wave_from_next(S1);
+    const float Xp = wave_from_prev(Um.wx), Xn = wave_from_next(U1.wx);
+    float Yp = 0.f, Yn = 0.f;
+    if (NOP == 2) {
+      Yp = wave_from_prev(Um.wy);
+      Yn = wave_from_next(U1.wy);
+    }
+    if (has && out_lane) {
+      const float S5[5] = {S0, Sm, S1, Sp, Sn};
+      const float X5[5] = {U0.wx, Um.wx, U1.wx, Xp, Xn};
+      const float Y5[5] = {U0.wy, Um.wy, U1.wy, Yp, Yn};
+      const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
+      float4 c0, c1;
+      sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, U0.du, NOP == 2 ? U0.dv : 0.0f, lIx, lIy, lIz, lIxx, lIxy, lIyy,
+                            lIxz, lIyz, c0, c1);
+      const long idx = (long)f0 + (long)pr * h + y;
+      if (NOP == 2) {
+        float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
+        C[0] = c0;
+        C[1] = c1;
+      } else {
+        reinterpret_cast<float4 *>(a.coef)[idx] = c0;
+      }
+    }
+    Um = U0;
+    U0 = U1;
+    U1 = U2;
+    Sm = S0;
+    S0 = S1;
   }
 }
 
@@ -4144,9 +4291,21 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
 // more than the smoothness round trip saves (config E, h = 544 / 272: 518 vs 299 us per launch).
 // Tall levels take the 2-D tiled form (k_tv_smsys2d) unless a.smsys2d = 0 (A/B: two launches there).
 bool tv_smsys_ok(const TvArgs &a) {
-  return a.smsys && ((smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) || a.smsys2d);
+  return a.smsys && ((smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) || a.smsys2d || a.smsys_march);
 }
 void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
+  if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {
+    const long waves = (long)a.n * march_segments(smsys_rows(a.w, a.h, a.wrap)) * march_strips(a.h);
+    const unsigned grid = ceil_div(waves, 4);
+    if (a.nop == 2) {
+      if (a.noc == 1) k_tv_smsys_m<2, 1><<<grid, 256, 0, s>>>(a);
+      else k_tv_smsys_m<2, 3><<<grid, 256, 0, s>>>(a);
+    } else {
+      if (a.noc == 1) k_tv_smsys_m<1, 1><<<grid, 256, 0, s>>>(a);
+      else k_tv_smsys_m<1, 3><<<grid, 256, 0, s>>>(a);
+    }
+    return;
+  }
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) {
     const dim3 g2(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), kS2R), ceil_div(a.h, kS2C));
     if (a.nop == 2) {

@@ -113,27 +113,32 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_cring", 0, 1),       # sweep-per-wave SOR without the LDS coefficient ring
     ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
-    ("smsys2d", 0, 2),         # tall levels: two launches instead of the 2-D tiled fused one (auto: on below 512 pairs)
+    ("smsys_march", 0, 1),     # tall levels: the 2-D tiled fused launch (smsys2d auto: on below 512 pairs)
+    (("smsys_march", "smsys2d"), (0, 0), (1, 2)),  # tall levels: two launches (smoothness, then system)
     ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
     ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
     ("patch_quad", 0, 1),      # gray p = 8 / 12 on eight lanes per patch (k_patchw) instead of four (k_patchq)
 ]
 
 
-@pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: f"{v[0]}={v[1]}")
+@pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: f"{v[0]}={v[1]}" if isinstance(v[0], str)
+                         else "+".join(f"{k}={x}" for k, x in zip(v[0], v[1])))
 @pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in CASES if c[0] <= 200 or c[1] > 256])
 def test_kernel_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op, over):
     """Every kernel variant (TV / SOR / DIS patch) gives the same bits as the default path and the oracle."""
     key, val, default = variant
+    keys, vals, defaults = ((key,), (val,), (default,)) if isinstance(key, str) else (key, val, default)
     a, b = od.synth_pair(w, h, noc, 4, mode)
     p, q = _params(od, oracle, w, noc, mode, op, over)
     ref = oracle.run_u8(a, b, q)
-    ctx.set_option(key, val)
+    for k, v in zip(keys, vals):
+        ctx.set_option(k, v)
     try:
         got = ctx.run_host(a, b, p)
     finally:
-        ctx.set_option(key, default)
-    assert_bitexact(got, ref, f"{key}={val}")
+        for k, d in zip(keys, defaults):
+            ctx.set_option(k, d)
+    assert_bitexact(got, ref, f"{keys}={vals}")
 
 
 @pytest.mark.parametrize("w,h,noc,op,over", [(160, 120, 1, 2, {}), (173, 97, 1, 2, {}), (192, 128, 3, 3, {}),

@@ -4,7 +4,8 @@ The reference takes any even patch size whose p*p*noc is a multiple of 4 (`run_d
 `oflow.cpp:80-91`, `patch.cpp:221-273`: LossComputeErrorImage walks novals/4 packets).  The library runs
 them on four kernel families, chosen by shape (`launch_patch`, ofdis_kernels.hip):
 
-* `k_patchw`  -- LDS-windowed eight-lane form, p = 8 / 12 (gray and RGB);
+* `k_patchq`  -- LDS-windowed four-lane form, gray p = 8 / 12 (round 3; `patch_quad=0` for the next one);
+* `k_patchw`  -- LDS-windowed eight-lane form, RGB p = 8 / 12 (and gray with `patch_quad=0`);
 * `k_patch8`  -- eight lanes per patch, values in registers: gray p = 2 / 4 / 6 / 10, p = 8 / 12 with
   `patch_window=0`;
 * `k_patch`   -- one wave per patch (p*p*noc <= 448): gray p = 14..20, RGB p = 4 / 6 / 10, and every
