@@ -164,6 +164,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "smsys" (0/1, default 1): smoothness and system of a TV iteration in one launch;
  *   "smsys2d" (0/1/2, default 2): the fused launch on 2-D tiles for levels taller than 256 rows (0: two
  *                        launches there; 2 = automatic: on for calls of fewer than 512 pairs);
+ *   "smsys_prefetch" (0/1, default 1): the fused launch (levels up to 256 rows, intensity images) issues a
+ *                        thread's derivative-image loads before the staging, not after two barriers;
  *   "smsys_march" (0/1, default 1): levels taller than 256 rows run smoothness + system as a register march
  *                        (one wave per 60 columns x 64 rows, no LDS; takes precedence over smsys2d);
  *   "prepd" (0/1, default 1): for intensity images, image warp, temporal images and the derivative filters

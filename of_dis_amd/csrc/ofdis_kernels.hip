@@ -2682,6 +2682,22 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
   const bool first = a.first_iter != 0;
   // plane row of a staged / s row index (r0 - 2 + i); -1 when it does not exist (unfolded layout)
   auto prow = [&](int r) { return a.wrap ? (r < 0 ? r + w : (r >= w ? r - w : r)) : (r < 0 || r >= rows ? -1 : r); };
+  // intensity images: the derivative images of this thread's phase-2 pixels (rb * h <= 1024: at most 4) are
+  // loaded first, so they are in flight with the staging loads instead of a second round trip after two barriers
+  constexpr int PF = NOC == 1 ? 4 : 1;
+  float pre[PF][8];
+  const bool pf = NOC == 1 && a.smsys_prefetch;
+  if (pf) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int i = threadIdx.x + j * (int)blockDim.x;
+      const int ri = i / h, y = i - ri * h, rr = r0 + ri;
+      const bool ok = i < rb * h && rr < rows;
+      const unsigned o = (unsigned)((long)f * a.sp + (long)(ok ? rr : 0) * h + (ok ? y : 0));
+      pre[j][0] = ldu(a.Ix, o); pre[j][1] = ldu(a.Iy, o); pre[j][2] = ldu(a.Iz, o); pre[j][3] = ldu(a.Ixx, o);
+      pre[j][4] = ldu(a.Ixy, o); pre[j][5] = ldu(a.Iyy, o); pre[j][6] = ldu(a.Ixz, o); pre[j][7] = ldu(a.Iyz, o);
+    }
+  }
   // ---- phase 0: stage
   for (int i = threadIdx.x; i < (rb + 4) * h; i += blockDim.x) {
     const int ri = i / h, y = i - ri * h;
@@ -2727,7 +2743,9 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
   }
   __syncthreads();
   // ---- phase 2: the system of rows r0 .. r0 + rb - 1
-  for (int i = threadIdx.x; i < rb * h; i += blockDim.x) {
+#pragma unroll
+  for (int j = 0; j < (NOC == 1 ? PF : 1); ++j) {
+  for (int i = threadIdx.x + j * (int)blockDim.x; i < rb * h; i += (NOC == 1 ? PF : 1) * (int)blockDim.x) {
     const int ri = i / h, y = i - ri * h;
     const int rr = r0 + ri;
     if (rr >= rows) break;
@@ -2750,11 +2768,16 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
     const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
     const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)rr * h + y);
     float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
+    if (pf && i < PF * (int)blockDim.x) {  // (rb * h <= 1024 whenever this kernel runs)
+      lIx[0] = pre[j][0]; lIy[0] = pre[j][1]; lIz[0] = pre[j][2]; lIxx[0] = pre[j][3];
+      lIxy[0] = pre[j][4]; lIyy[0] = pre[j][5]; lIxz[0] = pre[j][6]; lIyz[0] = pre[j][7];
+    } else {
 #pragma unroll
-    for (int ch = 0; ch < NOC; ++ch) {
-      const unsigned o = qd + (unsigned)(ch * a.sp);
-      lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
-      lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
+      for (int ch = 0; ch < NOC; ++ch) {
+        const unsigned o = qd + (unsigned)(ch * a.sp);
+        lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
+        lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
+      }
     }
     float4 c0, c1;
     sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, qc.z, NOP == 2 ? qc.w : 0.0f, lIx, lIy, lIz, lIxx, lIxy, lIyy,
@@ -2766,6 +2789,7 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
     } else {
       reinterpret_cast<float4 *>(a.coef)[idx] = c0;
     }
+  }
   }
 }
 
