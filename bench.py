@@ -35,9 +35,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # BASELINE.json configs -> (binary, width, height, noc, mode, oppoint, explicit 20 parameters or None, batch)
 CONFIGS = {
     "A": ("run_OF_INT", 640, 480, 1, 1, 2, None, 2048),  # 1024: 110k, 2048: 113k MPix/s (profiles/r02/sweep6)
-    # 2048 pairs per GPU per step = two 1024-pair chunks on two streams (measured best: 1024 pairs 266k,
-    # 1536 282k, 2048 298k, 3072 285k, 4096 293k MPix/s; profiles/r02/sweep3)
-    "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 2048),
+    # 4096 pairs per GPU per step = two 2048-pair chunks on two streams.  Round 3 (faster patch and TV kernels),
+    # same box, ABAB (profiles/r03/batch): 2048 pairs 291-309k (bimodal: the lanes' phase alignment), 3072 308k,
+    # 4096 312-316k MPix/s; round 2's sweep had 2048 best (profiles/r02/sweep3)
+    "B": ("run_OF_INT", 1920, 1080, 1, 1, 2, None, 4096),
     # op-point 3 as the config text states it ("finer scale, L1 cost"): op3 values with costfct = 1.
     # 512 pairs = two 256-pair chunks on two streams (64: 6.9k, 128: 7.4k, 256: 7.8k, 512: 8.1k, 1024: 8.2k
     # MPix/s; profiles/r02/ab/ab_batch*)
