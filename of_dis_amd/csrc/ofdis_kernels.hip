@@ -2591,7 +2591,16 @@ __device__ __forceinline__ void sys_compute(const TvArgs &a, int x, int y, const
     c0 = make_float4(A11, A12, A12, A22);  // (a11, a12) and (a12, a22) pair up for packed fp32
     c1 = make_float4(B1, B2, shv, svv);
   } else {
-    c0 = make_float4(A11, B1, shv, svv);
+    // the DE point SOR's diagonal a11 + (the four diffusivities of the pixel's existing neighbours), summed in
+    // its order (top, left, bottom, right; solver.c's DE branch) -- it depends on the system only, so it is
+    // computed here once instead of in every sweep (the SOR kernels read A = c0.x); vt / hl are the upper /
+    // left pixel's sv / sh with the same operands, and sv / sh of a missing bottom / right neighbour are 0
+    float dsum = 0.0f;
+    if (y > 0) dsum = dsum + (su + sc);
+    if (x > 0) dsum = dsum + (sl + sc);
+    if (y < h - 1) dsum = dsum + svv;
+    if (x < w - 1) dsum = dsum + shv;
+    c0 = make_float4(A11 + dsum, B1, shv, svv);
     c1 = c0;
   }
 }
@@ -3102,12 +3111,12 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
         dv[o] = (1.0f - omega) * dv[o] + omega / A22 * (B2 - A12 * du[o]);
       } else {
         const float4 c0 = C[o];
-        float su = 0.0f, sd = 0.0f;
-        if (y > 0) { const float q = SV_(oU); su -= q * du[oU]; sd += q; }
-        if (x > 0) { const float q = SH_(oL); su -= q * du[oL]; sd += q; }
-        if (y < h - 1) { su -= c0.w * du[oD]; sd += c0.w; }
-        if (x < w - 1) { su -= c0.z * du[oR]; sd += c0.z; }
-        const float A11 = c0.x + sd, B1 = c0.y - su;
+        float su = 0.0f;  // (c0.x = a11 + the diffusivities: sys_compute)
+        if (y > 0) { const float q = SV_(oU); su -= q * du[oU]; }
+        if (x > 0) { const float q = SH_(oL); su -= q * du[oL]; }
+        if (y < h - 1) { su -= c0.w * du[oD]; }
+        if (x < w - 1) { su -= c0.z * du[oR]; }
+        const float A11 = c0.x, B1 = c0.y - su;
         du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
       }
     }
@@ -3199,12 +3208,12 @@ __device__ __forceinline__ void rb_update(const RbPix &d, int x, int y, int w, i
     v = v + omega * (d.i12 * B1 + d.i22 * B2 - v);
     u = nu;
   } else {
-    float su = 0.0f, sd = 0.0f;
-    if (y > 0) { su = su - d.vt * ut; sd = sd + d.vt; }
-    if (x > 0) { su = su - d.hl * ul; sd = sd + d.hl; }
-    if (y < h - 1) { su = su - d.vb * ub; sd = sd + d.vb; }
-    if (x < w - 1) { su = su - d.hr * ur; sd = sd + d.hr; }
-    const float A = d.i11 + sd, Bv = d.b1 - su;
+    float su = 0.0f;  // (i11 = a11 + the diffusivities: sys_compute)
+    if (y > 0) { su = su - d.vt * ut; }
+    if (x > 0) { su = su - d.hl * ul; }
+    if (y < h - 1) { su = su - d.vb * ub; }
+    if (x < w - 1) { su = su - d.hr * ur; }
+    const float A = d.i11, Bv = d.b1 - su;
     u = (1.0f - omega) * u + omega * (Bv / A);
   }
 }
@@ -3410,12 +3419,12 @@ struct SorPipe {
         nvv[0] = own_v0 + omega * (d.i12 * B1 + d.i22 * B2 - own_v0);
       } else {
         d.i11 = c11;
-        float su = 0.0f, sd = 0.0f;
-        su = has_top ? su - d.vt * tu[0] : su;      sd = has_top ? sd + d.vt : sd;
-        su = x0 > 0 ? su - d.hl * hu[qp][0] : su;   sd = x0 > 0 ? sd + d.hl : sd;
-        su = has_bot ? su - d.vv * cbu : su;        sd = has_bot ? sd + d.vv : sd;
-        su = x0 < w - 1 ? su - d.hr * ur : su;      sd = x0 < w - 1 ? sd + d.hr : sd;
-        const float A = c11 + sd, Bv = d.b1 - su;
+        float su = 0.0f;  // (c11 = a11 + the diffusivities: sys_compute)
+        su = has_top ? su - d.vt * tu[0] : su;
+        su = x0 > 0 ? su - d.hl * hu[qp][0] : su;
+        su = has_bot ? su - d.vv * cbu : su;
+        su = x0 < w - 1 ? su - d.hr * ur : su;
+        const float A = c11, Bv = d.b1 - su;
         nu[0] = (1.0f - omega) * own_u0 + omega * (Bv / A);
         nvv[0] = 0.0f;
       }
@@ -3436,12 +3445,12 @@ struct SorPipe {
         nu[s] = ou + omega * (e.i11 * B1 + e.i12 * B2 - ou);
         nvv[s] = ov + omega * (e.i12 * B1 + e.i22 * B2 - ov);
       } else {
-        float su = 0.0f, sd = 0.0f;
-        su = has_top ? su - e.vt * tu[s] : su;          sd = has_top ? sd + e.vt : sd;
-        su = xs > 0 ? su - e.hl * hu[qp][s] : su;       sd = xs > 0 ? sd + e.hl : sd;
-        su = has_bot ? su - e.vv * bu[s - 1] : su;      sd = has_bot ? sd + e.vv : sd;
-        su = xs < w - 1 ? su - e.hr * ur : su;          sd = xs < w - 1 ? sd + e.hr : sd;
-        const float A = e.i11 + sd, Bv = e.b1 - su;
+        float su = 0.0f;
+        su = has_top ? su - e.vt * tu[s] : su;
+        su = xs > 0 ? su - e.hl * hu[qp][s] : su;
+        su = has_bot ? su - e.vv * bu[s - 1] : su;
+        su = xs < w - 1 ? su - e.hr * ur : su;
+        const float A = e.i11, Bv = e.b1 - su;
         nu[s] = (1.0f - omega) * ou + omega * (Bv / A);
         nvv[s] = 0.0f;
       }
@@ -3733,12 +3742,12 @@ struct SorLane {
         vv = c0.w;
         const bool has_top = !notop[r], has_bot = !(border[r] && has_top);
         const float tu = tp.x, ur = hasr ? rgt.x : 0.0f, hl = phr[r];
-        float su = 0.0f, sd = 0.0f;
-        su = has_top ? su - tsv * tu : su;   sd = has_top ? sd + tsv : sd;
-        su = hasl ? su - hl * pp[r].x : su;  sd = hasl ? sd + hl : sd;
-        su = has_bot ? su - vv * bt.x : su;  sd = has_bot ? sd + vv : sd;
-        su = hasr ? su - hr * ur : su;       sd = hasr ? sd + hr : sd;
-        const float A = a11 + sd, Bq = b1 - su;
+        float su = 0.0f;  // (a11 here is a11 + the diffusivities: sys_compute)
+        su = has_top ? su - tsv * tu : su;
+        su = hasl ? su - hl * pp[r].x : su;
+        su = has_bot ? su - vv * bt.x : su;
+        su = hasr ? su - hr * ur : su;
+        const float A = a11, Bq = b1 - su;
         nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
         phr[r] = hr;
       }
