@@ -166,6 +166,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        launches there; 2 = automatic: on for calls of fewer than 512 pairs);
  *   "smsys_prefetch" (0/1, default 1): the fused launch (levels up to 256 rows, intensity images) issues a
  *                        thread's derivative-image loads before the staging, not after two barriers;
+ *   "smsys_small" (0/1, default 1): a fused launch that cannot fill the chip (fewer than 4096 row blocks:
+ *                        a few pairs per call) takes ~1 pixel per thread (>= 4 rows per block) instead of 4;
  *   "smsys_march" (0/1, default 1): levels taller than 256 rows run smoothness + system as a register march
  *                        (one wave per 60 columns x 64 rows, no LDS; takes precedence over smsys2d);
  *   "prepd" (0/1, default 1): for intensity images, image warp, temporal images and the derivative filters

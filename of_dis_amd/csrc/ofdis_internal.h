@@ -113,6 +113,7 @@ struct TvArgs {
   int prepd;                   // prep + derivatives in one launch (k_tv_prepd, intensity images; 0: three launches)
   int smsys2d;                 // ... and on 2-D tiles for tall levels (k_tv_smsys2d; 0: two launches there, A/B)
   int smsys_prefetch;          // k_tv_smsys, intensity images: derivative images loaded before the staging
+  int smsys_small;             // k_tv_smsys: ~1 pixel per thread when a launch cannot fill the chip
   int smsys_march;             // tall levels: the register march k_tv_smsys_m (takes precedence over smsys2d)
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)
 };

@@ -2676,15 +2676,24 @@ __global__ __launch_bounds__(256) void k_tv_system(TvArgs a) {
 // frame, so the row blocks of a frame (which share halo rows) land on one XCD.
 __host__ __device__ __forceinline__ int smsys_rows(int w, int h, int wrap) { return wrap ? w : w + h - 1; }
 __host__ __device__ __forceinline__ int smsys_rb(int h) { return h >= 1024 ? 1 : (1024 / h > 16 ? 16 : 1024 / h); }
-__host__ __device__ __forceinline__ size_t smsys_lds(int h) {
-  const int rb = smsys_rb(h);
+__host__ __device__ __forceinline__ size_t smsys_lds_rb(int h, int rb) {
   return (size_t)(rb + 4) * h * 16 + (size_t)(rb + 2) * h * 4;
+}
+__host__ __device__ __forceinline__ size_t smsys_lds(int h) { return smsys_lds_rb(h, smsys_rb(h)); }
+// Rows per workgroup of a launch: smsys_rb's (up to 1024 pixels, 4 per thread) when the launch has enough
+// workgroups to fill the chip (>= 4096), else about one pixel per thread (>= 4 rows): the latency regime
+// (the drop-in CLI's single pair, config D's 32 pairs per GPU) then spreads a level over 3-4x the CUs.
+__host__ __device__ __forceinline__ int smsys_rb_n(int h, int rows, int n, int small) {
+  const int rb = smsys_rb(h);
+  if (!small || (long)n * ((rows + rb - 1) / rb) >= 4096) return rb;
+  const int r1 = (256 + h - 1) / h;
+  return r1 < 4 ? 4 : (r1 < rb ? r1 : rb);
 }
 
 template <int NOP, int NOC>
 __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
   extern __shared__ float4 st[];  // [(RB + 4) * h] (wx, wy, du, dv), then float s[(RB + 2) * h]
-  const int w = a.w, h = a.h, rb = smsys_rb(h), rows = smsys_rows(w, h, a.wrap);
+  const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap), rb = smsys_rb_n(h, rows, a.n, a.smsys_small);
   float *sl = reinterpret_cast<float *>(st + (rb + 4) * h);
   const int f = blockIdx.x, r0 = blockIdx.y * rb;
   const long f0 = (long)f * a.sp;
@@ -4350,8 +4359,9 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
     }
     return;
   }
-  const dim3 grid(a.n, ceil_div(smsys_rows(a.w, a.h, a.wrap), smsys_rb(a.h)));
-  const size_t lds = smsys_lds(a.h);
+  const int rows = smsys_rows(a.w, a.h, a.wrap), rb = smsys_rb_n(a.h, rows, a.n, a.smsys_small);
+  const dim3 grid(a.n, ceil_div(rows, rb));
+  const size_t lds = smsys_lds_rb(a.h, rb);
   if (a.nop == 2) {
     if (a.noc == 1)
       k_tv_smsys<2, 1><<<grid, 256, lds, s>>>(a);
