@@ -51,6 +51,8 @@ CASES = [
     (192, 128, 1, 1, 3, {}),                                  # gray op3: p = 12 flow on four lanes per patch
     (192, 128, 1, 1, 4, {"costfct": 1, "max_iter": 16, "min_iter": 16}),  # ... L1 cost
     (240, 120, 1, 2, 4, {"costfct": 2, "max_iter": 16, "min_iter": 16}),  # depth p = 12, pseudo-Huber
+    (192, 128, 1, 1, 3, {"usefbcon": 1, "costfct": 1}),       # four-lane p = 12 flow with forward-backward
+    (176, 140, 1, 1, 3, {"patnorm": 0, "min_iter": 4, "dp_thresh": 0.3, "dr_thresh": 0.9}),  # ... no norm., stops
     (160, 120, 1, 1, 2, {"costfct": 2}),                      # pseudo-Huber
     (160, 120, 1, 1, 2, {"min_iter": 2, "dp_thresh": 0.3, "dr_thresh": 0.9}),  # early stopping active
     (160, 120, 1, 1, 2, {"patnorm": 0, "tv_innerit": 2, "tv_solverit": 4, "tv_sor": 1.3}),
