@@ -128,8 +128,9 @@ def kernel_roofline(od, p, W, H, B, per_launch, cfg, steps, kernels, name):
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
            "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_us": round(k["avg_us"], 2)}
     if name == "patch":  # not an HBM-bound kernel: say what bounds it
-        out["limiter"] = ("VALU issue: SQ_ACTIVE_INST_VALU x waves/SIMD ~ 1.0 of SIMD cycles at configs C and E "
-                          "(profiles/r02/pmc); bytes = compulsory per patch (template, gradients, one window, outputs)")
+        out["limiter"] = ("VALU issue: SQ_ACTIVE_INST_VALU x waves/SIMD ~ 0.9-1.2 of SIMD cycles at configs C and E "
+                          "(profiles/r02/pmc, profiles/r03/pmc); bytes = compulsory per patch (template, gradients, "
+                          "one window, outputs)")
     return out
 
 
