@@ -115,8 +115,8 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_cring", 0, 1),       # sweep-per-wave SOR without the LDS coefficient ring
     ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
-    ("smsys_prefetch", 0, 1),
-    ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)  # fused smoothness + system: derivative images loaded in phase 2
+    ("smsys_prefetch", 0, 1),  # fused smoothness + system: derivative images loaded in phase 2
+    ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)
     ("smsys_march", 0, 1),     # tall levels: the 2-D tiled fused launch (smsys2d auto: on below 512 pairs)
     (("smsys_march", "smsys2d"), (0, 0), (1, 2)),  # tall levels: two launches (smoothness, then system)
     ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
