@@ -120,7 +120,8 @@ void ofdis_context_destroy(ofdis_context *ctx);
  * after the work already queued there and that stream's later work after the call.  Asynchronous w.r.t. the
  * host.  All calls on one context share its workspaces: a call waits for the previous call of the context
  * whatever stream either was issued on.  A batch is split into launches of at most
- * ofdis_max_frames_per_launch() frames.
+ * ofdis_max_frames_per_launch() frames.  n < 1, a non-positive size or a NULL image / flow pointer returns
+ * OFDIS_ERR_INVALID_ARGUMENT before anything is enqueued (the context stays usable).
  */
 int ofdis_run_batch_u8(ofdis_context *ctx, const uint8_t *img_a, const uint8_t *img_b, int n, int width,
                        int height, const ofdis_params *p, float *flow_out, void *stream);

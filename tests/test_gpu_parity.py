@@ -223,6 +223,32 @@ def test_batch_equals_singles(od, ctx):
             assert_bitexact(out[f], single, f"batch frame {f} (config {k})")
 
 
+def test_bad_batch_arguments_enqueue_nothing(od, ctx):
+    """An empty or malformed batch is refused with OFDIS_ERR_INVALID_ARGUMENT (ofdis.h, ofdis_run_batch_u8)
+    before anything is enqueued: the output buffer is untouched and the context runs the next batch bit-exact."""
+    import torch
+    from of_dis_amd import _lib
+    w, h = 160, 120
+    pa, pb = od.synth_pair(w, h, 1, 0, 1)
+    p = od.oppoint(2, w, 1, 1)
+    want = ctx.run_host(pa, pb, p)
+    a = torch.from_numpy(pa[None]).cuda().unsqueeze(-1)
+    b = torch.from_numpy(pb[None]).cuda().unsqueeze(-1)
+    out = torch.full((1, h, w, 2), 7.0, device="cuda")
+    torch.cuda.synchronize()
+    ap, bp, op = a.data_ptr(), b.data_ptr(), out.data_ptr()
+    for n, ww, hh, x, y, z in ((0, w, h, ap, bp, op), (-1, w, h, ap, bp, op), (1, 0, h, ap, bp, op),
+                               (1, w, -h, ap, bp, op), (1, w, h, 0, bp, op), (1, w, h, ap, 0, op), (1, w, h, ap, bp, 0)):
+        with pytest.raises(_lib.OfdisError) as e:
+            ctx.run_ptr(x, y, n, ww, hh, p, z)
+        assert e.value.code == _lib.ERR_INVALID_ARGUMENT, (n, ww, hh)
+    torch.cuda.synchronize()
+    assert bool((out == 7.0).all()), "a refused call wrote the output"
+    ctx.run_ptr(ap, bp, 1, w, h, p, op)
+    torch.cuda.synchronize()
+    assert_bitexact(out[0].cpu().numpy(), want, "batch after refused calls")
+
+
 def test_default_stream_inputs_are_ordered(od, ctx):
     """Inputs produced by kernels on torch's default (legacy NULL) stream right before the call -- here the
     copy kernel of .contiguous() on permuted views -- are complete when the flow kernels read them, and the
