@@ -115,6 +115,9 @@ struct TvArgs {
   int smsys_prefetch;          // k_tv_smsys, intensity images: derivative images loaded before the staging
   int smsys_small;             // k_tv_smsys: ~1 pixel per thread when a launch cannot fill the chip
   int smsys_march;             // tall levels: the register march k_tv_smsys_m (takes precedence over smsys2d)
+  int smsys_deriv;             // row-block k_tv_smsys, intensity images: Ixx .. Iyz computed from staged Ix, Iy, Iz
+                               // (k_tv_prepd then writes only Ix, Iy, Iz of the derivative planes); set by the
+                               // runtime only where tv_deriv_fused() holds
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)
 };
 
@@ -149,6 +152,7 @@ void launch_tv_prepd(const TvArgs &a, hipStream_t s);
 void launch_tv_smooth(const TvArgs &a, hipStream_t s);
 void launch_tv_system(const TvArgs &a, hipStream_t s);
 bool tv_smsys_ok(const TvArgs &a);
+bool tv_deriv_fused(const TvArgs &a);  // the level's derivative filters can move into k_tv_smsys (smsys_deriv)
 void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);

@@ -2206,6 +2206,7 @@ __global__ __launch_bounds__(256) void k_tv_prepd(TvArgs a) {
     a.Iz[k] = DT[ty][tx];
     a.Ix[k] = IX[iy][ix];
     a.Iy[k] = IY[iy][ix];
+    if (a.smsys_deriv) continue;  // the system kernel filters Ix, Iy, Iz itself
     a.Ixx[k] = ixx;
     a.Ixy[k] = ixy;
     a.Iyy[k] = iyy;
@@ -2690,11 +2691,26 @@ __host__ __device__ __forceinline__ int smsys_rb_n(int h, int rows, int n, int s
   return r1 < 4 ? 4 : (r1 < rb ? r1 : rb);
 }
 
-template <int NOP, int NOC>
+// DF (intensity images, option smsys_deriv): Ix, Iy, Iz are staged with (wx, wy, du, dv) -- same rows, same halo
+// -- and the five second-order filters of get_derivatives (Ixx, Ixy of Ix; Iyy of Iy; Ixz, Iyz of It = Iz:
+// opticalflow_aux.c:77-132, k_tv_deriv2 / k_tv_prepd's expressions and replicate border) are computed per
+// pixel from LDS instead of read as five planes (k_tv_prepd then does not write them): 20 bytes per pixel and
+// inner iteration less read, 20 per level less written.  A row-r pixel's horizontal neighbour x + k is staged
+// row r + k, same column; its vertical neighbour y + k is row r + k, column y + k (k <= 2: inside the halo).
+__host__ __device__ __forceinline__ size_t smsys_lds_df(int h, int rb, bool df) {
+  return smsys_lds_rb(h, rb) + (df ? (size_t)3 * (rb + 4) * h * 4 : 0);
+}
+constexpr size_t kSmsysDfCap = 40 * 1024;
+template <int NOP, int NOC, bool DF = false>
 __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
-  extern __shared__ float4 st[];  // [(RB + 4) * h] (wx, wy, du, dv), then float s[(RB + 2) * h]
-  const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap), rb = smsys_rb_n(h, rows, a.n, a.smsys_small);
+  extern __shared__ float4 st[];  // [(RB + 4) * h] (wx, wy, du, dv), then float s[(RB + 2) * h] (DF: Ix, Iy, Iz)
+  static_assert(!DF || NOC == 1, "staged derivatives: intensity images");
+  const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
+  int rb = smsys_rb_n(h, rows, a.n, a.smsys_small);
+  if (DF)  // four workgroups per CU (five, at 32 KB: slower, r03_s49); the launcher applies the same rule
+    while (rb > 1 && smsys_lds_df(h, rb, true) > kSmsysDfCap) --rb;
   float *sl = reinterpret_cast<float *>(st + (rb + 4) * h);
+  float *gIx = sl + (rb + 2) * h, *gIy = gIx + (rb + 4) * h, *gIz = gIy + (rb + 4) * h;  // DF
   const int f = blockIdx.x, r0 = blockIdx.y * rb;
   const long f0 = (long)f * a.sp;
   const bool first = a.first_iter != 0;
@@ -2704,7 +2720,7 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
   // loaded first, so they are in flight with the staging loads instead of a second round trip after two barriers
   constexpr int PF = NOC == 1 ? 4 : 1;
   float pre[PF][8];
-  const bool pf = NOC == 1 && a.smsys_prefetch;
+  const bool pf = NOC == 1 && !DF && a.smsys_prefetch;
   if (pf) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
@@ -2721,6 +2737,7 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
     const int ri = i / h, y = i - ri * h;
     const int r = prow(r0 - 2 + ri);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    float dx = 0.f, dy = 0.f, dz = 0.f;
     if (r >= 0) {
       const long o = f0 + (long)r * h + y;
       v.x = a.wxs[o];
@@ -2729,8 +2746,18 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
         v.y = a.wys[o];
         v.w = a.dv[o];
       }
+      if (DF) {
+        dx = a.Ix[o];
+        dy = a.Iy[o];
+        dz = a.Iz[o];
+      }
     }
     st[i] = v;
+    if (DF) {
+      gIx[i] = dx;
+      gIy[i] = dy;
+      gIz[i] = dz;
+    }
   }
   __syncthreads();
   // ---- phase 1: s of rows r0 - 1 .. r0 + rb
@@ -2786,7 +2813,27 @@ __global__ __launch_bounds__(256) void k_tv_smsys(TvArgs a) {
     const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
     const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)rr * h + y);
     float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
-    if (pf && i < PF * (int)blockDim.x) {  // (rb * h <= 1024 whenever this kernel runs)
+    if constexpr (DF) {
+      // replicate border: the clamped tap's staged offset (rows for x, rows + columns for y)
+      const int hx0 = (max(x - 2, 0) - x) * h, hx1 = (max(x - 1, 0) - x) * h;
+      const int hx3 = (min(x + 1, w - 1) - x) * h, hx4 = (min(x + 2, w - 1) - x) * h;
+      const int vy0 = (max(y - 2, 0) - y) * (h + 1), vy1 = (max(y - 1, 0) - y) * (h + 1);
+      const int vy3 = (min(y + 1, h - 1) - y) * (h + 1), vy4 = (min(y + 2, h - 1) - y) * (h + 1);
+      auto c5h = [&](const float *P) {
+        return kK5[0] * P[cs + hx0] + ((kK5[1] * P[cs + hx1] + kK5[2] * P[cs]) + (kK5[3] * P[cs + hx3] + kK5[4] * P[cs + hx4]));
+      };
+      auto c5v = [&](const float *P) {
+        return kK5[0] * P[cs + vy0] + ((kK5[1] * P[cs + vy1] + kK5[2] * P[cs]) + (kK5[3] * P[cs + vy3] + kK5[4] * P[cs + vy4]));
+      };
+      lIx[0] = gIx[cs];
+      lIy[0] = gIy[cs];
+      lIz[0] = gIz[cs];
+      lIxx[0] = c5h(gIx);
+      lIxy[0] = c5v(gIx);
+      lIyy[0] = c5v(gIy);
+      lIxz[0] = c5h(gIz);
+      lIyz[0] = c5v(gIz);
+    } else if (pf && i < PF * (int)blockDim.x) {  // (rb * h <= 1024 whenever this kernel runs)
       lIx[0] = pre[j][0]; lIy[0] = pre[j][1]; lIz[0] = pre[j][2]; lIxx[0] = pre[j][3];
       lIxy[0] = pre[j][4]; lIyy[0] = pre[j][5]; lIxz[0] = pre[j][6]; lIyz[0] = pre[j][7];
     } else {
@@ -4335,6 +4382,11 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
 bool tv_smsys_ok(const TvArgs &a) {
   return a.smsys && ((smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) || a.smsys2d || a.smsys_march);
 }
+// The derivative filters move into the system kernel only where the level runs the row-block k_tv_smsys and
+// k_tv_prepd (intensity images): the march, the 2-D tiles and the two-launch form read all eight planes.
+bool tv_deriv_fused(const TvArgs &a) {
+  return a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024;
+}
 void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {
     const long waves = (long)a.n * march_segments(smsys_rows(a.w, a.h, a.wrap)) * march_strips(a.h);
@@ -4359,7 +4411,16 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
     }
     return;
   }
-  const int rows = smsys_rows(a.w, a.h, a.wrap), rb = smsys_rb_n(a.h, rows, a.n, a.smsys_small);
+  const int rows = smsys_rows(a.w, a.h, a.wrap);
+  int rb = smsys_rb_n(a.h, rows, a.n, a.smsys_small);
+  if (a.smsys_deriv) {  // the kernel's rule: four workgroups per CU
+    while (rb > 1 && smsys_lds_df(a.h, rb, true) > kSmsysDfCap) --rb;
+    const dim3 grid(a.n, ceil_div(rows, rb));
+    const size_t lds = smsys_lds_df(a.h, rb, true);
+    if (a.nop == 2) k_tv_smsys<2, 1, true><<<grid, 256, lds, s>>>(a);
+    else k_tv_smsys<1, 1, true><<<grid, 256, lds, s>>>(a);
+    return;
+  }
   const dim3 grid(a.n, ceil_div(rows, rb));
   const size_t lds = smsys_lds_rb(a.h, rb);
   if (a.nop == 2) {

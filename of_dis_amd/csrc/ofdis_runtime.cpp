@@ -87,8 +87,9 @@ struct ofdis_context {
   // 544-551 ms per step) -- profiles/r02/ab/ab_smsys2d.
   int opt_smsys2d = 2;
   int opt_smsys_march = 1;     // tall levels: smoothness + system as a register march (k_tv_smsys_m)
-  int opt_smsys_prefetch = 1;
-  int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip  // fused smoothness + system (gray): derivative images issued before the staging
+  int opt_smsys_prefetch = 1;  // fused smoothness + system (gray): derivative images issued before the staging
+  int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
+  int opt_smsys_deriv = 1;     // fused smoothness + system (gray): second derivatives filtered from staged Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
   int opt_sor_cring = 1;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients)
   int opt_prepd = 1;           // prep + derivatives in one launch for intensity images (0: three launches, A/B)
@@ -507,9 +508,11 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.smsys_march = c->opt_smsys_march;
       tv.smsys_prefetch = c->opt_smsys_prefetch;
       tv.smsys_small = c->opt_smsys_small;
+      tv.smsys_deriv = c->opt_smsys_deriv;
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
+      tv.smsys_deriv = tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
       } else {
@@ -1222,6 +1225,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},
       {"smsys_prefetch", &ofdis_context::opt_smsys_prefetch, 0, 1},
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
+      {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 1},   {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},

@@ -117,6 +117,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
     ("smsys_prefetch", 0, 1),  # fused smoothness + system: derivative images loaded in phase 2
     ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)
+    ("smsys_deriv", 0, 1),     # fused launch reads all eight derivative planes (prepd writes them)
     ("smsys_march", 0, 1),     # tall levels: the 2-D tiled fused launch (smsys2d auto: on below 512 pairs)
     (("smsys_march", "smsys2d"), (0, 0), (1, 2)),  # tall levels: two launches (smoothness, then system)
     ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
