@@ -83,7 +83,8 @@ def parse():
                     help="diagnostic: time this many extra K-step regions before the reported one (stderr)")
     ap.add_argument("--dry-run", action="store_true", help="rank/shard bookkeeping on gloo, no GPU (CPU test)")
     ap.add_argument("--parity-frames", type=int, default=8,
-                    help="timed-pass frames re-checked against the CPU oracle on rank 0 (1 per rank at N > 1)")
+                    help="distinct timed-pass frames re-checked against the CPU oracle on every rank (their tiles: "
+                         "on the device)")
     return ap.parse_args()
 
 
@@ -127,6 +128,27 @@ def kernel_roofline(od, p, W, H, B, per_launch, cfg, steps, kernels, name):
     out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
            "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_us": round(k["avg_us"], 2)}
+    if name == "tv_sor":
+        # Three readings of one launch time.  The SURVEY §8(d) unit counts 44 (OF) / 24 (DE)
+        # B per pixel PER SWEEP (a streaming sweep-by-sweep model); k_tv_sor_lanes runs all sweeps of a call in one
+        # pass and reads each pixel's coefficients once, so that figure is a streaming-equivalent rate that can
+        # exceed the peak -- it is not a roofline fraction.  The two roofline fractions: the once-per-launch
+        # compulsory bytes (44 / 24 B per pixel, what a sweep-fused kernel must move) and the PMC bytes.
+        sweeps = max(1, int(p.tv_solverit))
+        comp = bytes_launch / sweeps
+        comp_gbs = comp / (k["avg_us"] * 1e-6) / 1e9
+        out["model_equiv_frac"] = out.pop("frac")
+        out["model_equiv_gbs"] = out.pop("achieved")
+        out["achieved"] = round(comp_gbs, 1)
+        out["frac"] = out["frac_compulsory"] = round(comp_gbs / HBM_PEAK_GBS, 4)
+        out["compulsory_bytes_per_launch"] = comp
+        out["frac_counters"] = (None if traffic is None else
+                                round(traffic / (k["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4))
+        out["counters_vs_compulsory"] = None if traffic is None else round(traffic / comp, 3)
+        out["note"] = ("frac = frac_compulsory: 44 (OF) / 24 (DE) B/px once per launch / launch time / 8 TB/s; "
+                       "frac_counters: PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/traffic.json) / launch "
+                       "time; model_equiv_frac: the SURVEY 8(d) per-sweep unit x sweeps, a streaming-equivalent "
+                       "rate of the sweep-fused kernel (may exceed 1, not a roofline fraction)")
     if name == "patch":  # not an HBM-bound kernel: say what bounds it
         out["limiter"] = ("VALU issue: SQ_ACTIVE_INST_VALU x waves/SIMD ~ 0.9-1.2 of SIMD cycles at configs C and E "
                           "(profiles/r02/pmc, profiles/r03/pmc); bytes = compulsory per patch (template, gradients, "
@@ -400,6 +422,20 @@ def main():
     elapsed = odd.max_over_ranks(elapsed, dev) if world > 1 else elapsed
     # the timed pass's output of the distinct pairs, for the parity check below
     timed_out = out[:nd].cpu().numpy()
+    # every other frame of the timed pass is a tile of one of the nd distinct pairs: compare its bits on the device
+    # with its tile source (frames nd.. against frames 0..nd-1, nd at a time), so the oracle check of the distinct
+    # frames covers the whole batch
+    tiles_equal = [0] * nd  # per distinct pair: the later frames equal to it bit for bit
+    ov = out.view(B, -1).view(torch.int32)
+    for j in range(nd, B, nd):
+        m = min(nd, B - j)
+        if torch.equal(ov[j:j + m], ov[:m]):
+            for i in range(m):
+                tiles_equal[i] += 1
+        else:
+            for i in range(m):
+                tiles_equal[i] += int(torch.equal(ov[j + i], ov[i]))
+    del ov
 
     frames = total * args.steps
     mpix = W * H * frames / elapsed / 1e6
@@ -444,6 +480,28 @@ def main():
     if rank == 0 and world == 1 and not args.no_latency:
         latency = pair_latency(od, ctx, p, pairs[0], dev, torch)
 
+    # ---- strong-scaling configs on one GPU: the per-GPU rate at the shard size 8 GPUs would run (config D: 32 of
+    # the 256 pairs), so a 1-GPU D number is never read as the per-GPU throughput of the 8-GPU job
+    shard8 = None
+    if scaling == "strong" and world == 1 and total >= 8:
+        n8 = total // 8
+        ctx.set_option("streams", 0)
+        ctx.set_option("chunk", 0)
+        for _ in range(args.warmup):
+            ctx.run_ptr(a.data_ptr(), b.data_ptr(), n8, W, H, p, out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        t0s = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.run_ptr(a.data_ptr(), b.data_ptr(), n8, W, H, p, out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        ts8 = time.perf_counter() - t0s
+        r8 = W * H * n8 * args.steps / ts8 / 1e6
+        shard8 = {"pairs_per_gpu": n8, "mpix_s_per_gpu": round(r8, 2), "ms_per_step": round(ts8 / args.steps * 1e3, 3),
+                  "projected_1to8_efficiency": round(r8 / mpix, 3),
+                  "what": f"1 GPU running the {n8}-pair shard each of 8 GPUs gets of this config's {total} pairs"}
+        ctx.set_option("streams", args.streams)
+        ctx.set_option("chunk", args.chunk)
+
     # ---- host-buffer entry point (PCIe-inclusive; never the headline value)
     host_io = None
     if args.host_io and rank == 0:
@@ -462,11 +520,13 @@ def main():
     # baseline (rank 0, N = 1 only): the oracle port on this host's cores, bounded samples
     cpu = None
     parity = None
-    sums = [0.0, 0.0, 0.0, 0.0]  # compared frames, sum of avg EPE, max avg EPE, bit-exact frames
+    # compared frames, sum of avg EPE, max avg EPE, bit-exact distinct frames, frames of the batch bit-exact (a
+    # bit-exact distinct frame and every later tile of it that equals it on the device), frames in the batch
+    sums = [0.0, 0.0, 0.0, 0.0, 0.0, float(B)]
     if args.cpu_seconds > 0:
         from oracle import pyoracle as O
         q = oracle_params(O, p)
-        ncmp = max(1, min(nd, args.parity_frames)) if world == 1 else 1
+        ncmp = max(1, min(nd, args.parity_frames))
         for k in range(ncmp):
             ref = O.run_u8(pairs[k][0], pairs[k][1], q)
             g = timed_out[k]
@@ -474,15 +534,20 @@ def main():
             sums[0] += 1
             sums[1] += epe
             sums[2] = max(sums[2], epe)
-            sums[3] += int(np.array_equal(g.view(np.uint32), ref.view(np.uint32)))
+            exact = np.array_equal(g.view(np.uint32), ref.view(np.uint32))
+            sums[3] += int(exact)
+            sums[4] += (1 + tiles_equal[k]) if exact else 0
         if rank == 0 and world == 1:
             cpu = cpu_baseline(O, q, pairs, W, H, args.cpu_seconds, binary, args.config)
     if world > 1:
-        tot = odd.sum_over_ranks([sums[0], sums[1], sums[3]], dev)
-        sums = [tot[0], tot[1], odd.max_over_ranks(sums[2], dev), tot[2]]
+        tot = odd.sum_over_ranks([sums[0], sums[1], sums[3], sums[4], sums[5]], dev)
+        sums = [tot[0], tot[1], odd.max_over_ranks(sums[2], dev), tot[2], tot[3], tot[4]]
     if sums[0]:
         parity = {"avg_epe_vs_cpu_ref": sums[1] / sums[0], "avg_epe_vs_cpu_ref_max": sums[2],
-                  "bitexact_frames": int(sums[3]), "compared_frames": int(sums[0]), "checked": "timed pass output"}
+                  "bitexact_frames": int(sums[4]), "batch_frames": int(sums[5]),
+                  "oracle_compared_frames": int(sums[0]), "oracle_bitexact_frames": int(sums[3]),
+                  "checked": "timed pass output: the distinct pairs against the CPU oracle bit for bit, every other "
+                             "frame of the batch against its tile source on the device (int32 views, torch.equal)"}
 
     if rank == 0:
         line = {
@@ -502,7 +567,7 @@ def main():
                        "parallelism": f"frame-sharded x{world}" + (" (rehearsal: ranks share the GPU)"
                                                                    if rehearsal else "")},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,
-            "latency": latency, "host_io": host_io, "kernels": kernels,
+            "latency": latency, "host_io": host_io, "shard_of_8": shard8, "kernels": kernels,
         }
         if cpu:
             line["speedup_vs_cpu_1core"] = round(mpix / cpu["value"], 1)

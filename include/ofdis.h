@@ -196,11 +196,11 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        two-stream pipeline only under a HIP runtime >= 7.2: the one bundled with
  *                        PyTorch's ROCm 7.0 build crashes capturing its mutually waiting lanes, so there
  *                        it is issued eagerly); 3 captures the pipeline whatever the runtime (diagnostic);
- *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1) and "chunk" (frames, default 0 =
- *                        the batch split evenly over the streams): a batch is cut into chunks that run
+ *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1): a batch is cut into chunks that run
  *                        round-robin on that many HIP streams with separate workspaces, overlapping one
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
+ *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
  *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).

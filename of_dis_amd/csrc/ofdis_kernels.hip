@@ -3696,6 +3696,11 @@ struct SorLane {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const unsigned yr = (unsigned)(y + 64 * r);
+      // only the lanes whose pixel (d - yr, yr) is inside the frame load (exec mask): a plane row holds h slots,
+      // of which the folded layout gives the other lanes to diagonal d -+ w, so unmasked every slot was fetched
+      // (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels (the PMC fetch excess); the
+      // masked lanes keep stale register values, which every use discards by a select
+      if (!((unsigned)(d - (int)yr) < (unsigned)w && yr < (unsigned)h)) continue;
       if (FIRST || CRN == 0) {
         const float4 *cp = C + (size_t)r0 * CW;
         B.c0[r] = cp[yr * CW];
@@ -4384,8 +4389,14 @@ bool tv_smsys_ok(const TvArgs &a) {
 }
 // The derivative filters move into the system kernel only where the level runs the row-block k_tv_smsys and
 // k_tv_prepd (intensity images): the march, the 2-D tiles and the two-launch form read all eight planes.
+// Not where the 40 KB LDS cap of the DF form leaves fewer than 3 rows per block (levels of ~180-256 rows): a
+// block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
-  return a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024;
+  if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024))
+    return false;
+  int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
+  while (rb > 1 && smsys_lds_df(a.h, rb, true) > kSmsysDfCap) --rb;
+  return rb >= 3;
 }
 void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {

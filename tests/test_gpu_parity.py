@@ -447,3 +447,56 @@ def test_capture_on_large_batch(oracle, od, ctx):
         o = out.cpu().numpy()
         assert_bitexact(o[0], ref, "frame 0")
         assert_bitexact(o[n - 1], ref, "last frame")
+
+
+def test_large_batch_1080p_first_middle_last(oracle, od, ctx):
+    """2048 pairs of a 1080p op-point-2 pair in one call (the library's two 1024-pair chunks on two streams,
+    34 GB of output): the first, middle (both chunk edges) and last frames equal the oracle bit for bit, and
+    every frame equals frame 0 on the device (late-frame indexing and chunking at the bench's output size)."""
+    import torch
+    w, h, n = 1920, 1080, 2048
+    pa, pb = od.synth_pair(w, h, 1, 7, 1)
+    a = torch.from_numpy(pa).cuda().unsqueeze(0).expand(n, -1, -1, -1).contiguous()
+    b = torch.from_numpy(pb).cuda().unsqueeze(0).expand(n, -1, -1, -1).contiguous()
+    p = od.oppoint(2, w, 1, 1)
+    ctx.set_option("streams", 0)
+    ctx.set_option("chunk", 0)
+    out = ctx.run(a, b, p)
+    torch.cuda.synchronize()
+    del a, b
+    ref = oracle.run_u8(pa, pb, oracle.oppoint(2, w, 1, 1))
+    for f in (0, n // 2 - 1, n // 2, n - 1):
+        assert_bitexact(out[f].cpu().numpy(), ref, f"frame {f} of {n}")
+    ov = out.view(n, -1).view(torch.int32)
+    same = [int(torch.equal(ov[f], ov[0])) for f in range(n)]
+    assert sum(same) == n, [f for f in range(n) if not same[f]][:10]
+    del out, ov
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("deriv", [0, 1])
+def test_throughput_row_blocks_bitexact(oracle, od, ctx, deriv):
+    """A batch large enough that the fused system kernel takes its throughput row blocks (frames x row blocks
+    >= 4096: 1400 pairs of 160 x 120) with smsys_deriv on and off: every frame equals the oracle's bits (the
+    single-pair tests only ever see the latency-regime row blocks)."""
+    import torch
+    w, h, n, nd = 160, 120, 1400, 4
+    pairs = [od.synth_pair(w, h, 1, 11 + f, 1) for f in range(nd)]
+    a = torch.from_numpy(np.stack([pairs[i % nd][0] for i in range(n)])).cuda()
+    b = torch.from_numpy(np.stack([pairs[i % nd][1] for i in range(n)])).cuda()
+    p = od.oppoint(2, w, 1, 1)
+    q = oracle.oppoint(2, w, 1, 1)
+    ctx.set_option("smsys_deriv", deriv)
+    ctx.set_option("streams", 1)
+    try:
+        out = ctx.run(a, b, p)
+        torch.cuda.synchronize()
+        out = out.cpu().numpy()
+    finally:
+        ctx.set_option("smsys_deriv", 1)
+        ctx.set_option("streams", 0)
+    for i in range(nd):
+        ref = oracle.run_u8(pairs[i][0], pairs[i][1], q)
+        assert_bitexact(out[i], ref, f"frame {i}")
+    for f in range(nd, n):
+        assert_bitexact(out[f], out[f % nd], f"frame {f}")

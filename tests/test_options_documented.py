@@ -11,9 +11,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def runtime_options():
     src = open(os.path.join(ROOT, "of_dis_amd", "csrc", "ofdis_runtime.cpp")).read()
-    opts = re.findall(r'\{"(\w+)", &ofdis_context::opt_\w+, (-?\d+), (\d+)\}', src)
+    table = src[src.index("static const Opt opts[] = {"):]
+    table = table[:table.index("};")]
+    # the hi field may be an expression ("1 << 30"): evaluated as the C++ constant expression it is
+    opts = re.findall(r'\{"(\w+)", &ofdis_context::opt_\w+, (-?\d+), ([^}]+)\}', table)
     assert opts, "option table not found in ofdis_runtime.cpp"
-    return {k: (int(lo), int(hi)) for k, lo, hi in opts}
+    assert len(opts) == table.count("&ofdis_context::opt_"), "an option entry the pattern does not parse"
+    return {k: (int(lo), int(eval(hi, {"__builtins__": {}}))) for k, lo, hi in opts}
 
 
 def test_every_runtime_option_is_documented():
@@ -26,7 +30,7 @@ def test_documented_ranges_match():
     hdr = open(os.path.join(ROOT, "include", "ofdis.h")).read()
     for k, (lo, hi) in runtime_options().items():
         m = re.search(rf'^ \*\s+"{k}" \(([^)]*)\)', hdr, re.M)
-        if not m or k in ("streams", "graph"):  # ranges written in words there
+        if not m or k in ("streams", "graph", "chunk"):  # ranges written in words there
             continue
         vals = [int(v) for v in re.findall(r"-?\d+", m.group(1).split(",")[0])]
         if vals:
