@@ -201,6 +201,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
  *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
+ *   "tv_flow" (0/1, default 1): levels of up to 128 rows run each TV inner iteration (smoothness, system and
+ *                        the exact-order SOR) as one launch whose waves hand the diagonals to each other through
+ *                        LDS (no coefficient round trip through HBM; 0: the system and SOR launches);
  *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
@@ -220,6 +223,10 @@ int ofdis_context_enable_kernel_timing(ofdis_context *ctx, int enable);
 int ofdis_context_kernel_time(ofdis_context *ctx, const char *name, double *total_ms, long *launches);
 /* Comma-separated list of kernel names known to the timer. */
 const char *ofdis_kernel_names(void);
+
+/* Diagnostic: launches of the dataflow TV iteration (option "tv_flow") on `device` that hit their bounded wait
+ * and ended early since the last call (then reset); 0 in every correct run, < 0 on a HIP error. */
+int ofdis_flow_abort_count(int device);
 
 /* Per-frame algorithmic byte counts of the §8(d) byte model for this workload. */
 int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const char *kernel, double *bytes_per_frame);

@@ -35,11 +35,7 @@ typedef float float4_v __attribute__((ext_vector_type(4)));
 
 namespace {
 
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-__device__ __forceinline__ float stdmaxf(float a, float b) { return (a < b) ? b : a; }
-__device__ __forceinline__ float stdminf(float a, float b) { return (b < a) ? b : a; }
-__device__ __forceinline__ float ssemin(float a, float b) { return (a < b) ? a : b; }
-__device__ __forceinline__ float ssemax(float a, float b) { return (a > b) ? a : b; }
+#include "ofdis_tv_dev.inc"  // clampi, ssemin/max, skewed indexing, data term, smoothness, system
 
 inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
@@ -2021,23 +2017,11 @@ __global__ __launch_bounds__(256) void k_aggregate(AggArgs a) {
 
 // ------------------------------------------------------------------------------------------------ variational
 
-// Pixel (x, y) of a w x h level sits in row d = x + y (its anti-diagonal), column y.  With `wrap` (h <= w)
-// the rows are folded modulo w: row d mod w then holds exactly one pixel of every column, the plane has no
-// holes (w * h slots instead of (w + h - 1) * h) and the pixels of one wavefront step stay contiguous.
-__device__ __forceinline__ int skrow(int d, int w, int wrap) { return wrap && d >= w ? d - w : d; }
-__device__ __forceinline__ long skw(int x, int y, int h, int w, int wrap) {
-  return (long)skrow(x + y, w, wrap) * h + y;
-}
 
 // image_warp (opticalflow_aux.c:31-75) + the mean / temporal images of get_derivatives (:88-99), plus the
 // skewed copies of the level flow and du = dv = 0 (refine_variational.cpp:185-190).  Row-major threads.
 // image_warp (opticalflow_aux.c:31-75) + the t / It inputs of get_derivatives (:77-132) for pixel (x, y):
 // v = {mask, wx, wy, t[0..noc), dt[0..noc)}.
-// image_warp's mask (opticalflow_aux.c:47): 1 where the warped position (x + wx, y + wy) lies inside the level.
-__device__ __forceinline__ float warp_mask(int x, int y, float wx, float wy, int w, int h) {
-  const float xx = (float)x + wx, yy = (float)y + wy;
-  return (xx >= 0 && xx <= (float)(w - 1) && yy >= 0 && yy <= (float)(h - 1)) ? 1.0f : 0.0f;
-}
 __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, int f, float *v) {
   const long plane = (long)a.w * a.h;
   const long o = (long)y * a.w + x;
@@ -2115,8 +2099,6 @@ __global__ __launch_bounds__(256) void k_tv_prep(TvArgs a) {
   }
 }
 
-__constant__ float kK5[5] = {1.0f / 12.0f, -8.0f / 12.0f, -0.0f, 8.0f / 12.0f, -1.0f / 12.0f};
-__constant__ float kK3[3] = {-0.5f, -0.0f, 0.5f};
 
 // 5-tap filters (image.cpp:419-624 fast paths) with replicate border, on a skewed plane.
 __device__ __forceinline__ float conv5h(const float *s, int x, int y, int w, int h, int wr) {
@@ -2132,11 +2114,6 @@ __device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int
   return kK5[0] * s0 + ((kK5[1] * s1 + kK5[2] * s2) + (kK5[3] * s3 + kK5[4] * s4));
 }
 
-// Load base[idx] through a 32-bit byte offset on a wave-uniform base: global_load's SGPR-base form, no
-// 64-bit address arithmetic per load.  The runtime keeps every TV plane group below 2^30 floats.
-__device__ __forceinline__ float ldu(const float *base, unsigned idx) {
-  return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(base) + (size_t)(idx * 4u));
-}
 
 // ---- prep + derivatives in one launch (intensity images): image_warp and get_derivatives' t / It
 // (opticalflow_aux.c:31-132) on a row-major tile with a 4-pixel halo in LDS, the first derivatives Ix, Iy of t
@@ -2258,263 +2235,6 @@ __global__ __launch_bounds__(256) void k_tv_deriv2(TvArgs a) {
   if (kk < a.sp) tv_deriv2_px(a, b.y, kk);
 }
 
-#define DNORM (0.1f * 0.1f)
-#define EPSC (0.001f * 0.001f)
-
-// compute_data (opticalflow_aux.c:408-594), one pixel; p* point at the pixel in channel plane 0.
-__device__ __forceinline__ void data_of(int noc, long plane, float u, float v, float m, const float *Ix,
-                                        const float *Iy, const float *Iz, const float *Ixx, const float *Ixy,
-                                        const float *Iyy, const float *Ixz, const float *Iyz, float hdo3, float hgo3,
-                                        float &A11, float &A12, float &A22, float &B1, float &B2) {
-  A11 = 0.0f; A12 = 0.0f; A22 = 0.0f; B1 = 0.0f; B2 = 0.0f;
-  float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
-  if (noc == 1) {
-    if (hdo3 != 0.0f) {
-      tmpx = Ix[0]; tmpy = Iy[0];
-      tmp2 = (Iz[0] + tmpx * u) + tmpy * v;
-      n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
-      tmp = (tmp2 * tmp2) / n1;
-      tmp = (m * hdo3) / sqrtf(EPSC + 3.0f * tmp);
-      tmp3 = tmp / n1;
-      tmp2 = tmp3 * tmpx;
-      tmp3 = tmp3 * tmpy;
-      A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
-      B1 = B1 - tmp2 * Iz[0]; B2 = B2 - tmp3 * Iz[0];
-    }
-    tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
-    tmp2 = (Ixz[0] + tmpx * u) + tmpxy * v;
-    tmp3 = (Iyz[0] + tmpxy * u) + tmpy * v;
-    tmpxy = tmpxy * tmpxy;
-    n1 = (tmpxy + DNORM) + tmpx * tmpx;
-    n2 = (tmpxy + DNORM) + tmpy * tmpy;
-    tmp = (tmp2 * tmp2) / n1 + (tmp3 * tmp3) / n2;
-    tmp = (m * hgo3) / sqrtf(EPSC + 3.0f * tmp);
-    tmp2 = tmp / n2; tmp3 = tmp / n1;
-    tmpxy = Ixy[0];
-    A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
-    B1 = (B1 - (tmp3 * tmpx) * Ixz[0]) - (tmp2 * tmpxy) * Iyz[0];
-    B2 = (B2 - (tmp2 * tmpy) * Iyz[0]) - (tmp3 * tmpxy) * Ixz[0];
-    tmpxy = tmpxy * tmpxy;
-    A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
-    A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
-    A11 = A11 * 3.0f; A12 = A12 * 3.0f; A22 = A22 * 3.0f; B1 = B1 * 3.0f; B2 = B2 * 3.0f;
-    return;
-  }
-  const long o2 = plane, o3 = 2 * plane;
-  float n3, n4, n5, n6;
-  if (hdo3 != 0.0f) {
-    tmpx = Ix[0]; tmpy = Iy[0];
-    tmp2 = (Iz[0] + tmpx * u) + tmpy * v;
-    n1 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
-    tmp = (tmp2 * tmp2) / n1;
-    tmpx = Ix[o2]; tmpy = Iy[o2];
-    tmp2 = (Iz[o2] + tmpx * u) + tmpy * v;
-    n2 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
-    tmp = tmp + (tmp2 * tmp2) / n2;
-    tmpx = Ix[o3]; tmpy = Iy[o3];
-    tmp2 = (Iz[o3] + tmpx * u) + tmpy * v;
-    n3 = (DNORM + tmpx * tmpx) + tmpy * tmpy;
-    tmp = tmp + (tmp2 * tmp2) / n3;
-    tmp = (m * hdo3) / sqrtf(EPSC + tmp);
-    tmp3 = tmp / n3; tmp2 = tmp3 * tmpx; tmp3 = tmp3 * tmpy;
-    A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
-    B1 = B1 - tmp2 * Iz[o3]; B2 = B2 - tmp3 * Iz[o3];
-    tmpx = Ix[o2]; tmpy = Iy[o2];
-    tmp3 = tmp / n2; tmp2 = tmp3 * tmpx; tmp3 = tmp3 * tmpy;
-    A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
-    B1 = B1 - tmp2 * Iz[o2]; B2 = B2 - tmp3 * Iz[o2];
-    tmpx = Ix[0]; tmpy = Iy[o2];  // upstream slip: channel 2's Iy (opticalflow_aux.c:495-496)
-    tmp3 = tmp / n1; tmp2 = tmp3 * tmpx; tmp3 = tmp3 * tmpy;
-    A11 = A11 + tmp2 * tmpx; A12 = A12 + tmp2 * tmpy; A22 = A22 + tmp3 * tmpy;
-    B1 = B1 - tmp2 * Iz[0]; B2 = B2 - tmp3 * Iz[0];
-  }
-  tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
-  tmp2 = (Ixz[0] + tmpx * u) + tmpxy * v;
-  tmp3 = (Iyz[0] + tmpxy * u) + tmpy * v;
-  tmpxy = tmpxy * tmpxy;
-  n1 = (tmpxy + DNORM) + tmpx * tmpx;
-  n2 = (tmpxy + DNORM) + tmpy * tmpy;
-  tmp = (tmp2 * tmp2) / n1 + (tmp3 * tmp3) / n2;
-  tmpx = Ixx[o2]; tmpy = Iyy[o2]; tmpxy = Ixy[o2];
-  tmp2 = (Ixz[o2] + tmpx * u) + tmpxy * v;
-  tmp3 = (Iyz[o2] + tmpxy * u) + tmpy * v;
-  tmpxy = tmpxy * tmpxy;
-  n3 = (tmpxy + DNORM) + tmpx * tmpx;
-  n4 = (tmpxy + DNORM) + tmpy * tmpy;
-  tmp = (tmp2 * tmp2) / n3 + (tmp3 * tmp3) / n4;  // upstream overwrite (opticalflow_aux.c:519,529,538)
-  tmpx = Ixx[o3]; tmpy = Iyy[o3]; tmpxy = Ixy[o3];
-  tmp2 = (Ixz[o3] + tmpx * u) + tmpxy * v;
-  tmp3 = (Iyz[o3] + tmpxy * u) + tmpy * v;
-  tmpxy = tmpxy * tmpxy;
-  n5 = (tmpxy + DNORM) + tmpx * tmpx;
-  n6 = (tmpxy + DNORM) + tmpy * tmpy;
-  tmp = (tmp2 * tmp2) / n5 + (tmp3 * tmp3) / n6;
-  tmp = (m * hgo3) / sqrtf(EPSC + tmp);
-  tmp2 = tmp / n6; tmp3 = tmp / n5;
-  A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
-  A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
-  tmpxy = Ixy[o3];
-  A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
-  B1 = (B1 - (tmp3 * tmpx) * Ixz[o3]) - (tmp2 * tmpxy) * Iyz[o3];
-  B2 = (B2 - (tmp2 * tmpy) * Iyz[o3]) - (tmp3 * tmpxy) * Ixz[o3];
-  tmp2 = tmp / n4; tmp3 = tmp / n3;
-  tmpx = Ixx[o2]; tmpy = Iyy[o2]; tmpxy = Ixy[o2];
-  A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
-  B1 = (B1 - (tmp3 * tmpx) * Ixz[o2]) - (tmp2 * tmpxy) * Iyz[o2];
-  B2 = (B2 - (tmp2 * tmpy) * Iyz[o2]) - (tmp3 * tmpxy) * Ixz[o2];
-  tmpxy = tmpxy * tmpxy;
-  A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
-  A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
-  tmpx = Ixx[0]; tmpy = Iyy[0];
-  tmp2 = tmp / n2; tmp3 = tmp / n1;
-  tmpxy = Ixy[0];
-  A12 = A12 + ((tmp3 * tmpx) + tmp2 * tmpy) * tmpxy;
-  B1 = (B1 - (tmp3 * tmpx) * Ixz[0]) - (tmp2 * tmpxy) * Iyz[0];
-  B2 = (B2 - (tmp2 * tmpy) * Iyz[0]) - (tmp3 * tmpxy) * Ixz[0];
-  tmpxy = tmpxy * tmpxy;
-  A11 = (A11 + tmp3 * (tmpx * tmpx)) + tmp2 * tmpxy;
-  A22 = (A22 + tmp2 * (tmpy * tmpy)) + tmp3 * tmpxy;
-}
-
-// compute_data_DE (opticalflow_aux.c:601-747), one pixel.
-__device__ __forceinline__ void data_de(int noc, long plane, float u, float m, const float *Ix, const float *Iy,
-                                        const float *Iz, const float *Ixx, const float *Ixy, const float *Iyy,
-                                        const float *Ixz, const float *Iyz, float hdo3, float hgo3, float &A11,
-                                        float &B1) {
-  A11 = 0.0f; B1 = 0.0f;
-  float tmp, tmp2, tmp3, tmpx, tmpy, tmpxy, n1, n2;
-  if (noc == 1) {
-    if (hdo3 != 0.0f) {
-      tmpx = Ix[0]; tmpy = Iy[0];
-      tmp2 = Iz[0] + tmpx * u;
-      n1 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
-      tmp = (tmp2 * tmp2) / n1;
-      tmp = (m * hdo3) / sqrtf(EPSC + 3.0f * tmp);
-      tmp2 = (tmp / n1) * tmpx;
-      A11 = A11 + tmp2 * tmpx;
-      B1 = B1 - tmp2 * Iz[0];
-    }
-    tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
-    tmp2 = Iyz[0] + tmpxy * u;
-    tmpxy = DNORM + tmpxy * tmpxy;
-    n1 = tmpxy + tmpx * tmpx;
-    n2 = tmpxy + tmpy * tmpy;
-    tmp = (tmp2 * tmp2) / n2;
-    tmp2 = Ixz[0] + tmpx * u;
-    tmp = tmp + (tmp2 * tmp2) / n1;
-    tmp = (m * hgo3) / sqrtf(EPSC + 3.0f * tmp);
-    tmpxy = Ixy[0];
-    tmp2 = (tmp / n2) * tmpxy; tmp3 = (tmp / n1) * tmpx;
-    A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
-    B1 = (B1 - tmp3 * Ixz[0]) - tmp2 * Iyz[0];
-    A11 = A11 * 3.0f; B1 = B1 * 3.0f;
-    return;
-  }
-  const long o2 = plane, o3 = 2 * plane;
-  float n3, n4, n5, n6;
-  if (hdo3 != 0.0f) {
-    tmpx = Ix[0]; tmpy = Iy[0];
-    tmp2 = Iz[0] + tmpx * u;
-    n1 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
-    tmp = (tmp2 * tmp2) / n1;
-    tmpx = Ix[o2]; tmpy = Iy[o2];
-    tmp2 = Iz[o2] + tmpx * u;
-    n2 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
-    tmp = tmp + (tmp2 * tmp2) / n2;
-    tmpx = Ix[o3]; tmpy = Iy[o3];
-    tmp2 = Iz[o3] + tmpx * u;
-    n3 = (DNORM + tmpy * tmpy) + tmpx * tmpx;
-    tmp = tmp + (tmp2 * tmp2) / n3;
-    tmp = (m * hdo3) / sqrtf(EPSC + tmp);
-    tmp2 = (tmp / n3) * tmpx;
-    A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[o3];
-    tmpx = Ix[o2];
-    tmp2 = (tmp / n2) * tmpx;
-    A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[o2];
-    tmpx = Ix[0];
-    tmp2 = (tmp / n1) * tmpx;
-    A11 = A11 + tmp2 * tmpx; B1 = B1 - tmp2 * Iz[0];
-  }
-  tmpx = Ixx[0]; tmpy = Iyy[0]; tmpxy = Ixy[0];
-  tmp2 = Iyz[0] + tmpxy * u;
-  tmpxy = DNORM + tmpxy * tmpxy;
-  n1 = tmpxy + tmpx * tmpx;
-  n2 = tmpxy + tmpy * tmpy;
-  tmp = (tmp2 * tmp2) / n2;
-  tmp2 = Ixz[0] + tmpx * u;
-  tmp = tmp + (tmp2 * tmp2) / n1;
-  tmpx = Ixx[o2]; tmpy = Iyy[o2]; tmpxy = Ixy[o2];
-  tmp2 = Iyz[o2] + tmpxy * u;
-  tmpxy = DNORM + tmpxy * tmpxy;
-  n3 = tmpxy + tmpx * tmpx;
-  n4 = tmpxy + tmpy * tmpy;
-  tmp = tmp + (tmp2 * tmp2) / n4;
-  tmp2 = Ixz[o2] + tmpx * u;
-  tmp = tmp + (tmp2 * tmp2) / n3;
-  tmpx = Ixx[o3]; tmpy = Iyy[o3]; tmpxy = Ixy[o3];
-  tmp2 = Iyz[o3] + tmpxy * u;
-  tmpxy = DNORM + tmpxy * tmpxy;
-  n5 = tmpxy + tmpx * tmpx;
-  n6 = tmpxy + tmpy * tmpy;
-  tmp = tmp + (tmp2 * tmp2) / n6;
-  tmp2 = Ixz[o3] + tmpx * u;
-  tmp = tmp + (tmp2 * tmp2) / n5;
-  tmp = (m * hgo3) / sqrtf(EPSC + tmp);
-  tmpxy = Ixy[o3];
-  tmp2 = (tmp / n6) * tmpxy; tmp3 = (tmp / n5) * tmpx;
-  A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
-  B1 = (B1 - tmp3 * Ixz[o3]) - tmp2 * Iyz[o3];
-  tmpx = Ixx[o2]; tmpxy = Ixy[o2];
-  tmp2 = (tmp / n4) * tmpxy; tmp3 = (tmp / n3) * tmpx;
-  A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
-  B1 = (B1 - tmp3 * Ixz[o2]) - tmp2 * Iyz[o2];
-  tmpx = Ixx[0]; tmpxy = Ixy[0];
-  tmp2 = (tmp / n2) * tmpxy; tmp3 = (tmp / n1) * tmpx;
-  A11 = (A11 + tmp3 * tmpx) + tmp2 * tmpxy;
-  B1 = (B1 - tmp3 * Ixz[0]) - tmp2 * Iyz[0];
-}
-
-// uu / vv of the current inner iteration (refine_variational.cpp:189-190,209-222,305-320)
-
-// s of one pixel from (wx, du, wy, dv) of the pixel and its clamped 4-neighbourhood (centre, left, right,
-// up, down): the arithmetic of compute_smoothness (opticalflow_aux.c:138-160) on uu = wx + du.
-// uu (and vv) of one pixel: wx on the first inner iteration, else wx + du (DE: clamped to the camera side)
-template <int NOP>
-__device__ __forceinline__ float smooth_uu(const TvArgs &a, bool first, float wx, float du) {
-  if (NOP == 2) return first ? wx : wx + du;
-  return first ? wx : (a.camlr == 0 ? ssemin(wx + du, 0.0f) : ssemax(wx + du, 0.0f));
-}
-template <int NOP>
-__device__ __forceinline__ float smooth_from_uu(const TvArgs &a, const float (&uu5)[5], const float (&vv5)[5]);
-template <int NOP>
-__device__ __forceinline__ float smooth_compute(const TvArgs &a, bool first, const float (&wx5)[5],
-                                             const float (&du5)[5], const float (&wy5)[5], const float (&dv5)[5]) {
-  float uu5[5], vv5[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    uu5[i] = smooth_uu<NOP>(a, first, wx5[i], du5[i]);
-    vv5[i] = NOP == 2 ? smooth_uu<2>(a, first, wy5[i], dv5[i]) : 0.0f;
-  }
-  return smooth_from_uu<NOP>(a, uu5, vv5);
-}
-// the rest of compute_smoothness from the clamped 5-neighbourhood of uu (centre, left, right, up, down)
-template <int NOP>
-__device__ __forceinline__ float smooth_from_uu(const TvArgs &a, const float (&uu5)[5], const float (&vv5)[5]) {
-  const float uc = uu5[0];
-  const float ux = kK3[0] * uu5[1] + (kK3[1] * uc + kK3[2] * uu5[2]);
-  const float uy = kK3[0] * uu5[3] + (kK3[1] * uc + kK3[2] * uu5[4]);
-  float vx, vy;
-  if (NOP == 2) {
-    const float vc = vv5[0];
-    vx = kK3[0] * vv5[1] + (kK3[1] * vc + kK3[2] * vv5[2]);
-    vy = kK3[0] * vv5[3] + (kK3[1] * vc + kK3[2] * vv5[4]);
-  } else {  // wy_dummy = 0 (refine_variational.cpp:268,294)
-    vx = kK3[0] * 0.0f + (kK3[1] * 0.0f + kK3[2] * 0.0f);
-    vy = vx;
-  }
-  const float eps = 0.001f * 0.001f;
-  return a.quarter_alpha / sqrtf(eps + ((ux * ux + uy * uy) + (vx * vx + vy * vy)));
-}
 
 // compute_smoothness (opticalflow_aux.c:138-160): s = (alpha/4) / sqrt(eps + |grad u|^2 + |grad v|^2)
 template <int NOP>
@@ -2541,70 +2261,6 @@ __device__ __forceinline__ void tv_smooth_px(const TvArgs &a, long fr, int kk, b
   a.s[idx] = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
 }
 
-// The system of one pixel from its gathered inputs (s, wx, wy of the pixel and its 4-neighbourhood in the
-// order centre, left, right, up, down; mask; du, dv; the derivative images).  Neighbours that do not exist
-// (hasl ... hasd false) may hold any value: every use of them is behind a select.  OF: c0 = (a11, a12,
-// a12, a22) (the inverse sor_coupled's first sweep computes, see below), c1 = (b1, b2, sh, sv); DE: c0 =
-// (a11, b1, sh, sv).
-template <int NOP, int NOC>
-__device__ __forceinline__ void sys_compute(const TvArgs &a, int x, int y, const float (&S5)[5], const float (&X5)[5],
-                                            const float (&Y5)[5], float m, float u, float v, const float (&lIx)[NOC],
-                                            const float (&lIy)[NOC], const float (&lIz)[NOC], const float (&lIxx)[NOC],
-                                            const float (&lIxy)[NOC], const float (&lIyy)[NOC],
-                                            const float (&lIxz)[NOC], const float (&lIyz)[NOC], float4 &c0,
-                                            float4 &c1) {
-  const int w = a.w, h = a.h;
-  const bool hasl = x >= 1, hasr = x <= w - 2, hasu = y >= 1, hasd = y <= h - 2;
-  const float sc = S5[0], sl = S5[1], sr = S5[2], su = S5[3], sd = S5[4];
-  const float xc = X5[0], xl = X5[1], xr = X5[2], xu = X5[3], xd = X5[4];
-  const float yc = Y5[0], yl = Y5[1], yr = Y5[2], yu = Y5[3], yd = Y5[4];
-  const float shv = x < w - 1 ? sc + sr : 0.0f;  // h[x] = s[x] + s[x+1]
-  const float svv = y < h - 1 ? sc + sd : 0.0f;  // v[y] = s[y] + s[y+1]
-  float A11, A12 = 0.0f, A22 = 0.0f, B1, B2 = 0.0f;
-  if (NOP == 2)
-    data_of(NOC, 1, u, v, m, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz, lIyz, a.hdo3, a.hgo3, A11, A12, A22, B1, B2);
-  else
-    data_de(NOC, 1, u, m, lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz, lIyz, a.hdo3, a.hgo3, A11, B1);
-  // b = ((((b - th[x-1]) + th[x]) - tv[y-1]) + tv[y]) with th[x] = h[x] (wx[x+1] - wx[x]) etc.
-  B1 = hasl ? B1 - (sl + sc) * (xc - xl) : B1;
-  B1 = hasr ? B1 + shv * (xr - xc) : B1;
-  B1 = hasu ? B1 - (su + sc) * (xc - xu) : B1;
-  B1 = hasd ? B1 + svv * (xd - xc) : B1;
-  if (NOP == 2) {
-    B2 = hasl ? B2 - (sl + sc) * (yc - yl) : B2;
-    B2 = hasr ? B2 + shv * (yr - yc) : B2;
-    B2 = hasu ? B2 - (su + sc) * (yc - yu) : B2;
-    B2 = hasd ? B2 + svv * (yd - yc) : B2;
-    // sor_coupled's first sweep replaces a11/a12/a22 by the inverse of [[a11+d, a12], [a12, a22+d]] with
-    // d = the sum of the four diffusivities (solver.c:122-128, border forms :131-190).  It depends on the
-    // system only, so it is computed here, fully parallel, with the same expressions; every SOR sweep then
-    // reads the inverse.  (w < 2 or h < 2 run the point-SOR fallback on the raw matrix, solver.c:34-78.)
-    if (w >= 2 && h >= 2 && !a.sor_point) {
-      const float hl = x > 0 ? sl + sc : 0.0f;  // h[x-1]
-      const float vt = su + sc;                  // v[y-1] (y > 0)
-      const float dpsis = y == 0 ? hl + (shv + svv) : (y < h - 1 ? (hl + shv) + (vt + svv) : hl + (shv + vt));
-      const float M11 = A22 + dpsis, M22 = A11 + dpsis;
-      const float det = M11 * M22 - A12 * A12;
-      A11 = M11 / det;
-      A22 = M22 / det;
-      A12 = A12 / (0.0f - det);
-    }
-    c0 = make_float4(A11, A12, A12, A22);  // (a11, a12) and (a12, a22) pair up for packed fp32
-    c1 = make_float4(B1, B2, shv, svv);
-  } else {
-    // the DE point SOR's diagonal a11 + (the four diffusivities of the pixel's existing neighbours), summed in
-    // its order (top, left, bottom, right; solver.c's DE branch) -- it depends on the system only, so it is
-    // computed here once instead of in every sweep (the SOR kernels read A = c0.x); vt / hl are the upper /
-    // left pixel's sv / sh with the same operands, and sv / sh of a missing bottom / right neighbour are 0
-    float dsum = 0.0f;
-    if (y > 0) dsum = dsum + (su + sc);
-    if (x > 0) dsum = dsum + (sl + sc);
-    if (y < h - 1) dsum = dsum + svv;
-    if (x < w - 1) dsum = dsum + shv;
-    c0 = make_float4(A11 + dsum, B1, shv, svv);
-    c1 = c0;
-  }
-}
 
 // One TV inner iteration's system (refine_variational.cpp:195-199): diffusivities from s
 // (opticalflow_aux.c:161-184), data term (:408-747) and sub_laplacian (:194-223).
@@ -3182,14 +2838,6 @@ __global__ __launch_bounds__(256) void k_tv_sor(TvArgs a) {
 #undef SV_
 }
 
-// Lane i <- lane i-1 (wave_shr:1) / lane i+1 (wave_shl:1).  bound_ctrl: the lane without a source reads 0
-// (its value is never used: border selects / cross-wave LDS values replace it), so no "old" register.
-__device__ __forceinline__ float dpp_from_prev_lane(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float dpp_from_next_lane(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
-}
 
 #ifdef OFDIS_SOR_PROBE
 // Step-timing probe of the sweep-per-wave SOR (a separate build, tools/sor_probe.py; never in libofdis.so):
@@ -3205,19 +2853,6 @@ struct SorPix {
   float i11, i12, i22, b1, b2, hl, hr, vv, vt;
 };
 
-// The three border variants of solver.c's block-SOR right-hand side as ONE branch-free expression tree.
-// The reference evaluates (first row / last row / interior, solver.c:131-190 and :241-300)
-//   top:      s = (b + X) + Z
-//   bottom:   s = (b + X) + Y
-//   interior: s = (X + Y) + (b + Z)
-// with X = hr*u_right, Y = vt*u_top, Z = vv*u_bottom.  Selecting operands (and -0.0f, the exact additive
-// identity of IEEE round-to-nearest: -0 + x == x bit-for-bit, x = +-0 included) reproduces every variant
-// exactly, so a wave never splits into per-lane branches.
-__device__ __forceinline__ float sor_rhs(bool border, bool notop, float b, float X, float Y, float Z) {
-  const float l = X + (border ? b : Y);
-  const float r = (border ? -0.0f : b) + (border ? (notop ? Z : Y) : Z);
-  return l + r;
-}
 // ---------------------------------------------------------------------------------- red-black SOR (opt-in)
 // The throughput mode of SURVEY §7 4(ii): the same per-pixel block SOR update as sor_coupled (2x2 inverse
 // precomputed by the system kernel, solver.c's right-hand-side trees via sor_rhs) but in red-black order --
@@ -3614,7 +3249,6 @@ __device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
   return min(dd >= lim ? dd - lim : dd, rmax);
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
 
 // Sweep-per-wave exact-order SOR, one row per lane.  Same wavefront as SorPipe (pixel (x, y) of sweep s at
 // step t = x + y + 2 s), but the S sweeps run on S different waves of the workgroup: wave (g, s) owns rows
@@ -3695,12 +3329,13 @@ struct SorLane {
     const unsigned r1 = FIRST ? (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane : 0u;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const unsigned yr = (unsigned)(y + 64 * r);
-      // only the lanes whose pixel (d - yr, yr) is inside the frame load (exec mask): a plane row holds h slots,
-      // of which the folded layout gives the other lanes to diagonal d -+ w, so unmasked every slot was fetched
-      // (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels (the PMC fetch excess); the
-      // masked lanes keep stale register values, which every use discards by a select
-      if (!((unsigned)(d - (int)yr) < (unsigned)w && yr < (unsigned)h)) continue;
+      // only the lanes whose pixel (d - yr, yr) is inside the frame fetch their own slot: a plane row holds h
+      // slots, of which the folded layout gives the others to diagonal d -+ w, so every slot was fetched
+      // (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels (the PMC fetch excess).  The
+      // other lanes read the row's first slot (one line they share; every use of their values is discarded by a
+      // select).  A select, not an exec-masked load: loads under a branch cost the prefetch (the wait-count pass
+      // then waits for them at the join, measured: tv_sor 135 -> 166 us per launch).
+      const unsigned yr = ((unsigned)(d - (y + 64 * r)) < (unsigned)w && y + 64 * r < h) ? (unsigned)(y + 64 * r) : 0u;
       if (FIRST || CRN == 0) {
         const float4 *cp = C + (size_t)r0 * CW;
         B.c0[r] = cp[yr * CW];
@@ -4392,6 +4027,7 @@ bool tv_smsys_ok(const TvArgs &a) {
 // Not where the 40 KB LDS cap of the DF form leaves fewer than 3 rows per block (levels of ~180-256 rows): a
 // block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
+  if (tv_flow_ok(a)) return false;  // the dataflow iteration reads all eight derivative planes
   if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024))
     return false;
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);

@@ -26,7 +26,7 @@ using namespace ofdis;
 namespace {
 
 const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample"};
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_flow"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -96,6 +96,7 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
+  int opt_tv_flow = 1;         // one dataflow launch per TV inner iteration (k_tv_flow) where it fits
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
@@ -512,6 +513,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
+      tv.tv_flow = c->opt_tv_flow;
+      tv.flow_err = tv_flow_err_counter();
       tv.smsys_deriv = tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
@@ -522,8 +525,13 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
           launch_tv_deriv2(tv, s);
         });
       }
+      const bool flow = tv_flow_ok(tv);
       for (int it = 0; it < n_inner; ++it) {
         tv.first_iter = it == 0;
+        if (flow) {  // smoothness + system + SOR of the iteration in one launch, intermediates in LDS
+          timed(c, 11, s, [&] { launch_tv_flow(tv, s); });
+          continue;
+        }
         timed(c, 7, s, [&] {
           if (tv_smsys_ok(tv)) {
             launch_tv_smsys(tv, s);
@@ -1231,6 +1239,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
+      {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {
@@ -1264,6 +1273,11 @@ int ofdis_context_kernel_time(ofdis_context *c, const char *name, double *total_
   if (total_ms) *total_ms = it == c->acc.end() ? 0.0 : it->second.first;
   if (launches) *launches = it == c->acc.end() ? 0 : it->second.second;
   return OFDIS_OK;
+}
+
+int ofdis_flow_abort_count(int device) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  return tv_flow_err_take();
 }
 
 const char *ofdis_kernel_names(void) {

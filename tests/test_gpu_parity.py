@@ -38,6 +38,9 @@ def ctx(od):
     c = od.Context(0)
     yield c
     c.close()
+    # no dataflow TV launch of this module ended on its bounded wait (a protocol error would also show as a
+    # parity failure; this names it)
+    assert od.lib().ofdis_flow_abort_count(0) == 0
 
 
 CASES = [
@@ -123,6 +126,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
     ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
     ("patch_quad", 0, 1),      # gray p = 8 / 12 on eight lanes per patch (k_patchw) instead of four (k_patchq)
+    ("tv_flow", 0, 1),         # levels <= 128 rows: system + SOR launches instead of the dataflow iteration
 ]
 
 
