@@ -40,11 +40,11 @@ namespace {
 
 #include "ofdis_tv_dev.inc"
 
-constexpr int kFlowRR = 8;   // row ring slots (rows e - 1 .. e + 2 live, + the SOR's lag)
-constexpr int kFlowRS = 8;   // s ring slots
-constexpr int kFlowRC = 10;  // coefficient ring slots
-constexpr int kFlowD = 4;    // (u, v) ring slots per sweep
-constexpr int kFlowK = 4;    // M's global-load prefetch depth (rows)
+constexpr int kFlowRR = 16;  // row ring slots: M runs up to RR - 5 rows ahead of sweep 0
+constexpr int kFlowRS = 16;  // s ring slots
+constexpr int kFlowRC = 16;  // coefficient ring slots: the system runs up to RC - 2 diagonals ahead of the last sweep
+constexpr int kFlowD = 6;    // (u, v) ring slots per sweep
+constexpr int kFlowK = 4;    // M's global loads in flight (rows; two per iteration)
 constexpr int kFlowSpinLimit = 1 << 22;
 
 // Progress counters live in LDS.  Release = every earlier LDS write of the wave has completed before the counter
@@ -59,6 +59,15 @@ __device__ __forceinline__ void cnt_publish(int *p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void cnt_acquire() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// The fast forms the SOR waves use.  A wave's LDS instructions are performed in issue order, so (1) a counter store
+// issued after the ring stores it publishes is seen after them without waiting for them, and (2) ring reads issued
+// after the counter read (in the same round trip) see at least the state the counter showed: a poll that finds its
+// counters ready has its operands too.  The empty asm keeps the compiler from reordering the LDS accesses.
+__device__ __forceinline__ void cnt_publish_ordered(int *p, int v) {
+  asm volatile("" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 template <int NOP, int NOC, int S, int G, int P>
 struct Flow {
@@ -148,55 +157,64 @@ struct Flow {
     return q;
   }
 
-  // iteration e: row e + 1 into the ring (R[Q] holds it), the load of row e + 1 + K, s of diagonal e
-  template <int Q>
-  __device__ __forceinline__ bool m_step(int e, int g, int y, float4 (&R)[kFlowK]) {
-    if (e >= E) return true;
-    // the row slot's previous row (e + 1 - RR) is read last by sweep 0 at diagonal e + 1 - RR and the system of
-    // diagonal e + 2 - RR: every sweep-0 wave done with diagonal e + 2 - RR
-    if (!wait([&](auto &C) { return cmin(C, C_SOR) >= e + 3 - kFlowRR; })) return false;
-    row[((e + 1) % kFlowRR) * NR + y + 1] = R[Q];
-    cnt_publish(cnt + C_M + g, e + 2);  // rows 0 .. e + 1 written
-    R[Q] = load_row(e + 1 + kFlowK, y);
-    // the neighbouring groups' rows e + 1 (lanes y -+ 1 at the group edges)
-    if (G > 1 && !wait([&](auto &C) {
-          return (g == 0 || C(C_M + g - 1) >= e + 2) && (g == G - 1 || C(C_M + g + 1) >= e + 2);
-        }))
-      return false;
+  // s of diagonal e at lane y from rows e - 1, e, e + 1 of the ring (compute_smoothness's replicate border: an
+  // absent neighbour is the centre); 0 outside the level
+  __device__ __forceinline__ float smooth_at(int e, int y) const {
     const int x = e - y;
-    const float4 q1 = row[(e % kFlowRR) * NR + y + 1];                            // centre
-    const float4 ql = row[((e + kFlowRR - 1) % kFlowRR) * NR + y + 1];            // left  (x - 1, y)
-    const float4 qu = row[((e + kFlowRR - 1) % kFlowRR) * NR + y];                // up    (x, y - 1)
-    const float4 qr = row[((e + 1) % kFlowRR) * NR + y + 1];                      // right (x + 1, y)
-    const float4 qd = row[((e + 1) % kFlowRR) * NR + y + 2];                      // down  (x, y + 1)
+    const float4 q1 = row[(e % kFlowRR) * NR + y + 1];                  // centre
+    const float4 ql = row[((e + kFlowRR - 1) % kFlowRR) * NR + y + 1];  // left  (x - 1, y)
+    const float4 qu = row[((e + kFlowRR - 1) % kFlowRR) * NR + y];      // up    (x, y - 1)
+    const float4 qr = row[((e + 1) % kFlowRR) * NR + y + 1];            // right (x + 1, y)
+    const float4 qd = row[((e + 1) % kFlowRR) * NR + y + 2];            // down  (x, y + 1)
     float sv = 0.0f;
-    if ((unsigned)x < (unsigned)w && y < h) {  // compute_smoothness's replicate border: absent -> the centre
+    if ((unsigned)x < (unsigned)w && y < h) {
       const bool l = x > 0, r = x < w - 1, u = y > 0, dn = y < h - 1;
       const float4 L = l ? ql : q1, Rt = r ? qr : q1, U = u ? qu : q1, D = dn ? qd : q1;
       const float wx5[5] = {q1.x, L.x, Rt.x, U.x, D.x}, du5[5] = {q1.z, L.z, Rt.z, U.z, D.z};
       const float wy5[5] = {q1.y, L.y, Rt.y, U.y, D.y}, dv5[5] = {q1.w, L.w, Rt.w, U.w, D.w};
       sv = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
     }
-    sr[(e % kFlowRS) * NR + y + 1] = sv;
-    cnt_publish(cnt + C_S + g, e + 1);
-    return true;
+    return sv;
   }
+  // iteration e (even): rows e + 3, e + 4 into the ring (R[2Q], R[2Q + 1] hold them), the loads of rows e + 3 + K,
+  // e + 4 + K, and s of diagonals e, e + 1 (rows e - 1 .. e + 2, written by every M wave two iterations ago)
   template <int Q>
-  __device__ __forceinline__ bool m_block(int e, int g, int y, float4 (&R)[kFlowK]) {
-    if (!m_step<Q>(e + Q, g, y, R)) return false;
-    if constexpr (Q + 1 < kFlowK) return m_block<Q + 1>(e, g, y, R);
+  __device__ __forceinline__ bool m_step(int e, int g, int y, float4 (&R)[kFlowK]) {
+    if (e >= E) return true;
+    // WAR: row e + 4 replaces row e + 4 - RR, read last by the system of diagonal e + 5 - RR (done once sweep 0 is
+    // past it); the neighbouring groups' rows <= e + 2 (lanes y -+ 1 at the group edges)
+    if (!wait([&](auto &C) {
+          bool ok = cmin(C, C_SOR) >= e + 6 - kFlowRR;
+          if (G > 1) ok = ok && (g == 0 || C(C_M + g - 1) >= e + 3) && (g == G - 1 || C(C_M + g + 1) >= e + 3);
+          return ok;
+        }))
+      return false;
+    row[((e + 3) % kFlowRR) * NR + y + 1] = R[2 * Q];
+    row[((e + 4) % kFlowRR) * NR + y + 1] = R[2 * Q + 1];
+    R[2 * Q] = load_row(e + 3 + kFlowK, y);
+    R[2 * Q + 1] = load_row(e + 4 + kFlowK, y);
+    const float s0 = smooth_at(e, y);
+    const float s1 = e + 1 < E ? smooth_at(e + 1, y) : 0.0f;
+    sr[(e % kFlowRS) * NR + y + 1] = s0;
+    sr[((e + 1) % kFlowRS) * NR + y + 1] = s1;
+    cnt_publish_ordered(cnt + C_M + g, e + 5);                     // rows 0 .. e + 4 written
+    cnt_publish_ordered(cnt + C_S + g, e + 2 < E ? e + 2 : E);     // s of diagonals 0 .. e + 1
     return true;
   }
   __device__ void run_m(int g, int lane) {
+    __builtin_amdgcn_s_setprio(2);
     const int y = 64 * g + lane;
-    // row 0 first, then rows 1 .. K in flight; R[Q] of block iteration e + Q holds row e + Q + 1
     row[0 * NR + y + 1] = load_row(0, y);
-    cnt_publish(cnt + C_M + g, 1);
-    float4 R[kFlowK];
+    row[1 * NR + y + 1] = load_row(1, y);
+    row[2 * NR + y + 1] = load_row(2, y);
+    cnt_publish_ordered(cnt + C_M + g, 3);
+    float4 R[kFlowK];  // rows 3 .. 3 + K - 1 in flight; iteration e consumes R[2Q], R[2Q + 1], Q = (e / 2) % 2
 #pragma unroll
-    for (int k = 0; k < kFlowK; ++k) R[k] = load_row(k + 1, y);
-    for (int e = 0; e < E; e += kFlowK)
-      if (!m_block<0>(e, g, y, R)) return;
+    for (int k = 0; k < kFlowK; ++k) R[k] = load_row(k + 3, y);
+    for (int e = 0; e < E; e += 4) {
+      if (!m_step<0>(e, g, y, R)) return;
+      if (!m_step<1>(e + 2, g, y, R)) return;
+    }
   }
 
   // ------------------------------------------------------------------------------------------------ Y
@@ -240,10 +258,11 @@ struct Flow {
     float4 *C = coef + (d % kFlowRC) * CW * NR + y + 1;
     C[0] = c0;
     if (NOP == 2) C[NR] = c1;
-    cnt_publish(cnt + C_Y + j * G + g, d + 1);
+    cnt_publish_ordered(cnt + C_Y + j * G + g, d + 1);
     return true;
   }
   __device__ void run_y(int g, int j, int lane) {
+    __builtin_amdgcn_s_setprio(0);
     const int y = 64 * g + lane;
     Der b0, b1;
     load_der(j, y, b0);
@@ -266,50 +285,70 @@ struct Flow {
     float phr = 0.0f, pvv = 0.0f;
     f2v *ring_s = uv + SI * kFlowD * NR;
     const f2v *ring_p = uv + (SI > 0 ? SI - 1 : 0) * kFlowD * NR;
+    __builtin_amdgcn_s_setprio(3);
+    const int lane63 = threadIdx.x & 63;
     for (int d = 0; d < E; ++d) {
       const int dn = d + 2 < E ? d + 2 : E;
-      if (!wait([&](auto &C) {
-            bool ok;
-            if (FIRST) {
-              ok = C(C_Y + (d % P) * G + g) >= d + 1;
-            } else {
-              ok = C(C_SOR + (SI - 1) * G + g) >= dn;
-              if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + (SI - 1) * G + g + 1) >= dn;
-            }
-            if (G > 1 && g > 0) ok = ok && C(C_SOR + SI * G + g - 1) >= d;  // top of lane 0: diagonal d - 1
-            if (!LAST) {
-              // WAR: this ring slot's diagonal d - D is read by sweep SI + 1 of this group as its own (at d - D)
-              // and right / bottom values (at d - D - 1), by sweep SI + 1 of the group above as lane 63's bottom
-              ok = ok && C(C_SOR + (SI + 1) * G + g) >= d - kFlowD + 1;
-              if (G > 1 && g > 0) ok = ok && C(C_SOR + (SI + 1) * G + g - 1) >= d - kFlowD;
-            }
-            // ... and by this sweep's group below as lane 0's top (at d - D + 1)
-            if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + SI * G + g + 1) >= d - kFlowD + 2;
-            return ok;
-          }))
-        return;
       const int x = d - y;
       const bool hasl = x > 0, hasr = x < w - 1;
-      f2v o, rgt, bt;
-      if (FIRST) {
-        const float4 r0 = row[(d % kFlowRR) * NR + y + 1];
-        const float4 r1 = row[((d + 1) % kFlowRR) * NR + y + 1], r2 = row[((d + 1) % kFlowRR) * NR + y + 2];
-        o = f2v{r0.z, r0.w};
-        rgt = f2v{r1.z, r1.w};
-        bt = f2v{r2.z, r2.w};
-      } else {
-        o = ring_p[(d % kFlowD) * NR + y + 1];
-        rgt = ring_p[((d + 1) % kFlowD) * NR + y + 1];
-        bt = ring_p[((d + 1) % kFlowD) * NR + y + 2];
+      const int dm = (d + kFlowD - 1) % kFlowD, cm = (d + kFlowRC - 1) % kFlowRC;
+      f2v o, rgt, bt, tpl;
+      float4 c0, c1;
+      float tsvl;
+      // one LDS round trip per poll: the counters, then (in issue order) the operands -- valid once they hold
+      for (int spin = 0;; ++spin) {
+        const int v = cnt_load(cnt + (lane63 < NCNT ? lane63 : 0));
+        lds_order();
+        if (FIRST) {
+          const float4 r0 = row[(d % kFlowRR) * NR + y + 1];
+          const float4 r1 = row[((d + 1) % kFlowRR) * NR + y + 1], r2 = row[((d + 1) % kFlowRR) * NR + y + 2];
+          o = f2v{r0.z, r0.w};
+          rgt = f2v{r1.z, r1.w};
+          bt = f2v{r2.z, r2.w};
+        } else {
+          o = ring_p[(d % kFlowD) * NR + y + 1];
+          rgt = ring_p[((d + 1) % kFlowD) * NR + y + 1];
+          bt = ring_p[((d + 1) % kFlowD) * NR + y + 2];
+        }
+        const float4 *Cp = coef + (d % kFlowRC) * CW * NR + y + 1;
+        c0 = Cp[0];
+        c1 = MODE == 0 ? Cp[NR] : c0;
+        if (G > 1) {  // lane 0 of a lower row group: the row above is the group above's
+          tpl = ring_s[dm * NR + y];
+          tsvl = coef[(cm * CW + CW - 1) * NR + y].w;
+        }
+        lds_order();
+        auto C = [&](int i) { return __builtin_amdgcn_readlane(v, i); };
+        bool ok;
+        if (FIRST) {
+          ok = C(C_Y + (d % P) * G + g) >= d + 1;
+        } else {
+          ok = C(C_SOR + (SI - 1) * G + g) >= dn;
+          if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + (SI - 1) * G + g + 1) >= dn;
+        }
+        if (G > 1 && g > 0) ok = ok && C(C_SOR + SI * G + g - 1) >= d;  // top of lane 0: diagonal d - 1
+        if (!LAST) {
+          // WAR: this ring slot's diagonal d - D is read by sweep SI + 1 of this group as its own (at d - D) and
+          // right / bottom values (at d - D - 1), by sweep SI + 1 of the group above as lane 63's bottom
+          ok = ok && C(C_SOR + (SI + 1) * G + g) >= d - kFlowD + 1;
+          if (G > 1 && g > 0) ok = ok && C(C_SOR + (SI + 1) * G + g - 1) >= d - kFlowD;
+        }
+        // ... and by this sweep's group below as lane 0's top (at d - D + 1)
+        if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + SI * G + g + 1) >= d - kFlowD + 2;
+        if (ok) break;
+        if (C(C_ABORT)) return;
+        if (spin > kFlowSpinLimit) {
+          cnt_publish(cnt + C_ABORT, 1);
+          if (lane63 == 0 && a.flow_err) atomicAdd(a.flow_err, 1);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      const float4 *C = coef + (d % kFlowRC) * CW * NR + y + 1;
-      const float4 c0 = C[0], c1 = MODE == 0 ? C[NR] : c0;
       f2v tp = f2v{dpp_from_prev_lane(pp.x), MODE == 0 ? dpp_from_prev_lane(pp.y) : 0.0f};
       float tsv = dpp_from_prev_lane(pvv);
-      if (top_lds) {
-        const int dm = (d + kFlowD - 1) % kFlowD, cm = (d + kFlowRC - 1) % kFlowRC;
-        tp = ring_s[dm * NR + y];
-        tsv = coef[(cm * CW + CW - 1) * NR + y].w;
+      if (G > 1 && top_lds) {
+        tp = tpl;
+        tsv = tsvl;
       }
       f2v nw;
       float vv;
@@ -348,7 +387,7 @@ struct Flow {
       }
       pp = nw;
       pvv = vv;
-      cnt_publish(cnt + C_SOR + SI * G + g, d + 1);
+      cnt_publish_ordered(cnt + C_SOR + SI * G + g, d + 1);
     }
   }
 };
@@ -387,11 +426,11 @@ void launch_flow(const TvArgs &a, hipStream_t s) {
 template <int NOP, int NOC, int S>
 bool flow_dispatch(const TvArgs &a, hipStream_t s, bool run) {
   if (a.h <= 64) {
-    if (run) launch_flow<NOP, NOC, S, 1, 4>(a, s);
+    if (run) launch_flow<NOP, NOC, S, 1, 8>(a, s);
     return true;
   }
   if (a.h <= 128) {
-    if (run) launch_flow<NOP, NOC, S, 2, 3>(a, s);
+    if (run) launch_flow<NOP, NOC, S, 2, 4>(a, s);
     return true;
   }
   return false;
