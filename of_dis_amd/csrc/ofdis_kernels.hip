@@ -4027,7 +4027,7 @@ bool tv_smsys_ok(const TvArgs &a) {
 // Not where the 40 KB LDS cap of the DF form leaves fewer than 3 rows per block (levels of ~180-256 rows): a
 // block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
-  if (tv_flow_ok(a)) return false;  // the dataflow iteration reads all eight derivative planes
+  if (tv_flow_ok(a)) return a.noc == 1;  // the dataflow iteration filters the second derivatives itself (gray)
   if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024))
     return false;
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
