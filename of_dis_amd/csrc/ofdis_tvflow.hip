@@ -534,6 +534,7 @@ template <int NOP, int NOC, int S, int G, int P>
 void launch_flow(const TvArgs &a, hipStream_t s) {
   using F = Flow<NOP, NOC, S, G, P>;
   static_assert(F::LDS <= 160 * 1024, "LDS");
+  static_assert(F::NW <= 16, "one workgroup of at most 1024 threads");
   static_assert(2 * F::NDMA < 64, "loader batches in flight");
   k_tv_flow<NOP, NOC, S, G, P><<<a.n, 64 * F::NW, F::LDS, s>>>(a);
 }
@@ -546,7 +547,7 @@ bool flow_dispatch(const TvArgs &a, hipStream_t s, bool run) {
   }
   if constexpr (NOC == 1) {
     if (a.h <= 128) {
-      if (run) launch_flow<NOP, NOC, S, 2, 4>(a, s);
+      if (run) launch_flow<NOP, NOC, S, 2, 3>(a, s);
       return true;
     }
   }
