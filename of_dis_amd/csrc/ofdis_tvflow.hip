@@ -130,7 +130,9 @@ struct Flow {
   static constexpr size_t LDS = OFF_S + sizeof(float) * kFlowRS * NR;
   static constexpr int NDMA = kFlowLB * NPL;  // DMA instructions per loader batch
 
-  const TvArgs &a;
+  // a copy: the fields live in scalar registers (a reference would make every LDS-order compiler barrier -- the
+  // empty asm with a memory clobber -- force a kernel-argument reload, an SMEM round trip, in the loops)
+  const TvArgs a;
   int *cnt;
   float *row;
   float4 *coef;
