@@ -109,19 +109,20 @@ struct ProbeRec {
 #define FLOW_PROBE(x)
 #endif
 
-// NOP 2 (flow) / 1 (depth); NOC channels; S sweeps; G row groups of 64 rows; P system waves per group.
-// DF (intensity images): the row ring also carries Ix, Iy, Iz and the system filters the second derivatives itself
-// (k_tv_prepd then writes only Ix, Iy, Iz); RGB: the system reads the eight derivative planes from memory.
-template <int NOP, int NOC, int S, int G, int P>
+// NOP 2 (flow) / 1 (depth); NOC channels; S sweeps; NM smoothness waves; P system waves (levels of <= 64 rows:
+// lane = row y).  DF (intensity images): the row ring also carries Ix, Iy, Iz and the system filters the second
+// derivatives itself (k_tv_prepd then writes only Ix, Iy, Iz); RGB: the system reads the eight derivative planes
+// from memory.
+template <int NOP, int NOC, int S, int NM, int P>
 struct Flow {
   static constexpr bool DF = NOC == 1;
-  static constexpr int NR = 64 * G + 2;   // entries per slot of the s / coefficient / (u, v) rings
-  static constexpr int NRA = 64 * G + 8;  // entries per plane of the row ring (16-byte multiple)
+  static constexpr int NR = 66;   // entries per slot of the s / coefficient / (u, v) rings (row y at y + 1)
+  static constexpr int NRA = 72;  // entries per plane of the row ring (row y at y + 4; 16-byte multiple)
   static constexpr int CW = NOP == 2 ? 2 : 1;
   static constexpr int NPL = (NOP == 2 ? 4 : 2) + (DF ? 3 : 0);  // wx, du, (wy, dv), (Ix, Iy, Iz)
   static constexpr int PWX = 0, PDU = 1, PWY = 2, PDV = 3, PIX = NOP == 2 ? 4 : 2;
-  static constexpr int NW = S * G + 1 + G + P * G;
-  static constexpr int C_SOR = 0, C_L = S * G, C_S = S * G + 1, C_Y = S * G + 1 + G, C_ABORT = S * G + 1 + G + P * G;
+  static constexpr int NW = S + 1 + NM + P;
+  static constexpr int C_SOR = 0, C_L = S, C_M = S + 1, C_Y = S + 1 + NM, C_ABORT = S + 1 + NM + P;
   static constexpr int NCNT = (C_ABORT + 1 + 3) / 4 * 4;
   static constexpr size_t OFF_ROW = 16 * NCNT;                                       // [RR][NPL][NRA] float
   static constexpr size_t OFF_COEF = OFF_ROW + sizeof(float) * kFlowRR * NPL * NRA;  // [RC][CW][NR] float4
@@ -159,10 +160,8 @@ struct Flow {
     first = a.first_iter != 0;
   }
   __device__ __forceinline__ int prow(int d) const { return d >= lim ? d - lim : d; }  // 0 <= d < E
-  // row ring: plane p of diagonal q (any q >= -RR: slot q mod RR), row y (-1 .. 64 G)
-  __device__ __forceinline__ float rr(int q, int p, int y) const {
-    return row[((q & (kFlowRR - 1)) * NPL + p) * NRA + y + 4];
-  }
+  // row ring: the first entry of diagonal q's slot (any q >= -RR: slot q mod RR, a uniform offset)
+  __device__ __forceinline__ const float *slot(int q) const { return row + (q & (kFlowRR - 1)) * NPL * NRA + 4; }
 
   // Poll until ok(C) holds, C(i) = counter i: lane i < NCNT reads counter i (one LDS round trip), the checks take
   // them by v_readlane.  false: the launch aborts.
@@ -185,13 +184,6 @@ struct Flow {
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  template <class CF>
-  __device__ __forceinline__ static int cmin(CF &C, int base) {  // min over the row groups (sweep s: C_SOR + s G)
-    int m = C(base);
-#pragma unroll
-    for (int g = 1; g < G; ++g) m = min(m, C(base + g));
-    return m;
-  }
 
   // ------------------------------------------------------------------------------------------------ L
   // The plane rows of diagonal q (clamped to the last one) into its ring slot: lane i < ceil(h / 4) moves floats
@@ -200,7 +192,7 @@ struct Flow {
   __device__ __forceinline__ void dma_row(int q, int lane) const {
     const int qc = q < E ? q : E - 1;
     const unsigned o = f0 + (unsigned)(prow(qc) * h) + 4u * (unsigned)lane;
-    float *dst = row + (size_t)((q & (kFlowRR - 1)) * NPL) * NRA + 4;
+    const float *dst = slot(q);
     const float *src[NPL];
     src[PWX] = a.wxs;
     src[PDU] = a.du;
@@ -227,8 +219,8 @@ struct Flow {
       if (b < nb) {
         const int rlast = b * kFlowLB + kFlowLB - 1;
         // WAR: row r replaces row r - RR, read last by the system of diagonal r - RR + 2 (filter taps d -+ 2):
-        // every sweep-0 wave past it
-        if (!wait([&](auto &C) { return cmin(C, C_SOR) >= rlast - kFlowRR + 3; })) return;
+        // sweep 0 past it
+        if (!wait([&](auto &C) { return C(C_SOR) >= rlast - kFlowRR + 3; })) return;
 #pragma unroll
         for (int k = 0; k < kFlowLB; ++k) dma_row(b * kFlowLB + k, lane);
         if (b > 0) wait_vmcnt<NDMA>();  // batch b - 1 has landed
@@ -244,64 +236,60 @@ struct Flow {
   }
 
   // ------------------------------------------------------------------------------------------------ M
-  // s of diagonal e at row y from rows e - 1, e, e + 1 (compute_smoothness's replicate border: an absent neighbour
-  // is the centre); 0 outside the level
+  // s of diagonal e at row y (compute_smoothness on rows e - 1, e, e + 1; its replicate border takes the centre
+  // for an absent neighbour: selected here by address, so each value is one read); 0 outside the level
   __device__ __forceinline__ float smooth_at(int e, int y) const {
     const int x = e - y;
-    float sv = 0.0f;
-    // centre, left (x - 1, y), right (x + 1, y), up (x, y - 1), down (x, y + 1)
-    float wx5[5] = {rr(e, PWX, y), rr(e - 1, PWX, y), rr(e + 1, PWX, y), rr(e - 1, PWX, y - 1), rr(e + 1, PWX, y + 1)};
-    float du5[5] = {rr(e, PDU, y), rr(e - 1, PDU, y), rr(e + 1, PDU, y), rr(e - 1, PDU, y - 1), rr(e + 1, PDU, y + 1)};
-    float wy5[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, dv5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    if (NOP == 2) {
-      const float t0[5] = {rr(e, PWY, y), rr(e - 1, PWY, y), rr(e + 1, PWY, y), rr(e - 1, PWY, y - 1),
-                           rr(e + 1, PWY, y + 1)};
-      const float t1[5] = {rr(e, PDV, y), rr(e - 1, PDV, y), rr(e + 1, PDV, y), rr(e - 1, PDV, y - 1),
-                           rr(e + 1, PDV, y + 1)};
+    const float *c = slot(e) + y;
+    const float *l = x > 0 ? slot(e - 1) + y : c;       // (x - 1, y)
+    const float *r = x < w - 1 ? slot(e + 1) + y : c;   // (x + 1, y)
+    const float *u = y > 0 ? slot(e - 1) + y - 1 : c;   // (x, y - 1)
+    const float *dn = y < h - 1 ? slot(e + 1) + y + 1 : c;  // (x, y + 1)
+    const float *q5[5] = {c, l, r, u, dn};
+    float wx5[5], du5[5], wy5[5], dv5[5];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        wy5[k] = t0[k];
-        dv5[k] = t1[k];
-      }
+    for (int k = 0; k < 5; ++k) {
+      wx5[k] = q5[k][PWX * NRA];
+      du5[k] = q5[k][PDU * NRA];
+      wy5[k] = NOP == 2 ? q5[k][PWY * NRA] : 0.0f;
+      dv5[k] = NOP == 2 ? q5[k][PDV * NRA] : 0.0f;
     }
-    if ((unsigned)x < (unsigned)w && y < h) {
-      const bool has[5] = {true, x > 0, x < w - 1, y > 0, y < h - 1};
-#pragma unroll
-      for (int k = 1; k < 5; ++k) {
-        wx5[k] = has[k] ? wx5[k] : wx5[0];
-        du5[k] = has[k] ? du5[k] : du5[0];
-        wy5[k] = has[k] ? wy5[k] : wy5[0];
-        dv5[k] = has[k] ? dv5[k] : dv5[0];
-      }
-      sv = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
-    }
-    return sv;
+    const float sv = smooth_compute<NOP>(a, first, wx5, du5, wy5, dv5);
+    return (unsigned)x < (unsigned)w && y < h ? sv : 0.0f;
   }
-  __device__ void run_m(int g, int lane) {
+  __device__ void run_m(int m, int y) {
     __builtin_amdgcn_s_setprio(2);
-    const int y = 64 * g + lane;
-    for (int e = 0; e < E; e += 2) {
+    for (int e = m; e < E; e += NM) {
       FLOW_PROBE(pr.start());
-      // rows <= e + 2 in the ring; WAR: s(e + 1) replaces s(e + 1 - RS), read last by the system of diagonal
-      // e + 2 - RS
-      const int need = e + 3 < E ? e + 3 : E;
-      if (!wait([&](auto &C) { return C(C_L) >= need && cmin(C, C_SOR) >= e + 3 - kFlowRS; })) return;
-      const float s0 = smooth_at(e, y);
-      const float s1 = e + 1 < E ? smooth_at(e + 1, y) : 0.0f;
-      sr[(e % kFlowRS) * NR + y + 1] = s0;
-      sr[((e + 1) % kFlowRS) * NR + y + 1] = s1;
-      cnt_publish(cnt + C_S + g, e + 2 < E ? e + 2 : E);  // s of diagonals 0 .. e + 1
-      FLOW_PROBE(pr.done(e / 2));
+      // rows <= e + 1 in the ring; WAR: s(e) replaces s(e - RS), read last by the system of diagonal e - RS + 1
+      const int need = e + 2 < E ? e + 2 : E;
+      if (!wait([&](auto &C) { return C(C_L) >= need && C(C_SOR) >= e - kFlowRS + 2; })) return;
+      sr[(e % kFlowRS) * NR + y + 1] = smooth_at(e, y);
+      cnt_publish(cnt + C_M + m, e + 1);  // s of this wave's diagonals <= e
+      FLOW_PROBE(pr.done((e - m) / NM));
     }
   }
 
   // ------------------------------------------------------------------------------------------------ Y
-  __device__ __forceinline__ bool y_step(int d, int g, int j, int y) {
+  // get_derivatives' 5-tap filter (k_tv_deriv2 / k_tv_smsys<.., DF>'s expression) from the taps at offsets -2 .. 2
+  // along one axis, replicate border: a tap past the border takes the border pixel's value, which is one of the
+  // taps read (pos = the pixel's coordinate along the axis, n = the level's extent)
+  __device__ __forceinline__ static float conv5_clamped(const float (&t)[5], int pos, int n) {
+    const float m1 = pos >= 1 ? t[1] : t[2];
+    const float m2 = pos >= 2 ? t[0] : m1;
+    const float p1 = pos <= n - 2 ? t[3] : t[2];
+    const float p2 = pos <= n - 3 ? t[4] : p1;
+    return kK5[0] * m2 + ((kK5[1] * m1 + kK5[2] * t[2]) + (kK5[3] * p1 + kK5[4] * p2));
+  }
+  __device__ __forceinline__ bool y_step(int d, int j, int y) {
     FLOW_PROBE(pr.start());
-    const int sneed = d + 2 < E ? d + 2 : E;  // s of diagonals <= d + 1 (and so rows <= d + 2)
-    if (!wait([&](auto &C) {
-          bool ok = C(C_S + g) >= sneed && cmin(C, C_SOR + (S - 1) * G) >= d - kFlowRC + 2;
-          if (G > 1) ok = ok && (g == 0 || C(C_S + g - 1) >= sneed) && (g == G - 1 || C(C_S + g + 1) >= sneed);
+    if (!wait([&](auto &C) {  // s(d - 1 .. d + 1); WAR: the coefficient slot's diagonal d - RC, read last at d - RC + 1
+          bool ok = C(C_SOR + S - 1) >= d - kFlowRC + 2;
+#pragma unroll
+          for (int k = -1; k <= 1; ++k) {
+            const int e = d + k;
+            if (e >= 0 && e < E) ok = ok && C(C_M + e % NM) >= e + 1;
+          }
           return ok;
         }))
       return false;
@@ -309,45 +297,38 @@ struct Flow {
     const int sm = ((d + kFlowRS - 1) % kFlowRS) * NR, s0 = (d % kFlowRS) * NR, sp1 = ((d + 1) % kFlowRS) * NR;
     // centre, left (x - 1, y), right (x + 1, y), up (x, y - 1), down (x, y + 1)
     const float S5[5] = {sr[s0 + y + 1], sr[sm + y + 1], sr[sp1 + y + 1], sr[sm + y], sr[sp1 + y + 2]};
-    const float X5[5] = {rr(d, PWX, y), rr(d - 1, PWX, y), rr(d + 1, PWX, y), rr(d - 1, PWX, y - 1),
-                         rr(d + 1, PWX, y + 1)};
+    const float *c = slot(d) + y, *pm = slot(d - 1) + y, *pp = slot(d + 1) + y;
+    const float X5[5] = {c[PWX * NRA], pm[PWX * NRA], pp[PWX * NRA], pm[PWX * NRA - 1], pp[PWX * NRA + 1]};
     float Y5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     if (NOP == 2) {
-      const float t[5] = {rr(d, PWY, y), rr(d - 1, PWY, y), rr(d + 1, PWY, y), rr(d - 1, PWY, y - 1),
-                          rr(d + 1, PWY, y + 1)};
+      const float t[5] = {c[PWY * NRA], pm[PWY * NRA], pp[PWY * NRA], pm[PWY * NRA - 1], pp[PWY * NRA + 1]};
 #pragma unroll
       for (int k = 0; k < 5; ++k) Y5[k] = t[k];
     }
-    const float u = rr(d, PDU, y), v = NOP == 2 ? rr(d, PDV, y) : 0.0f;
+    const float u = c[PDU * NRA], v = NOP == 2 ? c[PDV * NRA] : 0.0f;
     const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
     float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
     if constexpr (DF) {
-      // get_derivatives' 5-tap filters with replicate border (k_tv_smsys<.., DF>'s expressions): a tap at x + k is
-      // diagonal d + k' (k' the clamped offset), same row; a tap at y + k is diagonal d + k', row y + k'
-      const int xc = (unsigned)x < (unsigned)w ? x : 0, yc = y < h ? y : 0;  // (lanes outside: any valid taps)
-      int hx[5], vy[5];
+      // taps (x + k, y): diagonal d + k, row y; (x, y + k): diagonal d + k, row y + k
+      const float *q[5] = {slot(d - 2) + y, pm, c, pp, slot(d + 2) + y};
+      float hX[5], vX[5], vY[5], hZ[5], vZ[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
-        hx[k] = clampi(xc + k - 2, 0, w - 1) - xc;
-        vy[k] = clampi(yc + k - 2, 0, h - 1) - yc;
+        hX[k] = q[k][PIX * NRA];
+        vX[k] = q[k][PIX * NRA + k - 2];
+        vY[k] = q[k][(PIX + 1) * NRA + k - 2];
+        hZ[k] = q[k][(PIX + 2) * NRA];
+        vZ[k] = q[k][(PIX + 2) * NRA + k - 2];
       }
-      auto c5h = [&](int p) {
-        return kK5[0] * rr(d + hx[0], p, y) + ((kK5[1] * rr(d + hx[1], p, y) + kK5[2] * rr(d, p, y)) +
-                                               (kK5[3] * rr(d + hx[3], p, y) + kK5[4] * rr(d + hx[4], p, y)));
-      };
-      auto c5v = [&](int p) {
-        return kK5[0] * rr(d + vy[0], p, y + vy[0]) +
-               ((kK5[1] * rr(d + vy[1], p, y + vy[1]) + kK5[2] * rr(d, p, y)) +
-                (kK5[3] * rr(d + vy[3], p, y + vy[3]) + kK5[4] * rr(d + vy[4], p, y + vy[4])));
-      };
-      lIx[0] = rr(d, PIX, y);
-      lIy[0] = rr(d, PIX + 1, y);
-      lIz[0] = rr(d, PIX + 2, y);
-      lIxx[0] = c5h(PIX);
-      lIxy[0] = c5v(PIX);
-      lIyy[0] = c5v(PIX + 1);
-      lIxz[0] = c5h(PIX + 2);
-      lIyz[0] = c5v(PIX + 2);
+      const int xc = (unsigned)x < (unsigned)w ? x : 0, yc = y < h ? y : 0;  // (lanes outside: any valid taps)
+      lIx[0] = hX[2];
+      lIy[0] = vY[2];
+      lIz[0] = hZ[2];
+      lIxx[0] = conv5_clamped(hX, xc, w);
+      lIxy[0] = conv5_clamped(vX, yc, h);
+      lIyy[0] = conv5_clamped(vY, yc, h);
+      lIxz[0] = conv5_clamped(hZ, xc, w);
+      lIyz[0] = conv5_clamped(vZ, yc, h);
     } else {
       const bool in = (unsigned)x < (unsigned)w && y < h;
       const unsigned o0 = f0 * (unsigned)NOC + (unsigned)(prow(d) * h) + (in ? (unsigned)y : 0u);
@@ -363,26 +344,23 @@ struct Flow {
     float4 *C = coef + (d % kFlowRC) * CW * NR + y + 1;
     C[0] = c0;
     if (NOP == 2) C[NR] = c1;
-    cnt_publish(cnt + C_Y + j * G + g, d + 1);
+    cnt_publish(cnt + C_Y + j, d + 1);
     FLOW_PROBE(pr.done(d / P));
     return true;
   }
-  __device__ void run_y(int g, int j, int lane) {
+  __device__ void run_y(int j, int y) {
     __builtin_amdgcn_s_setprio(0);
-    const int y = 64 * g + lane;
     for (int d = j; d < E; d += P)
-      if (!y_step(d, g, j, y)) return;
+      if (!y_step(d, j, y)) return;
   }
 
   // ------------------------------------------------------------------------------------------------ SOR
   template <int SI>
-  __device__ void run_sor(int g, int lane) {
+  __device__ void run_sor(int y) {
     constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
     constexpr int MODE = NOP == 2 ? 0 : 2;
     __builtin_amdgcn_s_setprio(3);
-    const int y = 64 * g + lane;
     const bool border = y == 0 || y >= h - 1, notop = y == 0;
-    const bool top_lds = lane == 0 && g > 0;
     const float omega = a.omega;
     f2v pp = f2v{0.0f, 0.0f};  // own (u, v) of the previous diagonal (left neighbour; lane y + 1's top)
     float phr = 0.0f, pvv = 0.0f;
@@ -393,18 +371,17 @@ struct Flow {
       const int dn = d + 2 < E ? d + 2 : E;
       const int x = d - y;
       const bool hasl = x > 0, hasr = x < w - 1;
-      const int dm = (d + kFlowD - 1) % kFlowD, cm = (d + kFlowRC - 1) % kFlowRC;
-      f2v o, rgt, bt, tpl = f2v{0.f, 0.f};
+      f2v o, rgt, bt;
       float4 c0, c1;
-      float tsvl = 0.f;
       // one LDS round trip per poll: the counters, then (in issue order) the operands -- valid once they hold
       for (int spin = 0;; ++spin) {
-        const int v = cnt_load(cnt + (lane < NCNT ? lane : 0));
+        const int v = cnt_load(cnt + (y < NCNT ? y : 0));
         lds_order();
         if (FIRST) {
-          o = f2v{rr(d, PDU, y), NOP == 2 ? rr(d, PDV, y) : 0.0f};
-          rgt = f2v{rr(d + 1, PDU, y), NOP == 2 ? rr(d + 1, PDV, y) : 0.0f};
-          bt = f2v{rr(d + 1, PDU, y + 1), NOP == 2 ? rr(d + 1, PDV, y + 1) : 0.0f};
+          const float *r0 = slot(d) + y, *r1 = slot(d + 1) + y;
+          o = f2v{r0[PDU * NRA], NOP == 2 ? r0[PDV * NRA] : 0.0f};
+          rgt = f2v{r1[PDU * NRA], NOP == 2 ? r1[PDV * NRA] : 0.0f};
+          bt = f2v{r1[PDU * NRA + 1], NOP == 2 ? r1[PDV * NRA + 1] : 0.0f};
         } else {
           o = ring_p[(d % kFlowD) * NR + y + 1];
           rgt = ring_p[((d + 1) % kFlowD) * NR + y + 1];
@@ -413,28 +390,13 @@ struct Flow {
         const float4 *Cp = coef + (d % kFlowRC) * CW * NR + y + 1;
         c0 = Cp[0];
         c1 = MODE == 0 ? Cp[NR] : c0;
-        if (G > 1) {  // lane 0 of a lower row group: the row above is the group above's
-          tpl = ring_s[dm * NR + y];
-          tsvl = coef[(cm * CW + CW - 1) * NR + y].w;
-        }
         lds_order();
         auto C = [&](int i) { return __builtin_amdgcn_readlane(v, i); };
-        bool ok;
-        if (FIRST) {
-          ok = C(C_Y + (d % P) * G + g) >= d + 1;
-        } else {
-          ok = C(C_SOR + (SI - 1) * G + g) >= dn;
-          if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + (SI - 1) * G + g + 1) >= dn;
-        }
-        if (G > 1 && g > 0) ok = ok && C(C_SOR + SI * G + g - 1) >= d;  // top of lane 0: diagonal d - 1
-        if (!LAST) {
-          // WAR: this ring slot's diagonal d - D is read by sweep SI + 1 of this group as its own (at d - D) and
-          // right / bottom values (at d - D - 1), by sweep SI + 1 of the group above as lane 63's bottom
-          ok = ok && C(C_SOR + (SI + 1) * G + g) >= d - kFlowD + 1;
-          if (G > 1 && g > 0) ok = ok && C(C_SOR + (SI + 1) * G + g - 1) >= d - kFlowD;
-        }
-        // ... and by this sweep's group below as lane 0's top (at d - D + 1)
-        if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + SI * G + g + 1) >= d - kFlowD + 2;
+        // FIRST: the coefficients of d; later sweeps: the previous sweep's d + 1.  WAR (not the last sweep): this
+        // ring slot's diagonal d - D is read by the next sweep as its own (at d - D) and right / bottom values
+        // (at d - D - 1)
+        bool ok = FIRST ? C(C_Y + d % P) >= d + 1 : C(C_SOR + SI - 1) >= dn;
+        if (!LAST) ok = ok && C(C_SOR + SI + 1) >= d - kFlowD + 1;
         if (ok) {
           FLOW_PROBE(pr.ready(spin));
           break;
@@ -446,12 +408,9 @@ struct Flow {
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      f2v tp = f2v{dpp_from_prev_lane(pp.x), MODE == 0 ? dpp_from_prev_lane(pp.y) : 0.0f};
-      float tsv = dpp_from_prev_lane(pvv);
-      if (G > 1 && top_lds) {
-        tp = tpl;
-        tsv = tsvl;
-      }
+      // the upper neighbour (x, y - 1) of this sweep: lane y - 1's result of the previous diagonal
+      const f2v tp = f2v{dpp_from_prev_lane(pp.x), MODE == 0 ? dpp_from_prev_lane(pp.y) : 0.0f};
+      const float tsv = dpp_from_prev_lane(pvv);
       f2v nw;
       float vv;
       if (MODE == 0) {
@@ -490,15 +449,15 @@ struct Flow {
       }
       pp = nw;
       pvv = vv;
-      cnt_publish(cnt + C_SOR + SI * G + g, d + 1);
+      cnt_publish(cnt + C_SOR + SI, d + 1);
       FLOW_PROBE(pr.done(d));
     }
   }
 };
 
-template <int NOP, int NOC, int S, int G, int P>
-__global__ __launch_bounds__((64 * Flow<NOP, NOC, S, G, P>::NW)) void k_tv_flow(TvArgs a) {
-  using F = Flow<NOP, NOC, S, G, P>;
+template <int NOP, int NOC, int S, int NM, int P>
+__global__ __launch_bounds__((64 * Flow<NOP, NOC, S, NM, P>::NW)) void k_tv_flow(TvArgs a) {
+  using F = Flow<NOP, NOC, S, NM, P>;
   extern __shared__ __attribute__((aligned(16))) char flow_lds[];
   // zero everything (counters, ring halos: the slots of rows -1 / h stay finite)
   for (int i = threadIdx.x; i < (int)(F::LDS / 16); i += blockDim.x)
@@ -514,53 +473,42 @@ __global__ __launch_bounds__((64 * Flow<NOP, NOC, S, G, P>::NW)) void k_tv_flow(
     if (slot < 64u && wid < 16) fl.pr.p = g_flow_probe + 4 + ((size_t)slot * 16 + wid) * 256 * 4;
   }
 #endif
-  if (wid < S * G) {  // sweep wid / G of row group wid % G
-    const int s = wid / G, g = wid - s * G;
-    if (s == 0) fl.template run_sor<0>(g, lane);
-    else if (s == 1) fl.template run_sor<(S > 1 ? 1 : 0)>(g, lane);
-    else if (s == 2) fl.template run_sor<(S > 2 ? 2 : 0)>(g, lane);
-    else fl.template run_sor<(S > 3 ? 3 : 0)>(g, lane);
-  } else if (wid == S * G) {
+  if (wid < S) {  // sweep wid
+    if (wid == 0) fl.template run_sor<0>(lane);
+    else if (wid == 1) fl.template run_sor<(S > 1 ? 1 : 0)>(lane);
+    else if (wid == 2) fl.template run_sor<(S > 2 ? 2 : 0)>(lane);
+    else fl.template run_sor<(S > 3 ? 3 : 0)>(lane);
+  } else if (wid == S) {
     fl.run_l(lane);
-  } else if (wid < S * G + 1 + G) {
-    fl.run_m(wid - S * G - 1, lane);
+  } else if (wid < S + 1 + NM) {
+    fl.run_m(wid - S - 1, lane);
   } else {
-    const int k = wid - S * G - 1 - G, j = k / G, g = k - j * G;
-    fl.run_y(g, j, lane);
+    fl.run_y(wid - S - 1 - NM, lane);
   }
   __syncthreads();  // every role has left its loop (each wait is bounded)
   if (threadIdx.x == 0 && cnt_load(fl.cnt + F::C_ABORT) && a.flow_err) atomicAdd(a.flow_err, 1);
 }
 
-template <int NOP, int NOC, int S, int G, int P>
+template <int NOP, int NOC, int S>
 void launch_flow(const TvArgs &a, hipStream_t s) {
-  using F = Flow<NOP, NOC, S, G, P>;
+  constexpr int NM = 3, P = 12 - S;  // 16 waves
+  using F = Flow<NOP, NOC, S, NM, P>;
   static_assert(F::LDS <= 160 * 1024, "LDS");
   static_assert(F::NW <= 16, "one workgroup of at most 1024 threads");
   static_assert(2 * F::NDMA < 64, "loader batches in flight");
-  k_tv_flow<NOP, NOC, S, G, P><<<a.n, 64 * F::NW, F::LDS, s>>>(a);
-}
-
-template <int NOP, int NOC, int S>
-bool flow_dispatch(const TvArgs &a, hipStream_t s, bool run) {
-  if (a.h <= 64) {
-    if (run) launch_flow<NOP, NOC, S, 1, 8>(a, s);
-    return true;
-  }
-  if constexpr (NOC == 1) {
-    if (a.h <= 128) {
-      if (run) launch_flow<NOP, NOC, S, 2, 3>(a, s);
-      return true;
-    }
-  }
-  return false;
+  k_tv_flow<NOP, NOC, S, NM, P><<<a.n, 64 * F::NW, F::LDS, s>>>(a);
 }
 
 template <int NOP, int NOC>
 bool flow_dispatch_s(const TvArgs &a, hipStream_t s, bool run) {
+  if (a.h > 64) return false;
   switch (a.solverit) {
-    case 2: return flow_dispatch<NOP, NOC, 2>(a, s, run);
-    case 3: return flow_dispatch<NOP, NOC, 3>(a, s, run);
+    case 2:
+      if (run) launch_flow<NOP, NOC, 2>(a, s);
+      return true;
+    case 3:
+      if (run) launch_flow<NOP, NOC, 3>(a, s);
+      return true;
     default: return false;
   }
 }
@@ -572,7 +520,7 @@ bool flow_go(const TvArgs &a, hipStream_t s, bool run) {
 
 }  // namespace
 
-// The dataflow iteration runs where its rings fit: up to 64 rows (128 for intensity images), 2 or 3 sweeps, the
+// The dataflow iteration runs where its rings fit: up to 64 rows (lane = row), 2 or 3 sweeps, the
 // exact order (not the red-black mode, not the OpenMP build's point SOR), levels of at least 2 x 2 (solver.c's
 // border forms); intensity images also need k_tv_prepd (it writes the Ix, Iy, Iz the loader streams).
 bool tv_flow_ok(const TvArgs &a) {

@@ -25,17 +25,16 @@ SLOTS, WAVES, ITERS = 64, 16, 256
 
 
 def roles(h, S=3):
-    G, P = (1, 8) if h <= 64 else (2, 3)
+    G, NM, P = 1, 3, 12 - S
     r = {}
     for s in range(S):
         for g in range(G):
             r[s * G + g] = f"sor{s}_g{g}"
     r[S * G] = "L"
-    for g in range(G):
-        r[S * G + 1 + g] = f"M_g{g}"
+    for m in range(NM):
+        r[S + 1 + m] = f"M{m}"
     for j in range(P):
-        for g in range(G):
-            r[S * G + 1 + G + j * G + g] = f"Y{j}_g{g}"
+        r[S + 1 + NM + j] = f"Y{j}"
     return r
 
 
