@@ -201,9 +201,10 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
  *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
- *   "tv_flow" (0/1, default 1): levels of up to 128 rows run each TV inner iteration (smoothness, system and
+ *   "tv_flow" (0/1, default 0): levels of up to 64 rows run each TV inner iteration (smoothness, system and
  *                        the exact-order SOR) as one launch whose waves hand the diagonals to each other through
- *                        LDS (no coefficient round trip through HBM; 0: the system and SOR launches);
+ *                        LDS (no coefficient round trip through HBM; measured slower than the system and SOR
+ *                        launches: one CU issues the whole system);
  *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
