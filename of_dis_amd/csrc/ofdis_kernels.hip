@@ -4149,6 +4149,10 @@ static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
 // global-memory wavefront for the point SOR of the OpenMP build and degenerate sizes.
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
+  if (tv_sorflow_ok(a)) {  // barrier-free sweep waves fed by an LDS-DMA loader (ofdis_tvflow.hip)
+    launch_tv_sorflow(a, s);
+    return;
+  }
   const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);  // point SOR (solver.c:34-78)
   if (a.sor_redblack && !tiny) {  // opt-in red-black order (not the reference's bits)
     const int n = a.w * a.h;

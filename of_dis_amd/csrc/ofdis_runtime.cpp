@@ -96,6 +96,7 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
+  int opt_sor_flow = 1;        // exact-order SOR of levels <= 128 rows as the barrier-free k_tv_sorflow
   int opt_tv_flow = 0;         // one dataflow launch per TV inner iteration (k_tv_flow) where it fits (opt-in:
                                // measured slower than the two launches)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
@@ -515,6 +516,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
       tv.tv_flow = c->opt_tv_flow;
+      tv.sor_flow = c->opt_sor_flow;
       tv.flow_err = tv_flow_err_counter();
       tv.smsys_deriv = tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
@@ -1240,7 +1242,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
-      {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},
+      {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},      {"sor_flow", &ofdis_context::opt_sor_flow, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {

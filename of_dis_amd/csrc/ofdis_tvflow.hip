@@ -518,6 +518,287 @@ bool flow_go(const TvArgs &a, hipStream_t s, bool run) {
   return a.noc == 1 ? flow_dispatch_s<1, 1>(a, s, run) : flow_dispatch_s<1, 3>(a, s, run);
 }
 
+// ==================================================================================================== SOR only
+// k_tv_sorflow: the exact-order SOR call (solver.c:83-433 / :439-471) of one frame's level, the system computed
+// by the system launch as before, with the sweep-per-wave schedule of k_tv_sor_lanes run barrier-free: the sweep
+// waves (S per 64-row group, G <= 2 groups) and one loader wave hand diagonals to each other through LDS rings and
+// progress counters, as in k_tv_flow.  The loader streams each diagonal's coefficients (the system launch's
+// array-of-structs row) and the old (du, dv) rows into the rings by LDS-DMA, several rows ahead.  A sweep wave
+// thus waits only for the two waves it depends on (the previous sweep, the group above) -- not for every wave of
+// the workgroup at a barrier -- and never for a global load.  Same update expressions as k_tv_sor_lanes.
+constexpr int kSfRC = 8;   // coefficient ring slots
+constexpr int kSfRR = 8;   // (du, dv) row ring slots (power of 2)
+constexpr int kSfD = 4;    // (u, v) ring slots per sweep
+constexpr int kSfLB = 2;   // rows per loader batch (two batches in flight)
+
+template <int S, int MODE, int G>
+struct SorFlow {
+  static constexpr int CW = MODE == 0 ? 2 : 1;
+  static constexpr int NR = 64 * G + 2;   // (u, v) ring entries per slot (row y at y + 1)
+  static constexpr int NRA = 64 * G + 8;  // (du, dv) ring entries per plane (row y at y + 4)
+  static constexpr int NCR = 64 * G * CW; // coefficient ring float4 per slot (row y at y CW)
+  static constexpr int NPL = MODE == 0 ? 2 : 1;
+  static constexpr int NW = S * G + 1;
+  static constexpr int C_SOR = 0, C_L = S * G, C_ABORT = S * G + 1;
+  static constexpr int NCNT = (C_ABORT + 1 + 3) / 4 * 4;
+  static constexpr size_t OFF_COEF = 16 * NCNT;                                    // [RC][NCR] float4
+  static constexpr size_t OFF_DU = OFF_COEF + sizeof(float4) * kSfRC * NCR;          // [RR][NPL][NRA] float
+  static constexpr size_t OFF_UV = OFF_DU + sizeof(float) * kSfRR * NPL * NRA;       // [S][D][NR] f2v
+  static constexpr size_t LDS = OFF_UV + sizeof(f2v) * S * kSfD * NR;
+  // DMA instructions per row: coefficients 16 h CW bytes (1 KiB each), du / dv h floats each
+  static constexpr int NDMA_ROW = (NCR * 16 + 1023) / 1024 + NPL;
+
+  const TvArgs a;
+  int *cnt;
+  float4 *coef;
+  float *dur;
+  f2v *uv;
+  int w, h, E, lim;
+  unsigned f0;
+
+  __device__ SorFlow(const TvArgs &a_, char *lds, int frame) : a(a_) {
+    cnt = reinterpret_cast<int *>(lds);
+    coef = reinterpret_cast<float4 *>(lds + OFF_COEF);
+    dur = reinterpret_cast<float *>(lds + OFF_DU);
+    uv = reinterpret_cast<f2v *>(lds + OFF_UV);
+    w = a.w;
+    h = a.h;
+    E = a.w + a.h - 1;
+    lim = a.wrap ? a.w : 1 << 30;
+    f0 = (unsigned)((long)frame * a.sp);
+  }
+  __device__ __forceinline__ int prow(int d) const { return d >= lim ? d - lim : d; }
+  __device__ __forceinline__ const float *du_slot(int q) const { return dur + (q & (kSfRR - 1)) * NPL * NRA + 4; }
+
+  // loader: diagonal q's coefficient row (16 h CW contiguous bytes) and old du (dv) rows into the ring slots
+  __device__ __forceinline__ void dma_row(int q, int lane) const {
+    const int qc = q < E ? q : E - 1;
+    const unsigned pr = (unsigned)(prow(qc) * h);
+    const char *csrc = reinterpret_cast<const char *>(a.coef) + (size_t)(f0 + pr) * CW * 16;
+    const unsigned cdst = lds_addr(coef + (q % kSfRC) * NCR);
+    // every DMA instruction is issued by every batch (the loader's vmcnt waits count them): all lanes move 16
+    // bytes, those past the row re-read its start into slot entries of rows >= h (never read)
+    const int cbytes = h * CW * 16;
+#pragma unroll
+    for (int k = 0; k < (NCR * 16 + 1023) / 1024; ++k) {
+      const int off = 1024 * k + 16 * lane;
+      dma16(reinterpret_cast<const float *>(csrc + (off < cbytes ? off : 0)), __builtin_amdgcn_readfirstlane(cdst + 1024 * k));
+    }
+    if (lane < 16 * G) {  // (du, dv): 4 floats per lane, rows 0 .. 64 G - 1 of the slot (lane 0 always issues)
+      const float *d = du_slot(q);
+      const unsigned lo = 4 * lane < h ? 4u * (unsigned)lane : 0u;
+      dma16(a.du + f0 + pr + lo, __builtin_amdgcn_readfirstlane(lds_addr(d)));
+      if (MODE == 0) dma16(a.dv + f0 + pr + lo, __builtin_amdgcn_readfirstlane(lds_addr(d + NRA)));
+    }
+  }
+  template <class F>
+  __device__ __forceinline__ bool wait(F &&ok) {
+    const int lane = threadIdx.x & 63;
+    for (int spin = 0;; ++spin) {
+      const int v = cnt_load(cnt + (lane < NCNT ? lane : 0));
+      auto C = [&](int i) { return __builtin_amdgcn_readlane(v, i); };
+      if (ok(C)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        return true;
+      }
+      if (C(C_ABORT)) return false;
+      if (spin > kFlowSpinLimit) {
+        cnt_publish(cnt + C_ABORT, 1);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  template <class CF>
+  __device__ __forceinline__ static int cmin(CF &C, int base) {
+    int m = C(base);
+#pragma unroll
+    for (int g = 1; g < G; ++g) m = min(m, C(base + g));
+    return m;
+  }
+  __device__ void run_l(int lane) {
+    __builtin_amdgcn_s_setprio(2);
+    const int nb = (E + kSfLB - 1) / kSfLB;
+    for (int b = 0; b <= nb; ++b) {
+      if (b < nb) {
+        const int rlast = b * kSfLB + kSfLB - 1;
+        // WAR: coefficient slot of diagonal r - RC, read last by the last sweep (and lane 0's upper sv at
+        // r - RC + 1); (du, dv) row r - RR, read last by sweep 0 at diagonal r - RR
+        if (!wait([&](auto &C) {
+              return cmin(C, C_SOR + (S - 1) * G) >= rlast - kSfRC + 2 && cmin(C, C_SOR) >= rlast - kSfRR + 1;
+            }))
+          return;
+#pragma unroll
+        for (int k = 0; k < kSfLB; ++k) dma_row(b * kSfLB + k, lane);
+        if (b > 0) wait_vmcnt<kSfLB * NDMA_ROW>();  // batch b - 1 has landed (lanes without a row issue fewer)
+      } else {
+        wait_vmcnt<0>();
+      }
+      if (b > 0) cnt_publish(cnt + C_L, b * kSfLB < E ? b * kSfLB : E);  // rows 0 .. b LB - 1 in the rings
+    }
+  }
+
+  template <int SI>
+  __device__ void run_sor(int g, int lane) {
+    constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
+    __builtin_amdgcn_s_setprio(3);
+    const int y = 64 * g + lane;
+    const bool border = y == 0 || y >= h - 1, notop = y == 0;
+    const bool top_lds = lane == 0 && g > 0;
+    const float omega = a.omega;
+    f2v pp = f2v{0.0f, 0.0f};
+    float phr = 0.0f, pvv = 0.0f;
+    f2v *ring_s = uv + SI * kSfD * NR;
+    const f2v *ring_p = uv + (SI > 0 ? SI - 1 : 0) * kSfD * NR;
+    for (int d = 0; d < E; ++d) {
+      const int dn = d + 2 < E ? d + 2 : E;
+      const int x = d - y;
+      const bool hasl = x > 0, hasr = x < w - 1;
+      const int dm = (d + kSfD - 1) % kSfD, cm = (d + kSfRC - 1) % kSfRC;
+      f2v o, rgt, bt, tpl = f2v{0.f, 0.f};
+      float4 c0, c1;
+      float tsvl = 0.f;
+      for (int spin = 0;; ++spin) {
+        const int v = cnt_load(cnt + (lane < NCNT ? lane : 0));
+        lds_order();
+        if (FIRST) {
+          const float *r0 = du_slot(d) + y, *r1 = du_slot(d + 1) + y;
+          o = f2v{r0[0], MODE == 0 ? r0[NRA] : 0.0f};
+          rgt = f2v{r1[0], MODE == 0 ? r1[NRA] : 0.0f};
+          bt = f2v{r1[1], MODE == 0 ? r1[NRA + 1] : 0.0f};
+        } else {
+          o = ring_p[(d % kSfD) * NR + y + 1];
+          rgt = ring_p[((d + 1) % kSfD) * NR + y + 1];
+          bt = ring_p[((d + 1) % kSfD) * NR + y + 2];
+        }
+        const float4 *Cp = coef + (d % kSfRC) * NCR + y * CW;
+        c0 = Cp[0];
+        c1 = MODE == 0 ? Cp[1] : c0;
+        if (G > 1) {  // lane 0 of a lower row group: the row above is the group above's
+          tpl = ring_s[dm * NR + y];
+          tsvl = coef[cm * NCR + (y - 1) * CW + CW - 1].w;
+        }
+        lds_order();
+        auto C = [&](int i) { return __builtin_amdgcn_readlane(v, i); };
+        bool ok;
+        if (FIRST) {
+          ok = C(C_L) >= dn;  // the coefficients of d, the old rows d and d + 1
+        } else {
+          ok = C(C_SOR + (SI - 1) * G + g) >= dn;
+          if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + (SI - 1) * G + g + 1) >= dn;
+        }
+        if (G > 1 && g > 0) ok = ok && C(C_SOR + SI * G + g - 1) >= d;  // top of lane 0: diagonal d - 1
+        if (!LAST) {
+          ok = ok && C(C_SOR + (SI + 1) * G + g) >= d - kSfD + 1;
+          if (G > 1 && g > 0) ok = ok && C(C_SOR + (SI + 1) * G + g - 1) >= d - kSfD;
+        }
+        if (G > 1 && g + 1 < G) ok = ok && C(C_SOR + SI * G + g + 1) >= d - kSfD + 2;
+        if (ok) break;
+        if (C(C_ABORT)) return;
+        if (spin > kFlowSpinLimit) {
+          cnt_publish(cnt + C_ABORT, 1);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      f2v tp = f2v{dpp_from_prev_lane(pp.x), MODE == 0 ? dpp_from_prev_lane(pp.y) : 0.0f};
+      float tsv = dpp_from_prev_lane(pvv);
+      if (G > 1 && top_lds) {
+        tp = tpl;
+        tsv = tsvl;
+      }
+      f2v nw;
+      float vv;
+      if (MODE == 0) {
+        const float hr = c1.z;
+        vv = c1.w;
+        const f2v bb = f2v{c1.x, c1.y};
+        const f2v rrv = hasr ? rgt : f2v{0.0f, 0.0f};
+        const f2v X = hr * rrv, Yv = tsv * tp, Z = vv * bt;
+        const f2v l = X + (border ? bb : Yv);
+        const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Yv) : Z);
+        const f2v srr = l + rg;
+        const f2v Bv = hasl ? phr * pp + srr : srr;
+        const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;
+        nw = o + omega * ((m_1 + m_2) - o);
+        phr = hr;
+      } else {
+        const float a11 = c0.x, b1 = c0.y, hr = c0.z;
+        vv = c0.w;
+        const bool has_top = !notop, has_bot = !(border && has_top);
+        const float tu = tp.x, ur = hasr ? rgt.x : 0.0f, hl = phr;
+        float su = 0.0f;
+        su = has_top ? su - tsv * tu : su;
+        su = hasl ? su - hl * pp.x : su;
+        su = has_bot ? su - vv * bt.x : su;
+        su = hasr ? su - hr * ur : su;
+        const float A = a11, Bq = b1 - su;
+        nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
+        phr = hr;
+      }
+      ring_s[(d % kSfD) * NR + y + 1] = nw;
+      if (LAST && (unsigned)x < (unsigned)w && y < h) {
+        const unsigned oo = f0 + (unsigned)(prow(d) * h + y);
+        *reinterpret_cast<float *>(reinterpret_cast<char *>(a.du) + (size_t)oo * 4u) = nw.x;
+        if (MODE == 0) *reinterpret_cast<float *>(reinterpret_cast<char *>(a.dv) + (size_t)oo * 4u) = nw.y;
+      }
+      pp = nw;
+      pvv = vv;
+      cnt_publish(cnt + C_SOR + SI * G + g, d + 1);
+    }
+  }
+};
+
+template <int S, int MODE, int G>
+__global__ __launch_bounds__((64 * SorFlow<S, MODE, G>::NW)) void k_tv_sorflow(TvArgs a) {
+  using F = SorFlow<S, MODE, G>;
+  extern __shared__ __attribute__((aligned(16))) char sf_lds[];
+  for (int i = threadIdx.x; i < (int)(F::LDS / 16); i += blockDim.x)
+    reinterpret_cast<float4 *>(sf_lds)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  F fl(a, sf_lds, blockIdx.x);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid < S * G) {
+    const int s = wid / G, g = wid - s * G;
+    if (s == 0) fl.template run_sor<0>(g, lane);
+    else if (s == 1) fl.template run_sor<(S > 1 ? 1 : 0)>(g, lane);
+    else if (s == 2) fl.template run_sor<(S > 2 ? 2 : 0)>(g, lane);
+    else fl.template run_sor<(S > 3 ? 3 : 0)>(g, lane);
+  } else {
+    fl.run_l(lane);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && cnt_load(fl.cnt + F::C_ABORT) && a.flow_err) atomicAdd(a.flow_err, 1);
+}
+
+template <int S, int MODE, int G>
+void launch_sorflow(const TvArgs &a, hipStream_t s) {
+  using F = SorFlow<S, MODE, G>;
+  static_assert(F::LDS <= 64 * 1024, "LDS");
+  static_assert(2 * kSfLB * F::NDMA_ROW < 64, "loader batches in flight");
+  k_tv_sorflow<S, MODE, G><<<a.n, 64 * F::NW, F::LDS, s>>>(a);
+}
+template <int S, int MODE>
+bool sorflow_s(const TvArgs &a, hipStream_t s, bool run) {
+  if (a.h <= 64) {
+    if (run) launch_sorflow<S, MODE, 1>(a, s);
+    return true;
+  }
+  if (a.h <= 128) {
+    if (run) launch_sorflow<S, MODE, 2>(a, s);
+    return true;
+  }
+  return false;
+}
+bool sorflow_go(const TvArgs &a, hipStream_t s, bool run) {
+  const int mode = a.nop == 2 ? 0 : 2;
+  switch (a.solverit) {
+    case 2: return mode == 0 ? sorflow_s<2, 0>(a, s, run) : sorflow_s<2, 2>(a, s, run);
+    case 3: return mode == 0 ? sorflow_s<3, 0>(a, s, run) : sorflow_s<3, 2>(a, s, run);
+    default: return false;
+  }
+}
+
 }  // namespace
 
 // The dataflow iteration runs where its rings fit: up to 64 rows (lane = row), 2 or 3 sweeps, the
@@ -530,6 +811,14 @@ bool tv_flow_ok(const TvArgs &a) {
   return flow_go(a, nullptr, false);
 }
 void launch_tv_flow(const TvArgs &a, hipStream_t s) { flow_go(a, s, true); }
+
+// The barrier-free SOR: exact order, 2 or 3 sweeps, 2 .. 128 rows (option sor_flow); the system launch runs first.
+bool tv_sorflow_ok(const TvArgs &a) {
+  if (!a.sor_flow || a.sor_redblack || a.sor_point || a.sor_generic || a.sor_variant == 1) return false;
+  if (a.w < 2 || a.h < 2) return false;
+  return sorflow_go(a, nullptr, false);
+}
+void launch_tv_sorflow(const TvArgs &a, hipStream_t s) { sorflow_go(a, s, true); }
 
 __device__ int g_flow_err;
 #ifdef OFDIS_FLOW_PROBE
