@@ -201,9 +201,10 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
  *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
- *   "sor_flow" (0/1, default 1): levels of up to 128 rows run the exact-order SOR as sweep waves that hand the
+ *   "sor_flow" (0/1, default 0): levels of up to 128 rows run the exact-order SOR as sweep waves that hand the
  *                        diagonals to each other through LDS progress counters instead of workgroup barriers, fed
- *                        by an LDS-DMA loader wave (0: the barrier-synchronised sweep-per-wave SOR);
+ *                        by an LDS-DMA loader wave (0: the barrier-synchronised sweep-per-wave SOR; opt-in: measured
+ *                        ~3x slower per launch);
  *   "tv_flow" (0/1, default 0): levels of up to 64 rows run each TV inner iteration (smoothness, system and
  *                        the exact-order SOR) as one launch whose waves hand the diagonals to each other through
  *                        LDS (no coefficient round trip through HBM; measured slower than the system and SOR

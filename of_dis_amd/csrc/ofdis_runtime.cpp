@@ -96,7 +96,8 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
-  int opt_sor_flow = 1;        // exact-order SOR of levels <= 128 rows as the barrier-free k_tv_sorflow
+  int opt_sor_flow = 0;        // exact-order SOR of levels <= 128 rows as the barrier-free k_tv_sorflow (opt-in:
+                               // measured ~3x slower per launch than k_tv_sor_lanes)
   int opt_tv_flow = 0;         // one dataflow launch per TV inner iteration (k_tv_flow) where it fits (opt-in:
                                // measured slower than the two launches)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
