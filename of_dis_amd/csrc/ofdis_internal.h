@@ -70,6 +70,7 @@ struct PatchArgs {
   int generic;                                // 1: force the any-shape kernel k_patchg (parity testing)
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
   int quad;                                   // four lanes per patch (k_patchq) where the shape has that form
+  int x16;                                    // sixteen lanes per patch (k_patchx) for RGB p = 12
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;

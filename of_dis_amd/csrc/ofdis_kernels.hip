@@ -1854,6 +1854,307 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   if (live && s4 < NOP) a.p_iter[gp * NOP + s4] = s4 == 0 ? p0 : p1;
 }
 
+// ------------------------------------------------------------------ DIS patches, sixteen lanes per patch (round 4)
+// The big RGB shape (p = 12, 432 values) holds 54 values per lane on eight lanes: template + two gradients alone
+// are 162 VGPRs, so k_patchw spills at two waves per SIMD and reads every tap twice (LEAN).  Here sixteen lanes
+// share a patch (four patches per wave): lane s holds the values s + 16 m (m = 0 .. NV/16 - 1), which are Eigen
+// packet slot j = s & 7 of the 8-value blocks k = 2 m + (s >> 3).  Everything per value -- taps, bilinear sample,
+// loss, products -- runs on all sixteen lanes, the samples stay in registers; Eigen's eight slot chains stay
+// sequential in block order on the owner lanes s < 8: block 2m is the owner's own value, block 2m + 1 its
+// partner's (lane s + 8, moved by DPP row_ror:8), added in that order.  The same additions in the same order as
+// k_patchw / k_patch8, so the same bits; the lanes s >= 8 get the totals from their owners by one DPP move.
+template <int P, int NOC>
+struct XShape {
+  static constexpr int NV = P * P * NOC;
+  static constexpr int M = NV / 16;         // values per lane
+  static constexpr int ROWV = P * NOC;      // values per patch row
+  static constexpr int WR = (P + 1) * NOC;  // window row (floats)
+  static constexpr int Q4 = (WR + 3) / 4;   // 16-byte loads per window row
+  static constexpr int RS = Q4 * 4;         // LDS row stride (floats)
+  // windows 16 (mod 32) dwords apart: the two patches of a 32-lane half read disjoint bank halves
+  static constexpr int WIN = (P + 1) * RS + (16 - ((P + 1) * RS) % 32 + 32) % 32;
+  static constexpr int NQ = (P + 1) * Q4;   // 16-byte loads per window
+  static constexpr int LPL = (NQ + 15) / 16;
+  static constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
+  // value m -> m + KP of a lane advances its taps by KROWS whole patch rows
+  static constexpr int KP = (16 / gcd(16, ROWV) * ROWV) / 16;
+  static constexpr int KROWS = 16 * KP / ROWV;
+  static_assert(NV % 16 == 0, "sixteen-lane form: p * p * noc a multiple of 16");
+};
+
+// Eigen's chain of one packet slot, folded on the owner lanes in block order (see above).
+struct XAcc {
+  float acc = 0.0f;
+  __device__ __forceinline__ void add(int m, float x) {  // values of blocks 2m (own) and 2m + 1 (partner)
+    const float part = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
+    acc = m == 0 ? x : acc + x;
+    acc = acc + part;
+  }
+  // res0 + res1, (l0 + l2) + (l1 + l3) on the owners, then the owners' totals to lanes 8 .. 15
+  __device__ __forceinline__ float total() const {
+    float r = acc + grp_xor4(acc);
+    r = r + grp_xor2(r);
+    r = r + grp_xor1(r);
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, r), __builtin_bit_cast(int, r),
+                                                                 0x128, 0xF, 0xC, false));
+  }
+};
+
+template <int NOP, int P, int NOC, int MINW, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchx(PatchArgs a) {
+  const uint3 xb = xcd_block();
+  using S = XShape<P, NOC>;
+  constexpr int M = S::M, RS = S::RS, KP = S::KP;
+  extern __shared__ __attribute__((aligned(16))) float win_all[];
+  const LevelGeom &g = a.g;
+  const int s16 = threadIdx.x & 15;
+  const long gp = (long)xb.x * 16 + (threadIdx.x >> 4);
+  const bool live = gp < (long)a.n * g.npatch;
+  const long gq = live ? gp : 0;
+  const int f = (int)(gq / g.npatch), ip = (int)(gq % g.npatch);
+  const int pxi = ip / g.noph, pyi = ip % g.noph;
+  const float ptr0 = (float)(pxi * a.steps + g.offw), ptr1 = (float)(pyi * a.steps + g.offh);
+  const long fs = (long)g.W * g.H * NOC;
+  const int W = g.W;
+  constexpr float inv_n = 1.0f / (float)S::NV;
+  constexpr bool pow2 = (S::NV & (S::NV - 1)) == 0;
+  auto div_n = [&](float x) {
+    if constexpr (pow2)
+      return x * inv_n;
+    else
+      return div_by_const<S::NV>(x);
+  };
+  float *win = win_all + (threadIdx.x >> 4) * S::WIN;
+  // window offset of the D tap of value m: dbase[m mod KP] + (m / KP) KROWS RS
+  auto dtap = [&](int v) { return (v / S::ROWV) * RS + v % S::ROWV; };
+  int dbase[KP < M ? KP : M];
+#pragma unroll
+  for (int i = 0; i < (KP < M ? KP : M); ++i) dbase[i] = dtap(s16 + 16 * i);
+  // ---- template + gradients at the integer reference position (getPatchStaticNNGrad, patch.cpp:297-343)
+  float tmp[M], gx[M], gy[NOP == 2 ? M : 1];
+  {
+    const int px = (int)roundf(ptr0) + g.pad, py = (int)roundf(ptr1) + g.pad;
+    const long base = ((long)(py - P / 2) * W + (px - P / 2)) * NOC;
+    const float *A = a.img_a + f * fs + base, *DX = a.dx_a + f * fs + base, *DY = a.dy_a + f * fs + base;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int v = s16 + 16 * m;
+      const int o = (v / S::ROWV) * W * NOC + v % S::ROWV;
+      tmp[m] = A[o];
+      gx[m] = DX[o];
+      if constexpr (NOP == 2) gy[m] = DY[o];
+    }
+  }
+  if (a.patnorm > 0) {
+    XAcc mc;
+#pragma unroll
+    for (int m = 0; m < M; ++m) mc.add(m, tmp[m]);
+    const float mean = div_n(mc.total());
+#pragma unroll
+    for (int m = 0; m < M; ++m) tmp[m] = tmp[m] - mean;
+  }
+  // ---- ComputeHessian (patch.cpp:69-86)
+  float H00, H01 = 0.0f, H11 = 0.0f;
+  {
+    XAcc h0, h1, h2;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      h0.add(m, gx[m] * gx[m]);
+      if constexpr (NOP == 2) {
+        h1.add(m, gx[m] * gy[m]);
+        h2.add(m, gy[m] * gy[m]);
+      }
+    }
+    H00 = h0.total();
+    if (NOP == 2) {
+      H01 = h1.total();
+      H11 = h2.total();
+      if (H00 * H11 - H01 * H01 == 0.0f) {
+        H00 = (float)((double)H00 + 1e-10);
+        H11 = (float)((double)H11 + 1e-10);
+      }
+    } else if (H00 == 0.0f) {
+      H00 = (float)((double)H00 + 1e-10);
+    }
+  }
+  const Llt2 fac = llt2_factor(H00, H01, H11);
+  const float fac1 = llt1_factor(H00);
+  if (a.stage == 1) {  // timing diagnostic "pconst"
+    if (live && s16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[M - 1];
+    return;
+  }
+  // ---- initial parameters (InitializeFromCoarserOF, patchgrid.cpp:195-211)
+  float pin0 = 0.0f, pin1 = 0.0f;
+  if (a.prev) {
+    const int x = (int)floorf(ptr0 / 2), y = (int)floorf(ptr1 / 2);
+    const float *pv = a.prev + (long)f * a.prev_frame_stride + (long)(y * a.prev_w + x) * a.prev_elem_stride;
+    pin0 = pv[0] * 2;
+    if (NOP == 2) pin1 = pv[a.prev_comp_stride] * 2;
+  }
+  if (a.stage == 2) {  // "pconst + pinit"
+    if (live && s16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[M - 1] + pin0 + pin1;
+    return;
+  }
+  const float *Bimg = a.img_b + f * fs;
+  // ---- OptimizeStart (patch.cpp:117-154)
+  float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
+  float pt0 = ptr0 + p0, pt1 = (NOP == 2) ? ptr1 + p1 : ptr1;
+  const float st0 = pt0, st1 = pt1;
+  float sq = (float)1e-10, sq_init = (float)1e-10, mares = (float)1e20, mares_old = (float)1e20;
+  int cnt = 0;
+  bool converged = false;
+  float b0 = 0.0f, b1 = 0.0f;
+  auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
+  int lpos0 = -0x7fffffff, lpos1 = 0;
+  const unsigned wb = (unsigned)(uintptr_t)win;
+  // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
+  auto evaluate = [&](float &r0, float *out, auto store_t) {
+    constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
+    const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
+    const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
+    const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
+    const float rx = pt0 - (float)pos2, ry = pt1 - (float)pos3;
+    const float w0 = rx * ry, w1 = (1 - rx) * ry, w2 = rx * (1 - ry), w3 = (1 - rx) * (1 - ry);
+    const float *Q = Bimg + ((long)(pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC;
+    if (__builtin_amdgcn_ballot_w64(pos0 != lpos0 || pos1 != lpos1) != 0) {
+      lpos0 = pos0;
+      lpos1 = pos1;
+      wave_lds_sync();
+      // the load offsets are recomputed here (an opaque copy of the lane index): hoisted out of the iteration
+      // loop they are 27 more live registers for the whole loop
+      int sl = s16;
+      asm volatile("" : "+v"(sl));
+      float4_u t[S::LPL];
+#pragma unroll
+      for (int j = 0; j < S::LPL; ++j) {
+        const int e = sl + 16 * j, e2 = e < S::NQ ? e : S::NQ - 1;
+        const int row = e2 / S::Q4, c4 = e2 % S::Q4;
+        t[j] = *reinterpret_cast<const float4_u *>(Q + (row * W * NOC + c4 * 4));
+      }
+#pragma unroll
+      for (int j = 0; j < S::LPL; ++j) {
+        const int e = sl + 16 * j, e2 = e < S::NQ ? e : S::NQ - 1;
+        const int row = e2 / S::Q4, c4 = e2 % S::Q4;
+        if (e < S::NQ) *reinterpret_cast<float4_v *>(win + (row * RS + c4 * 4)) = t[j];
+      }
+      wave_lds_sync();
+    }
+    // taps of value m: (D, C) and (B, A) by one ds_read2_b32 each; the next value's reads in flight
+    float pd[M];
+    f2p q[2][2];
+    auto issue = [&](auto mc) {
+      constexpr int m = decltype(mc)::value, o0 = (m / KP) * S::KROWS * RS;
+      constexpr bool imm = o0 + RS + NOC <= 255;
+      constexpr int o = imm ? o0 : 0;
+      const unsigned b = wb + 4u * (unsigned)dbase[m % KP] + (imm ? 0u : 4u * (unsigned)o0);
+      q[m & 1][0] = lds_read2<o, o + NOC>(b);            // D, C
+      q[m & 1][1] = lds_read2<o + RS, o + RS + NOC>(b);  // B, A
+    };
+    issue(std::integral_constant<int, 0>{});
+    XAcc mcc;
+    static_for<M>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      if constexpr (m + 1 < M) {
+        issue(std::integral_constant<int, m + 1>{});
+        lds_wait<2>();
+      } else {
+        lds_wait<0>();
+      }
+      f2p *t = q[m & 1];
+      reg_fence(t[0]);
+      reg_fence(t[1]);
+      const float x = ((w0 * t[1].y + w1 * t[1].x) + w2 * t[0].y) + w3 * t[0].x;
+      pd[m] = x;
+      if (a.patnorm > 0) mcc.add(m, x);
+    });
+    const float mean = a.patnorm > 0 ? div_n(mcc.total()) : 0.0f;
+    XAcc ab, ex, ey;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float d = (pd[m] - mean) - tmp[m];
+      float w, e;
+      if (COST == 0) {
+        e = d;
+        w = fabsf(d);
+      } else if (COST == 1) {
+        w = sqrt_nonneg(fabsf(d));
+        e = copysignf(w, d);
+      } else {
+        w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        e = copysignf(w, d);
+      }
+      if (STORE == 0) {
+        ab.add(m, fabsf(w));
+        ex.add(m, gx[m] * e);
+        if (NOP == 2) ey.add(m, gy[m] * e);
+      } else {
+        out[s16 + 16 * m] = w;
+      }
+    }
+    if (STORE == 0) {
+      r0 = ab.total();
+      b0 = ex.total();
+      if (NOP == 2) b1 = ey.total();
+    }
+  };
+  float *pwo = a.pweight + gq * S::NV;
+  bool start_oob = false, first = true;
+  converged = !live;
+  if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
+#pragma unroll
+    for (int m = 0; m < M; ++m) pwo[s16 + 16 * m] = 0.0f;
+    converged = true;
+    start_oob = true;
+  } else {
+    mares = 1e5f;
+  }
+  for (;;) {
+    if (__builtin_amdgcn_ballot_w64(!converged) == 0) break;
+    if (!converged) {
+      if (!first) {
+        ++cnt;
+        if (NOP == 2) {
+          llt2_solve(fac, b0, b1, d0, d1);
+          p0 = p0 - d0;
+          p1 = p1 - d1;
+        } else {
+          d0 = llt1_solve(fac1, b0);
+          p0 = p0 - d0;
+          p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
+        }
+        pt0 = ptr0 + p0;
+        if (NOP == 2) pt1 = ptr1 + p1;
+        const float ex = st0 - pt0, ey = st1 - pt1;
+        if (ex * ex + ey * ey > a.outlier_sq || oob(pt0, pt1)) {
+          p0 = pin0;
+          p1 = pin1;
+          pt0 = ptr0 + p0;
+          if (NOP == 2) pt1 = ptr1 + p1;
+          converged = true;
+        }
+      }
+      float r0 = 0.0f;
+      evaluate(r0, nullptr, std::integral_constant<int, 0>());
+      // OptimizeComputeErrImg (patch.cpp:275-295)
+      sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
+      if (cnt == 1) sq_init = sq;
+      mares_old = mares;
+      mares = div_n(r0);
+      bool rates = true;
+      if (__builtin_amdgcn_ballot_w64(cnt >= a.min_iter) != 0)
+        rates = (cnt < a.min_iter) | ((sq / sq_init >= a.dp_thresh_sq) & (mares / mares_old <= a.dr_thresh));
+      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) & rates;
+      if (!keep) converged = true;
+    }
+    first = false;
+  }
+  if (live && !start_oob) {
+    float r0;
+    evaluate(r0, pwo, std::integral_constant<int, 1>());
+  }
+  if (live && s16 < NOP) a.p_iter[gp * NOP + s16] = s16 == 0 ? p0 : p1;
+}
+
 // ------------------------------------------------------------------------------------------------ aggregation
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -3949,7 +4250,25 @@ static void patchq(const PatchArgs &a, hipStream_t s) {
     default: k_patchq<2, P, NOC, MINW2, 2><<<grid, 256, lds, s>>>(a); return;
   }
 }
+template <int P, int NOC, int MINW>
+static void patchx(const PatchArgs &a, hipStream_t s) {
+  const long patches = (long)a.n * a.g.npatch;
+  const size_t lds = sizeof(float) * 16 * XShape<P, NOC>::WIN;
+  const dim3 grid(ceil_div(patches, 16));
+  switch (a.costfct * 2 + (a.nop == 2 ? 1 : 0)) {
+    case 0: k_patchx<1, P, NOC, MINW, 0><<<grid, 256, lds, s>>>(a); return;
+    case 1: k_patchx<2, P, NOC, MINW, 0><<<grid, 256, lds, s>>>(a); return;
+    case 2: k_patchx<1, P, NOC, MINW, 1><<<grid, 256, lds, s>>>(a); return;
+    case 3: k_patchx<2, P, NOC, MINW, 1><<<grid, 256, lds, s>>>(a); return;
+    case 4: k_patchx<1, P, NOC, MINW, 2><<<grid, 256, lds, s>>>(a); return;
+    default: k_patchx<2, P, NOC, MINW, 2><<<grid, 256, lds, s>>>(a); return;
+  }
+}
 void launch_patch(const PatchArgs &a, hipStream_t s) {
+  if (a.window && a.x16 && !a.wave_per_patch && !a.generic && a.p == 12 && a.noc == 3) {  // sixteen lanes per patch
+    patchx<12, 3, 3>(a, s);
+    return;
+  }
   if (a.window && a.quad && !a.wave_per_patch && !a.generic) {  // four lanes per patch: gray p = 8 / 12
     switch (a.p * 4 + a.noc) {
       case 8 * 4 + 1: patchq<8, 1, 4, 3>(a, s); return;

@@ -126,6 +126,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
     ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
     ("patch_quad", 0, 1),      # gray p = 8 / 12 on eight lanes per patch (k_patchw) instead of four (k_patchq)
+    ("patch_x16", 0, 1),       # RGB p = 12 on eight lanes per patch (k_patchw) instead of sixteen (k_patchx)
     ("tv_flow", 1, 0),         # levels <= 64 rows: one dataflow launch per inner iteration (k_tv_flow)
     ("sor_flow", 1, 0),        # levels <= 128 rows: the barrier-free k_tv_sorflow instead of the barrier SOR
 ]
