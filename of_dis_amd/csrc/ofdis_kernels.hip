@@ -1886,7 +1886,7 @@ struct XShape {
 struct XAcc {
   float acc = 0.0f;
   __device__ __forceinline__ void add(int m, float x) {  // values of blocks 2m (own) and 2m + 1 (partner)
-    const float part = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
+    const float part = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
     acc = m == 0 ? x : acc + x;
     acc = acc + part;
   }
@@ -1905,6 +1905,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   const uint3 xb = xcd_block();
   using S = XShape<P, NOC>;
   constexpr int M = S::M, RS = S::RS, KP = S::KP;
+  // value groups of KP: pairs of groups (2g, 2g + 1) run packed, an odd last group alone
+  constexpr int NPG = M / KP / 2, NPP = NPG * KP, NS = M - 2 * NPP;
+  static_assert(M % KP == 0 && NS <= KP, "sixteen-lane form: whole value groups");
   extern __shared__ __attribute__((aligned(16))) float win_all[];
   const LevelGeom &g = a.g;
   const int s16 = threadIdx.x & 15;
@@ -1995,6 +1998,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     if (live && s16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[M - 1] + pin0 + pin1;
     return;
   }
+  // template and gradients as value pairs (m, m + KP) of the pair groups, and the values of an odd last group
+  f2p tmp2[NPP > 0 ? NPP : 1], gx2[NPP > 0 ? NPP : 1], gy2[NOP == 2 && NPP > 0 ? NPP : 1];
+  float tmps[NS > 0 ? NS : 1], gxs[NS > 0 ? NS : 1], gys[NOP == 2 && NS > 0 ? NS : 1];
+#pragma unroll
+  for (int j = 0; j < NPP; ++j) {
+    const int m = (j / KP) * 2 * KP + j % KP;
+    tmp2[j] = f2p{tmp[m], tmp[m + KP]};
+    gx2[j] = f2p{gx[m], gx[m + KP]};
+    if constexpr (NOP == 2) gy2[j] = f2p{gy[m], gy[m + KP]};
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    tmps[i] = tmp[2 * NPP + i];
+    gxs[i] = gx[2 * NPP + i];
+    if constexpr (NOP == 2) gys[i] = gy[2 * NPP + i];
+  }
   const float *Bimg = a.img_b + f * fs;
   // ---- OptimizeStart (patch.cpp:117-154)
   float p0 = pin0, p1 = pin1, d0 = 0.0f, d1 = 0.0f;
@@ -2008,8 +2027,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   int lpos0 = -0x7fffffff, lpos1 = 0;
   const unsigned wb = (unsigned)(uintptr_t)win;
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
-  auto evaluate = [&](float &r0, float *out, auto store_t) {
+  // FAST: the loss square roots by sqrt_nonneg_s64 (exact below 2^64; a sum that comes out non-finite makes the
+  // caller redo the evaluation with sqrt_nonneg)
+  auto evaluate = [&](float &r0, float *out, auto store_t, auto fast_t) {
     constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
+    constexpr bool FAST = decltype(fast_t)::value;
     const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
     const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
@@ -2021,76 +2043,132 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       lpos1 = pos1;
       wave_lds_sync();
       // the load offsets are recomputed here (an opaque copy of the lane index): hoisted out of the iteration
-      // loop they are 27 more live registers for the whole loop
+      // loop they are 27 more live registers for the whole loop.  Load e of the window is 16-byte column e mod Q4
+      // of window row e / Q4; in LDS (row stride RS = 4 Q4) it lands at float 4 e.
       int sl = s16;
       asm volatile("" : "+v"(sl));
+      sl &= 15;
+      const int gstride = W * NOC - RS;
       float4_u t[S::LPL];
 #pragma unroll
       for (int j = 0; j < S::LPL; ++j) {
         const int e = sl + 16 * j, e2 = e < S::NQ ? e : S::NQ - 1;
-        const int row = e2 / S::Q4, c4 = e2 % S::Q4;
-        t[j] = *reinterpret_cast<const float4_u *>(Q + (row * W * NOC + c4 * 4));
+        t[j] = *reinterpret_cast<const float4_u *>(Q + ((e2 / S::Q4) * gstride + 4 * e2));
       }
 #pragma unroll
       for (int j = 0; j < S::LPL; ++j) {
-        const int e = sl + 16 * j, e2 = e < S::NQ ? e : S::NQ - 1;
-        const int row = e2 / S::Q4, c4 = e2 % S::Q4;
-        if (e < S::NQ) *reinterpret_cast<float4_v *>(win + (row * RS + c4 * 4)) = t[j];
+        const int e = sl + 16 * j;
+        if (e < S::NQ) *reinterpret_cast<float4_v *>(win + 4 * e) = t[j];
       }
       wave_lds_sync();
     }
-    // taps of value m: (D, C) and (B, A) by one ds_read2_b32 each; the next value's reads in flight
-    float pd[M];
-    f2p q[2][2];
-    auto issue = [&](auto mc) {
-      constexpr int m = decltype(mc)::value, o0 = (m / KP) * S::KROWS * RS;
-      constexpr bool imm = o0 + RS + NOC <= 255;
-      constexpr int o = imm ? o0 : 0;
-      const unsigned b = wb + 4u * (unsigned)dbase[m % KP] + (imm ? 0u : 4u * (unsigned)o0);
-      q[m & 1][0] = lds_read2<o, o + NOC>(b);            // D, C
-      q[m & 1][1] = lds_read2<o + RS, o + RS + NOC>(b);  // B, A
+    // taps: value pairs (m, m + KP) -- their taps are KROWS patch rows apart whatever the lane, so each tap of a
+    // pair is one ds_read2_b32 into a register pair and the bilinear sample runs packed; the values of a last
+    // odd group of KP alone, (D, C) and (B, A) per ds_read2_b32.  The next unit's reads are in flight while a
+    // unit is computed.
+    constexpr int PD = S::KROWS * RS;
+    f2p pd2[NPP > 0 ? NPP : 1];
+    float pds[NS > 0 ? NS : 1];
+    f2p q[2][4];
+    auto issue = [&](auto uc) {  // unit u: pairs 0 .. NPP - 1, then singles
+      constexpr int u = decltype(uc)::value;
+      if constexpr (u < NPP) {
+        constexpr int i = u % KP, o0 = 2 * (u / KP) * PD;
+        constexpr bool imm = o0 + RS + NOC + PD <= 255;
+        constexpr int o = imm ? o0 : 0;
+        const unsigned b = wb + 4u * (unsigned)dbase[i] + (imm ? 0u : 4u * (unsigned)o0);
+        q[u & 1][0] = lds_read2<o, o + PD>(b);                        // D
+        q[u & 1][1] = lds_read2<o + NOC, o + NOC + PD>(b);            // C
+        q[u & 1][2] = lds_read2<o + RS, o + RS + PD>(b);              // B
+        q[u & 1][3] = lds_read2<o + RS + NOC, o + RS + NOC + PD>(b);  // A
+      } else {
+        constexpr int i = u - NPP, o0 = (2 * NPP / KP) * PD;
+        constexpr bool imm = o0 + RS + NOC <= 255;
+        constexpr int o = imm ? o0 : 0;
+        const unsigned b = wb + 4u * (unsigned)dbase[i] + (imm ? 0u : 4u * (unsigned)o0);
+        q[u & 1][0] = lds_read2<o, o + NOC>(b);            // D, C
+        q[u & 1][1] = lds_read2<o + RS, o + RS + NOC>(b);  // B, A
+      }
     };
     issue(std::integral_constant<int, 0>{});
-    XAcc mcc;
-    static_for<M>([&](auto mc) {
-      constexpr int m = decltype(mc)::value;
-      if constexpr (m + 1 < M) {
-        issue(std::integral_constant<int, m + 1>{});
-        lds_wait<2>();
+    static_for<NPP + NS>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if constexpr (u + 1 < NPP + NS) {
+        issue(std::integral_constant<int, u + 1>{});
+        lds_wait<(u + 1 < NPP ? 4 : 2)>();
       } else {
         lds_wait<0>();
       }
-      f2p *t = q[m & 1];
-      reg_fence(t[0]);
-      reg_fence(t[1]);
-      const float x = ((w0 * t[1].y + w1 * t[1].x) + w2 * t[0].y) + w3 * t[0].x;
-      pd[m] = x;
-      if (a.patnorm > 0) mcc.add(m, x);
+      f2p *t = q[u & 1];
+      if constexpr (u < NPP) {
+        static_for<4>([&](auto ic) { reg_fence(t[decltype(ic)::value]); });
+        f2p x = t[3] * w0 + t[2] * w1;
+        x = x + t[1] * w2;
+        x = x + t[0] * w3;
+        pd2[u] = x;
+      } else {
+        reg_fence(t[0]);
+        reg_fence(t[1]);
+        pds[u - NPP] = ((w0 * t[1].y + w1 * t[1].x) + w2 * t[0].y) + w3 * t[0].x;
+      }
     });
-    const float mean = a.patnorm > 0 ? div_n(mcc.total()) : 0.0f;
-    XAcc ab, ex, ey;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const float d = (pd[m] - mean) - tmp[m];
-      float w, e;
+    auto pdv = [&](int m) -> float {  // compile-time m: the sample of value m
+      const int gi = m / KP, i = m % KP;
+      if (gi < 2 * NPG) return gi % 2 == 0 ? pd2[(gi / 2) * KP + i].x : pd2[(gi / 2) * KP + i].y;
+      return pds[i];
+    };
+    float mean = 0.0f;
+    if (a.patnorm > 0) {
+      XAcc mc;
+      static_for<M>([&](auto mc_) {
+        constexpr int m = decltype(mc_)::value;
+        mc.add(m, pdv(m));
+      });
+      mean = div_n(mc.total());
+    }
+    // loss of one value: w (weight) and e (signed residual)
+    auto loss = [&](float d, float &w, float &e) {
       if (COST == 0) {
         e = d;
         w = fabsf(d);
-      } else if (COST == 1) {
-        w = sqrt_nonneg(fabsf(d));
-        e = copysignf(w, d);
       } else {
-        w = sqrt_nonneg((sqrt_nonneg(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        auto sq = [](float x) { return FAST ? sqrt_nonneg_s64(x) : sqrt_nonneg(x); };
+        w = COST == 1 ? sq(fabsf(d)) : sq((sq(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
         e = copysignf(w, d);
       }
-      if (STORE == 0) {
-        ab.add(m, fabsf(w));
-        ex.add(m, gx[m] * e);
-        if (NOP == 2) ey.add(m, gy[m] * e);
+    };
+    XAcc ab, ex, ey;
+    // pair groups: d of both halves packed; the .x halves (values m) go into the chains at once, the .y halves'
+    // d (values m + KP) are kept until their turn, after the group's KP .x values
+    auto value_out = [&](int m, float d, float gxv, float gyv) {  // compile-time m
+      float w, e;
+      loss(d, w, e);
+      if constexpr (STORE == 0) {
+        ab.add(m, w);  // w >= +0 for every cost (|d| or a square root): |w| == w
+        ex.add(m, gxv * e);
+        if constexpr (NOP == 2) ey.add(m, gyv * e);
       } else {
         out[s16 + 16 * m] = w;
       }
-    }
+    };
+    static_for<NPG>([&](auto gc) {
+      constexpr int gg = decltype(gc)::value;
+      float dy[KP];
+      static_for<KP>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, j = gg * KP + i;
+        const f2p d = (pd2[j] - mean) - tmp2[j];
+        dy[i] = d.y;
+        value_out(2 * gg * KP + i, d.x, gx2[j].x, NOP == 2 ? gy2[j].x : 0.0f);
+      });
+      static_for<KP>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, j = gg * KP + i;
+        value_out(2 * gg * KP + KP + i, dy[i], gx2[j].y, NOP == 2 ? gy2[j].y : 0.0f);
+      });
+    });
+    static_for<NS>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gxs[i], NOP == 2 ? gys[i] : 0.0f);
+    });
     if (STORE == 0) {
       r0 = ab.total();
       b0 = ex.total();
@@ -2134,7 +2212,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         }
       }
       float r0 = 0.0f;
-      evaluate(r0, nullptr, std::integral_constant<int, 0>());
+      evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type());
+      if (COST != 0 && __builtin_amdgcn_ballot_w64(!(r0 <= 3.402823466e38f)) != 0)
+        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type());
       // OptimizeComputeErrImg (patch.cpp:275-295)
       sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
       if (cnt == 1) sq_init = sq;
@@ -2150,7 +2230,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   if (live && !start_oob) {
     float r0;
-    evaluate(r0, pwo, std::integral_constant<int, 1>());
+    evaluate(r0, pwo, std::integral_constant<int, 1>(), std::false_type());
   }
   if (live && s16 < NOP) a.p_iter[gp * NOP + s16] = s16 == 0 ? p0 : p1;
 }
