@@ -1885,10 +1885,16 @@ struct XShape {
 // Eigen's chain of one packet slot, folded on the owner lanes in block order (see above).
 struct XAcc {
   float acc = 0.0f;
-  __device__ __forceinline__ void add(int m, float x) {  // values of blocks 2m (own) and 2m + 1 (partner)
-    const float part = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
-    acc = m == 0 ? x : acc + x;
-    acc = acc + part;
+  // values of blocks 2m (own) and 2m + 1 (partner), in two steps: callers with several chains issue every chain's
+  // own() before the partner() adds, so no DPP add reads an accumulator written by the instruction just before
+  // it (a DPP source VGPR needs two wait states after its VALU write)
+  __device__ __forceinline__ void own(int m, float x) { acc = m == 0 ? x : acc + x; }
+  __device__ __forceinline__ void partner(float x) {
+    acc = acc + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
+  }
+  __device__ __forceinline__ void add(int m, float x) {
+    own(m, x);
+    partner(x);
   }
   // res0 + res1, (l0 + l2) + (l1 + l3) on the owners, then the owners' totals to lanes 8 .. 15
   __device__ __forceinline__ float total() const {
@@ -1962,10 +1968,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     XAcc h0, h1, h2;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      h0.add(m, gx[m] * gx[m]);
+      const float a0 = gx[m] * gx[m], a1 = NOP == 2 ? gx[m] * gy[m] : 0.0f, a2 = NOP == 2 ? gy[m] * gy[m] : 0.0f;
+      h0.own(m, a0);
       if constexpr (NOP == 2) {
-        h1.add(m, gx[m] * gy[m]);
-        h2.add(m, gy[m] * gy[m]);
+        h1.own(m, a1);
+        h2.own(m, a2);
+      }
+      h0.partner(a0);
+      if constexpr (NOP == 2) {
+        h1.partner(a1);
+        h2.partner(a2);
       }
     }
     H00 = h0.total();
@@ -2140,13 +2152,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     XAcc ab, ex, ey;
     // pair groups: d of both halves packed; the .x halves (values m) go into the chains at once, the .y halves'
     // d (values m + KP) are kept until their turn, after the group's KP .x values
-    auto value_out = [&](int m, float d, float gxv, float gyv) {  // compile-time m
+    // chain adds run one value behind the products: a DPP source written by the instruction just before needs wait
+    // states (s_nop), the previous value's products were written long before
+    float pw = 0.0f, pqx = 0.0f, pqy = 0.0f;
+    auto flush = [&](int m) {  // compile-time m: value m's terms into the chains
+      ab.own(m, pw);  // w >= +0 for every cost (|d| or a square root): |w| == w
+      ex.own(m, pqx);
+      if constexpr (NOP == 2) ey.own(m, pqy);
+      ab.partner(pw);
+      ex.partner(pqx);
+      if constexpr (NOP == 2) ey.partner(pqy);
+    };
+    auto value_out = [&](int m, float d, float gxv, float gyv) {  // compile-time m, in increasing order
       float w, e;
       loss(d, w, e);
       if constexpr (STORE == 0) {
-        ab.add(m, w);  // w >= +0 for every cost (|d| or a square root): |w| == w
-        ex.add(m, gxv * e);
-        if constexpr (NOP == 2) ey.add(m, gyv * e);
+        const float qx = gxv * e, qy = NOP == 2 ? gyv * e : 0.0f;
+        if (m > 0) flush(m - 1);
+        pw = w;
+        pqx = qx;
+        pqy = qy;
       } else {
         out[s16 + 16 * m] = w;
       }
@@ -2170,6 +2195,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gxs[i], NOP == 2 ? gys[i] : 0.0f);
     });
     if (STORE == 0) {
+      flush(M - 1);
       r0 = ab.total();
       b0 = ex.total();
       if (NOP == 2) b1 = ey.total();
