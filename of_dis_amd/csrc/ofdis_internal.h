@@ -71,6 +71,9 @@ struct PatchArgs {
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
   int quad;                                   // four lanes per patch (k_patchq) where the shape has that form
   int x16;                                    // sixteen lanes per patch (k_patchx) for RGB p = 12
+  int absw;                                   // 1: write the aggregation weight of every patch pixel (p * p floats per
+                                              // patch) instead of the p * p * noc loss weights, where the kernel can
+                                              // (launch_patch returns whether it did)
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;
@@ -81,6 +84,7 @@ struct AggArgs {
   const float *cg_p_iter, *cg_pweight;  // complementary (backward) grid for usefbcon, or NULL
   float *flow;  // planar [n][nop][h][w]
   int n, nop, noc, p, novals, steps;
+  int absw;     // 1: pweight holds the patch kernel's aggregation weights ([patch][p * p], patch_absw), 0: loss weights
   LevelGeom g;
 };
 
@@ -147,7 +151,7 @@ void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s);
 void launch_pyr_gradmag(const PyrGradmagArgs &a, hipStream_t s);
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s);
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s);
-void launch_patch(const PatchArgs &a, hipStream_t s);
+bool launch_patch(const PatchArgs &a, hipStream_t s);  // true: wrote aggregation weights (PatchArgs::absw)
 void launch_aggregate(const AggArgs &a, hipStream_t s);
 void launch_tv_prep(const TvArgs &a, hipStream_t s);
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s);

@@ -328,6 +328,27 @@ __device__ __forceinline__ float llt1_solve(float L, float b) {
   return y / L;
 }
 
+// The aggregation weight AggregateFlowDense gives patch pixel (lx, ly) -- a pixel of the level (patchgrid.cpp:236-262):
+// 1 / max(2, w) of its loss weight (gray); RGB: the upstream weight pointer advances by 1 for out-of-image pixels and
+// by 3 inside (patchgrid.cpp:243,256-258), so the three weights summed start at ly p + lx + 2 (in-image pixels
+// before it).  (ptx, pty): the patch's reference position.  Used by the aggregation on loss weights and by the patch
+// kernels that hand it the aggregation weights directly (PatchArgs::absw).
+__device__ __forceinline__ float agg_weight(const float *pw, int noc, int p, int w, int h, int ptx, int pty, int lx,
+                                            int ly) {
+  const int hp = p / 2;
+  if (noc == 1) return 1.0f / stdmaxf(2.0f, pw[ly * p + lx]);
+  const int lx0 = max(0, hp - ptx), lx1 = min(p, w - ptx + hp);
+  const int ly0 = max(0, hp - pty), ly1 = min(p, h - pty + hp);
+  const int nin = lx1 - lx0;
+  int before_in = max(0, min(ly, ly1) - ly0) * nin;
+  if (ly >= ly0 && ly < ly1) before_in += max(0, min(lx, lx1) - lx0);
+  const int off = ly * p + lx + 2 * before_in;
+  float absw = stdmaxf(2.0f, pw[off]);
+  absw = absw + stdmaxf(2.0f, pw[off + 1]);
+  absw = absw + stdmaxf(2.0f, pw[off + 2]);
+  return 1.0f / absw;
+}
+
 template <int JM>
 struct PatchCtx {
   const float *B;
@@ -2149,6 +2170,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         e = copysignf(w, d);
       }
     };
+    auto gyp = [&](int j) -> f2p {  // compile-time j (depth: no y gradients)
+      if constexpr (NOP == 2) return gy2[j];
+      return f2p{0.0f, 0.0f};
+    };
+    auto gys_ = [&](int i) -> float {
+      if constexpr (NOP == 2) return gys[i];
+      return 0.0f;
+    };
     XAcc ab, ex, ey;
     // pair groups: d of both halves packed; the .x halves (values m) go into the chains at once, the .y halves'
     // d (values m + KP) are kept until their turn, after the group's KP .x values
@@ -2183,16 +2212,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         constexpr int i = decltype(ic)::value, j = gg * KP + i;
         const f2p d = (pd2[j] - mean) - tmp2[j];
         dy[i] = d.y;
-        value_out(2 * gg * KP + i, d.x, gx2[j].x, NOP == 2 ? gy2[j].x : 0.0f);
+        value_out(2 * gg * KP + i, d.x, gx2[j].x, gyp(j).x);
       });
       static_for<KP>([&](auto ic) {
         constexpr int i = decltype(ic)::value, j = gg * KP + i;
-        value_out(2 * gg * KP + KP + i, dy[i], gx2[j].y, NOP == 2 ? gy2[j].y : 0.0f);
+        value_out(2 * gg * KP + KP + i, dy[i], gx2[j].y, gyp(j).y);
       });
     });
     static_for<NS>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gxs[i], NOP == 2 ? gys[i] : 0.0f);
+      value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gxs[i], gys_(i));
     });
     if (STORE == 0) {
       flush(M - 1);
@@ -2201,12 +2230,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (NOP == 2) b1 = ey.total();
     }
   };
-  float *pwo = a.pweight + gq * S::NV;
+  // absw: the patch's aggregation weights, p * p floats (agg_weight of each pixel), instead of its loss weights
+  float *pwo = a.pweight + gq * (a.absw ? P * P : S::NV);
   bool start_oob = false, first = true;
   converged = !live;
   if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
+    if (!a.absw) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) pwo[s16 + 16 * m] = 0.0f;
+      for (int m = 0; m < M; ++m) pwo[s16 + 16 * m] = 0.0f;
+    }
     converged = true;
     start_oob = true;
   } else {
@@ -2254,7 +2286,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     }
     first = false;
   }
-  if (live && !start_oob) {
+  if (a.absw) {
+    // the loss weights into the patch's LDS window (its tap reads are complete: one wave, LDS in order), then
+    // each lane the aggregation weights of pixels s16 + 16 i from there
+    if (live && !start_oob) {
+      float r0;
+      evaluate(r0, win, std::integral_constant<int, 1>(), std::false_type());
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) win[s16 + 16 * m] = 0.0f;
+    }
+    wave_lds_sync();
+    if (live) {
+      const int ptx = (int)ptr0, pty = (int)ptr1;
+#pragma unroll
+      for (int i = 0; i < (P * P + 15) / 16; ++i) {
+        const int q = s16 + 16 * i, lx = q % P, ly = q / P;
+        const int x = ptx - P / 2 + lx, y = pty - P / 2 + ly;
+        if (q < P * P)
+          pwo[q] = (x >= 0 && y >= 0 && x < g.w && y < g.h) ? agg_weight(win, NOC, P, g.w, g.h, ptx, pty, lx, ly) : 0.0f;
+      }
+    }
+  } else if (live && !start_oob) {
     float r0;
     evaluate(r0, pwo, std::integral_constant<int, 1>(), std::false_type());
   }
@@ -2286,22 +2339,7 @@ __device__ __forceinline__ void aggregate_own(const AggArgs &a, int x, int y, in
       const int ly = y - pty + hp;
       const int ip = px * g.noph + py;
       const float *pw = PW + (long)ip * a.novals;
-      float absw;
-      if (a.noc == 1) {
-        absw = 1.0f / stdmaxf(2.0f, pw[ly * a.p + lx]);
-      } else {
-        // upstream weight pointer advances by 1 for out-of-image pixels and by 3 inside (patchgrid.cpp:243,256-258)
-        const int lx0 = max(0, hp - ptx), lx1 = min(a.p, g.w - ptx + hp);
-        const int ly0 = max(0, hp - pty), ly1 = min(a.p, g.h - pty + hp);
-        const int nin = lx1 - lx0;
-        int before_in = max(0, min(ly, ly1) - ly0) * nin;
-        if (ly >= ly0 && ly < ly1) before_in += max(0, min(lx, lx1) - lx0);
-        const int off = ly * a.p + lx + 2 * before_in;
-        absw = stdmaxf(2.0f, pw[off]);
-        absw = absw + stdmaxf(2.0f, pw[off + 1]);
-        absw = absw + stdmaxf(2.0f, pw[off + 2]);
-        absw = 1.0f / absw;
-      }
+      const float absw = a.absw ? pw[ly * a.p + lx] : agg_weight(pw, a.noc, a.p, g.w, g.h, ptx, pty, lx, ly);
       we = we + absw;
       f0 = f0 + PI[ip * a.nop] * absw;
       if (a.nop == 2) f1 = f1 + PI[ip * a.nop + 1] * absw;
@@ -4370,11 +4408,18 @@ static void patchx(const PatchArgs &a, hipStream_t s) {
     default: k_patchx<2, P, NOC, MINW, 2><<<grid, 256, lds, s>>>(a); return;
   }
 }
-void launch_patch(const PatchArgs &a, hipStream_t s) {
+void launch_patch_loss(const PatchArgs &a, hipStream_t s);
+bool launch_patch(const PatchArgs &a, hipStream_t s) {
   if (a.window && a.x16 && !a.wave_per_patch && !a.generic && a.p == 12 && a.noc == 3) {  // sixteen lanes per patch
     patchx<12, 3, 3>(a, s);
-    return;
+    return a.absw != 0;
   }
+  PatchArgs b = a;
+  b.absw = 0;  // the other kernels write the loss weights
+  launch_patch_loss(b, s);
+  return false;
+}
+void launch_patch_loss(const PatchArgs &a, hipStream_t s) {
   if (a.window && a.quad && !a.wave_per_patch && !a.generic) {  // four lanes per patch: gray p = 8 / 12
     switch (a.p * 4 + a.noc) {
       case 8 * 4 + 1: patchq<8, 1, 4, 3>(a, s); return;

@@ -103,6 +103,7 @@ struct ofdis_context {
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw)
+  int opt_patch_absw = 1;      // patch kernels that can hand the aggregation its weights directly do (0: loss weights)
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
@@ -402,6 +403,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.window = c->opt_patch_window;
     pa.quad = c->opt_patch_quad;
     pa.x16 = c->opt_patch_x16;
+    pa.absw = !P.fb && c->opt_patch_absw;  // usefbcon: the complementary grid's loss weights are read raw
     pa.generic = c->opt_patch_generic;
     pa.g = g;
     if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
@@ -413,7 +415,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       launch_patch(pd, s);
       HIP_OK(hipEventRecord(ev[2], s));
     }
-    timed(c, 3, s, [&] { launch_patch(pa, s); });
+    bool absw = false;
+    timed(c, 3, s, [&] { absw = launch_patch(pa, s); });
     // usefbcon: the backward grid -- template on image b, target image a, right camera (camlr = 1),
     // initialised from the coarser backward flow (oflow.cpp:158-169, 193-196, 209-211, 231-233)
     PatchArgs pb = pa;
@@ -438,7 +441,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     ag.nop = nop;
     ag.noc = noc;
     ag.p = p->p_samp_s;
-    ag.novals = novals;
+    ag.novals = absw ? p->p_samp_s * p->p_samp_s : novals;
+    ag.absw = absw;
     ag.steps = steps;
     ag.g = g;
     ag.cg_p_iter = P.fb ? pb.p_iter : nullptr;
@@ -1245,7 +1249,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
-      {"patch_x16", &ofdis_context::opt_patch_x16, 0, 1},
+      {"patch_x16", &ofdis_context::opt_patch_x16, 0, 1},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},      {"sor_flow", &ofdis_context::opt_sor_flow, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
