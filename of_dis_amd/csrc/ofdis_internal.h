@@ -71,9 +71,10 @@ struct PatchArgs {
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
   int quad;                                   // four lanes per patch (k_patchq) where the shape has that form
   int x16;                                    // sixteen lanes per patch (k_patchx) for RGB p = 12
-  int absw;                                   // 1: write the aggregation weight of every patch pixel (p * p floats per
-                                              // patch) instead of the p * p * noc loss weights, where the kernel can
-                                              // (launch_patch returns whether it did)
+  int absw;                                   // 1: write the aggregation weight of every patch pixel into the slot
+                                              // planes (agg_plane_off) instead of the loss weights, where the kernel
+                                              // can (launch_patch returns whether it did)
+  int aslots;                                 // A = (p - 1) / steps + 1: slot planes per axis
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;
@@ -84,7 +85,8 @@ struct AggArgs {
   const float *cg_p_iter, *cg_pweight;  // complementary (backward) grid for usefbcon, or NULL
   float *flow;  // planar [n][nop][h][w]
   int n, nop, noc, p, novals, steps;
-  int absw;     // 1: pweight holds the patch kernel's aggregation weights ([patch][p * p], patch_absw), 0: loss weights
+  int absw;     // 1: pweight holds the patch kernel's aggregation weights as slot planes ([n][A * A][h][w]), 0: loss weights
+  int aslots;   // A
   LevelGeom g;
 };
 

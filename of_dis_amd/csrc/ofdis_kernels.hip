@@ -349,6 +349,15 @@ __device__ __forceinline__ float agg_weight(const float *pw, int noc, int p, int
   return 1.0f / absw;
 }
 
+// Aggregation-weight slot planes (PatchArgs::absw / AggArgs::absw): per frame A * A planes of the level's w x h,
+// A = (p - 1) / steps + 1 -- the most patches of one grid column (row) that cover a pixel, consecutive in px (py),
+// so (px mod A, py mod A) tells apart every patch covering a pixel.  Patch (px, py) writes agg_weight of its pixel
+// (x, y) at plane (px mod A) A + py mod A, pixel (x, y): each plane pixel is written by at most one patch, and the
+// aggregation reads a pixel's weights as whole coalesced plane rows.
+__device__ __forceinline__ long agg_plane_off(int f, int A, int px, int py, int w, int h, int x, int y) {
+  return (((long)f * A * A + (px % A) * A + (py % A)) * h + y) * w + x;
+}
+
 template <int JM>
 struct PatchCtx {
   const float *B;
@@ -1694,6 +1703,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   auto oob = [&](float x, float y) { return x < g.tmp_lb || y < g.tmp_lb || x > g.tmp_ubw || y > g.tmp_ubh; };
   int lpos0 = -0x7fffffff, lpos1 = 0;
   const unsigned wb = (unsigned)(uintptr_t)win + 4u * (unsigned)s4;  // lane s's taps: wb + 4 * (constant)
+  // absw (gray: value v is pixel v): the aggregation weight of the value's pixel into the slot planes
+  const int ptxi = (int)ptr0, ptyi = (int)ptr1;
+  float *pl = a.absw ? a.pweight + agg_plane_off(f, a.aslots, pxi, pyi, g.w, g.h, ptxi - P / 2, ptyi - P / 2) : nullptr;
+  auto put_agg = [&](int v, float wv) {
+    const int lx = v % P, ly = v / P, x = ptxi - P / 2 + lx, y = ptyi - P / 2 + ly;
+    if (x >= 0 && y >= 0 && x < g.w && y < g.h) pl[ly * g.w + lx] = 1.0f / stdmaxf(2.0f, wv);
+  };
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
   auto evaluate = [&](float &r0, float *out, auto store_t) {
     constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
@@ -1804,8 +1820,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         }
       } else {
         const float wl = COST == 0 ? fabsf(wv.x) : wv.x, wh = COST == 0 ? fabsf(wv.y) : wv.y;
-        out[s4 + 8 * k] = wl;
-        out[s4 + 4 + 8 * k] = wh;
+        if (a.absw) {
+          put_agg(s4 + 8 * k, wl);
+          put_agg(s4 + 4 + 8 * k, wh);
+        } else {
+          out[s4 + 8 * k] = wl;
+          out[s4 + 4 + 8 * k] = wh;
+        }
       }
     });
     if constexpr (STORE == 0) {
@@ -1820,8 +1841,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      pwo[s4 + 8 * k] = 0.0f;
-      pwo[s4 + 4 + 8 * k] = 0.0f;
+      if (a.absw) {
+        put_agg(s4 + 8 * k, 0.0f);
+        put_agg(s4 + 4 + 8 * k, 0.0f);
+      } else {
+        pwo[s4 + 8 * k] = 0.0f;
+        pwo[s4 + 4 + 8 * k] = 0.0f;
+      }
     }
     converged = true;
     start_oob = true;
@@ -2230,8 +2256,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (NOP == 2) b1 = ey.total();
     }
   };
-  // absw: the patch's aggregation weights, p * p floats (agg_weight of each pixel), instead of its loss weights
-  float *pwo = a.pweight + gq * (a.absw ? P * P : S::NV);
+  // absw: the patch's aggregation weights into the slot planes (agg_plane_off) instead of its loss weights
+  float *pwo = a.pweight + gq * S::NV;
   bool start_oob = false, first = true;
   converged = !live;
   if (live && oob(pt0, pt1)) {  // converged at once; pweight never written upstream, defined as 0
@@ -2299,12 +2325,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     wave_lds_sync();
     if (live) {
       const int ptx = (int)ptr0, pty = (int)ptr1;
+      float *pl = a.pweight + agg_plane_off(f, a.aslots, pxi, pyi, g.w, g.h, ptx - P / 2, pty - P / 2);
 #pragma unroll
       for (int i = 0; i < (P * P + 15) / 16; ++i) {
         const int q = s16 + 16 * i, lx = q % P, ly = q / P;
         const int x = ptx - P / 2 + lx, y = pty - P / 2 + ly;
-        if (q < P * P)
-          pwo[q] = (x >= 0 && y >= 0 && x < g.w && y < g.h) ? agg_weight(win, NOC, P, g.w, g.h, ptx, pty, lx, ly) : 0.0f;
+        if (q < P * P && x >= 0 && y >= 0 && x < g.w && y < g.h)
+          pl[ly * g.w + lx] = agg_weight(win, NOC, P, g.w, g.h, ptx, pty, lx, ly);
       }
     }
   } else if (live && !start_oob) {
@@ -2338,8 +2365,8 @@ __device__ __forceinline__ void aggregate_own(const AggArgs &a, int x, int y, in
       const int pty = py * a.steps + g.offh;
       const int ly = y - pty + hp;
       const int ip = px * g.noph + py;
-      const float *pw = PW + (long)ip * a.novals;
-      const float absw = a.absw ? pw[ly * a.p + lx] : agg_weight(pw, a.noc, a.p, g.w, g.h, ptx, pty, lx, ly);
+      const float absw = a.absw ? a.pweight[agg_plane_off(f, a.aslots, px, py, g.w, g.h, x, y)]
+                                : agg_weight(PW + (long)ip * a.novals, a.noc, a.p, g.w, g.h, ptx, pty, lx, ly);
       we = we + absw;
       f0 = f0 + PI[ip * a.nop] * absw;
       if (a.nop == 2) f1 = f1 + PI[ip * a.nop + 1] * absw;
@@ -4412,6 +4439,10 @@ void launch_patch_loss(const PatchArgs &a, hipStream_t s);
 bool launch_patch(const PatchArgs &a, hipStream_t s) {
   if (a.window && a.x16 && !a.wave_per_patch && !a.generic && a.p == 12 && a.noc == 3) {  // sixteen lanes per patch
     patchx<12, 3, 3>(a, s);
+    return a.absw != 0;
+  }
+  if (a.window && a.quad && !a.wave_per_patch && !a.generic && a.noc == 1 && (a.p == 8 || a.p == 12)) {
+    launch_patch_loss(a, s);  // k_patchq: the aggregation weights too
     return a.absw != 0;
   }
   PatchArgs b = a;

@@ -265,8 +265,9 @@ Plan make_plan(const ofdis_params *p, int n, int Wp, int Hp, int pad, bool init 
   }
   P.off_piter = off;
   off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
-  P.off_pw = off;
-  off = align_up(off + sizeof(float) * (size_t)n * max_np * novals);
+  P.off_pw = off;  // loss weights [n][npatch][novals], or the aggregation-weight slot planes [n][A * A][h][w]
+  const size_t aslots = (size_t)((p->p_samp_s - 1) / steps_of(p) + 1);
+  off = align_up(off + sizeof(float) * (size_t)n * std::max(max_np * novals, aslots * aslots * max_plane));
   P.off_piter_bw = off;
   if (P.fb) off = align_up(off + sizeof(float) * (size_t)n * max_np * P.nop);
   P.off_pw_bw = off;
@@ -404,6 +405,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.quad = c->opt_patch_quad;
     pa.x16 = c->opt_patch_x16;
     pa.absw = !P.fb && c->opt_patch_absw;  // usefbcon: the complementary grid's loss weights are read raw
+    pa.aslots = (p->p_samp_s - 1) / steps + 1;
     pa.generic = c->opt_patch_generic;
     pa.g = g;
     if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
@@ -441,8 +443,9 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     ag.nop = nop;
     ag.noc = noc;
     ag.p = p->p_samp_s;
-    ag.novals = absw ? p->p_samp_s * p->p_samp_s : novals;
+    ag.novals = novals;
     ag.absw = absw;
+    ag.aslots = pa.aslots;
     ag.steps = steps;
     ag.g = g;
     ag.cg_p_iter = P.fb ? pb.p_iter : nullptr;
