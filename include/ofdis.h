@@ -189,9 +189,11 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        slot pairs packed (0: eight lanes per patch);
  *   "patch_x16" (0/1, default 1): windowed RGB p = 12 patches on sixteen lanes per patch, the Eigen slot chains
  *                        folded in block order on eight owner lanes (0: eight lanes per patch);
- *   "patch_absw" (0/1, default 1): without usefbcon, the sixteen-lane RGB patch kernel stores each patch pixel's
- *                        aggregation weight (p * p floats per patch) instead of its p * p * noc loss weights,
- *                        so the aggregation reads a third of the bytes (0: loss weights);
+ *   "patch_absw" (0/1, default 1): without usefbcon, the four- and sixteen-lane patch kernels store each patch
+ *                        pixel's aggregation weight into slot planes ([n][A*A][h][w], A = (p-1)/steps + 1) instead
+ *                        of their loss weights, so the aggregation reads coalesced plane rows (0: loss weights);
+ *   "patch_buf" (0/1, default 1): gray p = 12 patch windows by buffer loads with 32-bit offsets where the level's
+ *                        image array spans less than 4 GiB (0: 64-bit address arithmetic per load);
  *   "patch_generic" (0/1, default 0): every patch shape on the any-shape kernel (runtime value loops: the
  *                        default for p*p*noc > 448, e.g. RGB p >= 14, gray p >= 22);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;

@@ -1723,10 +1723,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       lpos0 = pos0;
       lpos1 = pos1;
       wave_lds_sync();
+      bool done = false;
+      if constexpr (S::Q4 == 4 && S::LPL == P + 1) {
+        if (a.buf32) {
+          // window row j is one 16-byte load per lane (column 4 s4) at a wave-uniform row offset: buffer loads off
+          // the image array with the lane's 32-bit byte offset and the row in the scalar offset, no per-load
+          // address arithmetic.  Stores: row j's floats j RS + 4 s4 .. + 3; lane 3's last two (past the RS = 14
+          // columns) land on row j + 1's first two, which lane 0 rewrites with row j + 1 right after (one wave's LDS
+          // stores are performed in order; the empty asm keeps the compiler's), the last row's in the padding.
+          const __amdgpu_buffer_rsrc_t rsrc =
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.img_b), (short)0, (int)0xffffffff, 0x00020000);
+          const unsigned vo = ((unsigned)(f * fs) + (unsigned)(((pos1 - P / 2 - 1) * W + (pos0 - P / 2 - 1)) * NOC) +
+                               4u * (unsigned)s4) * 4u;
+          float4_v t[P + 1];
+#pragma unroll
+          for (int j = 0; j <= P; ++j)
+            t[j] = __builtin_bit_cast(float4_v, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, j * W * NOC * 4, 0));
+          f2p *d = reinterpret_cast<f2p *>(win + 4 * s4);
+#pragma unroll
+          for (int j = 0; j <= P; ++j) {
+            d[j * (RS / 2)] = f2p{t[j].x, t[j].y};
+            d[j * (RS / 2) + 1] = f2p{t[j].z, t[j].w};
+            asm volatile("" ::: "memory");
+          }
+          done = true;
+        }
+      }
       // every load of the tile in flight at once: one round trip to L2 per reload (the 8-lane kernel's count)
       constexpr int NB = S::LPL;
 #pragma unroll
-      for (int j0 = 0; j0 < S::LPL; j0 += NB) {
+      for (int j0 = 0; j0 < (done ? 0 : S::LPL); j0 += NB) {
         float4_u t[NB];
         int lo[NB];
 #pragma unroll

@@ -104,6 +104,7 @@ struct ofdis_context {
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw)
   int opt_patch_absw = 1;      // patch kernels that can hand the aggregation its weights directly do (0: loss weights)
+  int opt_patch_buf = 1;       // gray p = 12 windows by buffer loads (32-bit offsets) where the image array allows
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
@@ -406,6 +407,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.x16 = c->opt_patch_x16;
     pa.absw = !P.fb && c->opt_patch_absw;  // usefbcon: the complementary grid's loss weights are read raw
     pa.aslots = (p->p_samp_s - 1) / steps + 1;
+    pa.buf32 = c->opt_patch_buf && (size_t)n * fsp * sizeof(float) + 4096 <= 0xffffffffu;
     pa.generic = c->opt_patch_generic;
     pa.g = g;
     if (times) {  // verbosity 2: pconst / pinit from construction-only launches (their output is overwritten)
@@ -1253,6 +1255,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 1},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
+      {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},
       {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},      {"sor_flow", &ofdis_context::opt_sor_flow, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
