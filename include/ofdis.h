@@ -212,6 +212,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        diagonals to each other through LDS progress counters instead of workgroup barriers, fed
  *                        by an LDS-DMA loader wave (0: the barrier-synchronised sweep-per-wave SOR; opt-in: measured
  *                        ~3x slower per launch);
+ *   "sor_dma" (0/1/2, default 0): levels of up to 128 rows run the exact-order SOR with its sweep-0 operands (the
+ *                        coefficient row, the old (du, dv)) streamed into LDS by an LDS-DMA loader wave ahead of the
+ *                        wavefront, one barrier per step (2: only for launches of at most 256 frames);
  *   "tv_flow" (0/1, default 0): levels of up to 64 rows run each TV inner iteration (smoothness, system and
  *                        the exact-order SOR) as one launch whose waves hand the diagonals to each other through
  *                        LDS (no coefficient round trip through HBM; measured slower than the system and SOR

@@ -131,6 +131,7 @@ struct TvArgs {
                                // intermediates in LDS) where tv_flow_ok() holds
   int *flow_err;               // device counter of k_tv_flow launches that hit their spin bound (0 = none)
   int sor_flow;                // exact-order SOR as the barrier-free k_tv_sorflow where tv_sorflow_ok() holds
+  int sor_dma;                 // exact-order SOR as k_tv_sordma (barriers, LDS-DMA loader) where tv_sordma_ok() holds
 };
 
 struct UpArgs {
@@ -170,6 +171,8 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s);
 bool tv_flow_ok(const TvArgs &a);  // ofdis_tvflow.hip
 void launch_tv_flow(const TvArgs &a, hipStream_t s);
 bool tv_sorflow_ok(const TvArgs &a);
+bool tv_sordma_ok(const TvArgs &a);
+void launch_tv_sordma(const TvArgs &a, hipStream_t s);
 void launch_tv_sorflow(const TvArgs &a, hipStream_t s);
 int *tv_flow_err_counter();        // device address of the current device's k_tv_flow abort counter
 int tv_flow_err_take();            // its value (synchronous read), reset to 0

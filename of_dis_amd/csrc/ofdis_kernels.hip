@@ -4676,6 +4676,10 @@ static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
 // global-memory wavefront for the point SOR of the OpenMP build and degenerate sizes.
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
+  if (tv_sordma_ok(a)) {  // latency regime: sweep waves fed by an LDS-DMA loader, barrier per step (ofdis_tvflow.hip)
+    launch_tv_sordma(a, s);
+    return;
+  }
   if (tv_sorflow_ok(a)) {  // barrier-free sweep waves fed by an LDS-DMA loader (ofdis_tvflow.hip)
     launch_tv_sorflow(a, s);
     return;

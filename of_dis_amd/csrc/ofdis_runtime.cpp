@@ -98,6 +98,7 @@ struct ofdis_context {
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
   int opt_sor_flow = 0;        // exact-order SOR of levels <= 128 rows as the barrier-free k_tv_sorflow (opt-in:
                                // measured ~3x slower per launch than k_tv_sor_lanes)
+  int opt_sor_dma = 0;         // levels <= 128 rows: k_tv_sordma (1 always, 2 when a launch has at most 256 frames)
   int opt_tv_flow = 0;         // one dataflow launch per TV inner iteration (k_tv_flow) where it fits (opt-in:
                                // measured slower than the two launches)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
@@ -529,6 +530,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.prepd = c->opt_prepd;
       tv.tv_flow = c->opt_tv_flow;
       tv.sor_flow = c->opt_sor_flow;
+      tv.sor_dma = c->opt_sor_dma == 2 ? n <= 256 : c->opt_sor_dma;
       tv.flow_err = tv_flow_err_counter();
       tv.smsys_deriv = tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
@@ -1257,6 +1259,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 1},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},
       {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},      {"sor_flow", &ofdis_context::opt_sor_flow, 0, 1},
+      {"sor_dma", &ofdis_context::opt_sor_dma, 0, 2},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {

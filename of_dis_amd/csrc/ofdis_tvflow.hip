@@ -799,6 +799,225 @@ bool sorflow_go(const TvArgs &a, hipStream_t s, bool run) {
   }
 }
 
+// ================================================================================== SOR, barriers + LDS-DMA
+// k_tv_sordma: the exact-order SOR call (solver.c:83-433 / :439-471) of one frame's level in the latency regime
+// (a launch of at most one frame per CU).  The sweep-per-wave schedule of k_tv_sor_lanes -- sweep s of row group g
+// is one wave, pixel (x, y) of sweep s at wavefront step x + y + 2 s, one workgroup barrier per step -- but sweep 0
+// never waits on a global load: a loader wave streams every diagonal's coefficient row (the system launch's
+// array-of-structs row) and old (du, dv) rows into LDS rings by LDS-DMA, kDmLA rows ahead, and waits for the rows
+// the next step needs (explicit vmcnt) before the barrier that publishes them.  The sweeps read everything from the
+// rings; same update expressions as k_tv_sor_lanes / k_tv_sorflow, same bits.
+constexpr int kDmLA = 6;   // rows the loader runs ahead of sweep 0
+constexpr int kDmRC = 14;  // coefficient ring slots: > kDmLA + 2 S + 1 (a slot is rewritten only after its last read)
+constexpr int kDmRR = 16;  // (du, dv) row ring slots (power of 2): > kDmLA + 2
+
+template <int S, int MODE, int G>
+struct SorDma {
+  static constexpr int CW = MODE == 0 ? 2 : 1;
+  static constexpr int NPL = MODE == 0 ? 2 : 1;
+  static constexpr int NR = 64 * G + 2;    // (u, v) ring entries per slot (row y at y + 1)
+  static constexpr int NRA = 64 * G + 8;   // (du, dv) ring entries per plane (row y at y + 4)
+  static constexpr int NCR = 64 * G * CW;  // coefficient ring float4 per slot (row y at y CW)
+  static constexpr int D = 4;              // (u, v) ring slots per sweep
+  static constexpr int NW = S * G + 1;
+  static constexpr size_t OFF_COEF = 0;
+  static constexpr size_t OFF_DU = OFF_COEF + sizeof(float4) * kDmRC * NCR;
+  static constexpr size_t OFF_UV = OFF_DU + sizeof(float) * kDmRR * NPL * NRA;
+  static constexpr size_t LDS = OFF_UV + sizeof(f2v) * S * D * NR;
+  static constexpr int NDMA_ROW = (NCR * 16 + 1023) / 1024 + NPL;  // DMA instructions per row
+  static_assert(kDmRC > kDmLA + 2 * S + 1 && kDmRR > kDmLA + 2, "ring slots");
+
+  const TvArgs a;
+  float4 *coef;
+  float *dur;
+  f2v *uv;
+  int w, h, E, lim;
+  unsigned f0;
+
+  __device__ SorDma(const TvArgs &a_, char *lds, int frame) : a(a_) {
+    coef = reinterpret_cast<float4 *>(lds + OFF_COEF);
+    dur = reinterpret_cast<float *>(lds + OFF_DU);
+    uv = reinterpret_cast<f2v *>(lds + OFF_UV);
+    w = a.w;
+    h = a.h;
+    E = a.w + a.h - 1;
+    lim = a.wrap ? a.w : 1 << 30;
+    f0 = (unsigned)((long)frame * a.sp);
+  }
+  __device__ __forceinline__ int prow(int d) const { return d >= lim ? d - lim : d; }
+  __device__ __forceinline__ const float *du_slot(int q) const { return dur + (q & (kDmRR - 1)) * NPL * NRA + 4; }
+
+  // diagonal q's coefficient row (16 h CW contiguous bytes) and old (du, dv) rows into their ring slots; rows past
+  // the last diagonal re-read the last one (never used).  Every DMA instruction issues (lane 0 always has work), so
+  // the loader's vmcnt waits count them exactly.
+  __device__ __forceinline__ void dma_row(int q, int lane) const {
+    const int qc = q < E ? q : E - 1;
+    const unsigned pr = (unsigned)(prow(qc) * h);
+    const char *csrc = reinterpret_cast<const char *>(a.coef) + (size_t)(f0 + pr) * CW * 16;
+    const unsigned cdst = lds_addr(coef + (q % kDmRC) * NCR);
+    const int cbytes = h * CW * 16;
+#pragma unroll
+    for (int k = 0; k < (NCR * 16 + 1023) / 1024; ++k) {
+      const int off = 1024 * k + 16 * lane;
+      dma16(reinterpret_cast<const float *>(csrc + (off < cbytes ? off : 0)), __builtin_amdgcn_readfirstlane(cdst + 1024 * k));
+    }
+    if (lane < 16 * G) {
+      const float *d = du_slot(q);
+      const unsigned lo = 4 * lane < h ? 4u * (unsigned)lane : 0u;
+      dma16(a.du + f0 + pr + lo, __builtin_amdgcn_readfirstlane(lds_addr(d)));
+      if (MODE == 0) dma16(a.dv + f0 + pr + lo, __builtin_amdgcn_readfirstlane(lds_addr(d + NRA)));
+    }
+  }
+
+  // T steps; at the barrier ending step t the rows <= t + 2 have landed (sweep 0 at step t + 1 reads rows t + 1
+  // and t + 2), rows t + 3 .. t + kDmLA + 1 may still be in flight
+  __device__ void run_l(int lane, int T) {
+    for (int q = 0; q <= kDmLA; ++q) dma_row(q, lane);
+    wait_vmcnt<(kDmLA - 1) * NDMA_ROW>();
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      dma_row(t + kDmLA + 1, lane);
+      wait_vmcnt<(kDmLA - 1) * NDMA_ROW>();
+      __syncthreads();
+    }
+    wait_vmcnt<0>();
+  }
+
+  template <int SI>
+  __device__ void run_sor(int g, int lane, int T) {
+    constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
+    const int y = 64 * g + lane;
+    const bool border = y == 0 || y >= h - 1, notop = y == 0;
+    const bool top_lds = lane == 0 && g > 0;
+    const float omega = a.omega;
+    f2v pp = f2v{0.0f, 0.0f};
+    float phr = 0.0f, pvv = 0.0f;
+    f2v *ring_s = uv + SI * D * NR;
+    const f2v *ring_p = uv + (SI > 0 ? SI - 1 : 0) * D * NR;
+    __syncthreads();  // the loader's prologue
+    for (int t = 0; t < T; ++t) {
+      const int d = t - 2 * SI;
+      if (d >= 0 && d < E) {
+        const int x = d - y;
+        const bool hasl = x > 0, hasr = x < w - 1;
+        const int dm = (d + D - 1) % D, cm = (d + kDmRC - 1) % kDmRC;
+        f2v o, rgt, bt, tpl = f2v{0.f, 0.f};
+        float tsvl = 0.f;
+        if (FIRST) {
+          const float *r0 = du_slot(d) + y, *r1 = du_slot(d + 1) + y;
+          o = f2v{r0[0], MODE == 0 ? r0[NRA] : 0.0f};
+          rgt = f2v{r1[0], MODE == 0 ? r1[NRA] : 0.0f};
+          bt = f2v{r1[1], MODE == 0 ? r1[NRA + 1] : 0.0f};
+        } else {
+          o = ring_p[(d % D) * NR + y + 1];
+          rgt = ring_p[((d + 1) % D) * NR + y + 1];
+          bt = ring_p[((d + 1) % D) * NR + y + 2];
+        }
+        const float4 *Cp = coef + (d % kDmRC) * NCR + y * CW;
+        const float4 c0 = Cp[0];
+        const float4 c1 = MODE == 0 ? Cp[1] : c0;
+        if (G > 1) {  // lane 0 of a lower row group: the row above is the group above's
+          tpl = ring_s[dm * NR + y];
+          tsvl = coef[cm * NCR + (y - 1) * CW + CW - 1].w;
+        }
+        f2v tp = f2v{dpp_from_prev_lane(pp.x), MODE == 0 ? dpp_from_prev_lane(pp.y) : 0.0f};
+        float tsv = dpp_from_prev_lane(pvv);
+        if (G > 1 && top_lds) {
+          tp = tpl;
+          tsv = tsvl;
+        }
+        f2v nw;
+        float vv;
+        if (MODE == 0) {
+          const float hr = c1.z;
+          vv = c1.w;
+          const f2v bb = f2v{c1.x, c1.y};
+          const f2v rrv = hasr ? rgt : f2v{0.0f, 0.0f};
+          const f2v X = hr * rrv, Yv = tsv * tp, Z = vv * bt;
+          const f2v l = X + (border ? bb : Yv);
+          const f2v rg = (border ? f2v{-0.0f, -0.0f} : bb) + (border ? (notop ? Z : Yv) : Z);
+          const f2v srr = l + rg;
+          const f2v Bv = hasl ? phr * pp + srr : srr;
+          const f2v m_1 = f2v{c0.x, c0.y} * Bv.x, m_2 = f2v{c0.z, c0.w} * Bv.y;
+          nw = o + omega * ((m_1 + m_2) - o);
+          phr = hr;
+        } else {
+          const float a11 = c0.x, b1 = c0.y, hr = c0.z;
+          vv = c0.w;
+          const bool has_top = !notop, has_bot = !(border && has_top);
+          const float tu = tp.x, ur = hasr ? rgt.x : 0.0f, hl = phr;
+          float su = 0.0f;
+          su = has_top ? su - tsv * tu : su;
+          su = hasl ? su - hl * pp.x : su;
+          su = has_bot ? su - vv * bt.x : su;
+          su = hasr ? su - hr * ur : su;
+          const float A = a11, Bq = b1 - su;
+          nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
+          phr = hr;
+        }
+        ring_s[(d % D) * NR + y + 1] = nw;
+        if (LAST && (unsigned)x < (unsigned)w && y < h) {
+          const unsigned oo = f0 + (unsigned)(prow(d) * h + y);
+          *reinterpret_cast<float *>(reinterpret_cast<char *>(a.du) + (size_t)oo * 4u) = nw.x;
+          if (MODE == 0) *reinterpret_cast<float *>(reinterpret_cast<char *>(a.dv) + (size_t)oo * 4u) = nw.y;
+        }
+        pp = nw;
+        pvv = vv;
+      }
+      __syncthreads();
+    }
+  }
+};
+
+template <int S, int MODE, int G>
+__global__ __launch_bounds__((64 * SorDma<S, MODE, G>::NW)) void k_tv_sordma(TvArgs a) {
+  using F = SorDma<S, MODE, G>;
+  extern __shared__ __attribute__((aligned(16))) char sd_lds[];
+  for (int i = threadIdx.x; i < (int)(F::LDS / 16); i += blockDim.x)
+    reinterpret_cast<float4 *>(sd_lds)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  F fl(a, sd_lds, blockIdx.x);
+  const int T = fl.E + 2 * (S - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid < S * G) {
+    const int s = wid / G, g = wid - s * G;
+    if (s == 0) fl.template run_sor<0>(g, lane, T);
+    else if (s == 1) fl.template run_sor<(S > 1 ? 1 : 0)>(g, lane, T);
+    else if (s == 2) fl.template run_sor<(S > 2 ? 2 : 0)>(g, lane, T);
+    else fl.template run_sor<(S > 3 ? 3 : 0)>(g, lane, T);
+  } else {
+    fl.run_l(lane, T);
+  }
+}
+
+template <int S, int MODE, int G>
+void launch_sordma(const TvArgs &a, hipStream_t s) {
+  using F = SorDma<S, MODE, G>;
+  static_assert(F::LDS <= 160 * 1024, "LDS");
+  static_assert(kDmLA * F::NDMA_ROW < 64, "loader rows in flight");
+  k_tv_sordma<S, MODE, G><<<a.n, 64 * F::NW, F::LDS, s>>>(a);
+}
+template <int S, int MODE>
+bool sordma_s(const TvArgs &a, hipStream_t s, bool run) {
+  if (a.h <= 64) {
+    if (run) launch_sordma<S, MODE, 1>(a, s);
+    return true;
+  }
+  if (a.h <= 128) {
+    if (run) launch_sordma<S, MODE, 2>(a, s);
+    return true;
+  }
+  return false;
+}
+bool sordma_go(const TvArgs &a, hipStream_t s, bool run) {
+  const int mode = a.nop == 2 ? 0 : 2;
+  switch (a.solverit) {
+    case 2: return mode == 0 ? sordma_s<2, 0>(a, s, run) : sordma_s<2, 2>(a, s, run);
+    case 3: return mode == 0 ? sordma_s<3, 0>(a, s, run) : sordma_s<3, 2>(a, s, run);
+    default: return false;
+  }
+}
+
 }  // namespace
 
 // The dataflow iteration runs where its rings fit: up to 64 rows (lane = row), 2 or 3 sweeps, the
@@ -811,6 +1030,14 @@ bool tv_flow_ok(const TvArgs &a) {
   return flow_go(a, nullptr, false);
 }
 void launch_tv_flow(const TvArgs &a, hipStream_t s) { flow_go(a, s, true); }
+
+// The barrier SOR fed by LDS-DMA: exact order, 2 or 3 sweeps, 2 .. 128 rows (option sor_dma).
+bool tv_sordma_ok(const TvArgs &a) {
+  if (!a.sor_dma || a.sor_redblack || a.sor_point || a.sor_generic || a.sor_variant == 1) return false;
+  if (a.w < 2 || a.h < 2) return false;
+  return sordma_go(a, nullptr, false);
+}
+void launch_tv_sordma(const TvArgs &a, hipStream_t s) { sordma_go(a, s, true); }
 
 // The barrier-free SOR: exact order, 2 or 3 sweeps, 2 .. 128 rows (option sor_flow); the system launch runs first.
 bool tv_sorflow_ok(const TvArgs &a) {

@@ -131,6 +131,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
     ("tv_flow", 1, 0),         # levels <= 64 rows: one dataflow launch per inner iteration (k_tv_flow)
     ("sor_flow", 1, 0),        # levels <= 128 rows: the barrier-free k_tv_sorflow instead of the barrier SOR
+    ("sor_dma", 1, 0),         # levels <= 128 rows: the barrier SOR fed by an LDS-DMA loader (k_tv_sordma)
 ]
 
 
