@@ -238,7 +238,11 @@ def cpu_baseline(O, q, pairs, W, H, seconds, binary, cfg_name):
     cores = host_cores()
     done_all, t_all = parallel(cores) if cores > 1 else (0, 0.0)
     node = os.cpu_count() or 1
-    done_node, t_node = parallel(node) if node > cores else (0, 0.0)
+    quota = cpu_quota()
+    # the node leg only where this process may use more CPUs than the all-cores leg: under a cgroup quota of <= cores
+    # CPUs, nproc workers time-share the same CPUs (slower than the cores leg, not a node figure -- VERDICT r03)
+    node_runs = node > cores and (quota is None or quota > cores)
+    done_node, t_node = parallel(node) if node_runs else (0, 0.0)
     fair = None
     ff = os.path.join(ROOT, "profiles", "cpu_fairness.json")
     if os.path.exists(ff):
@@ -271,6 +275,10 @@ def cpu_baseline(O, q, pairs, W, H, seconds, binary, cfg_name):
         out["value_all_cores"] = round(W * H * done_all / t_all / 1e6, 3)
         out["frames_per_sec_all_cores"] = round(done_all / t_all, 3)
         out["sample_all_cores"] = f"{done_all} pairs over {cores} worker threads, {t_all:.1f} s"
+    if node > cores and not node_runs:
+        out["value_node"] = None
+        out["node_leg"] = (f"skipped: nproc {node} CPUs, but the cgroup quota caps this process at {quota} CPUs "
+                           f"(the {cores}-worker leg is this host share's figure)")
     if done_node:
         out["value_node"] = round(W * H * done_node / t_node / 1e6, 3)
         out["frames_per_sec_node"] = round(done_node / t_node, 3)
