@@ -170,9 +170,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        thread's derivative-image loads before the staging, not after two barriers;
  *   "smsys_small" (0/1, default 1): a fused launch that cannot fill the chip (fewer than 4096 row blocks:
  *                        a few pairs per call) takes ~1 pixel per thread (>= 4 rows per block) instead of 4;
- *   "smsys_deriv" (0/1, default 1): where the fused launch and "prepd" run (levels up to 256 rows, intensity
- *                        images), the system kernel filters Ixx, Ixy, Iyy, Ixz, Iyz from staged Ix, Iy, Iz and
- *                        the prep launch does not write those five planes;
+ *   "smsys_deriv" (0/1, default 1): where "prepd" and the fused launch (levels up to 256 rows) or the register
+ *                        march (taller levels) run (intensity images), the system kernel filters Ixx, Ixy, Iyy,
+ *                        Ixz, Iyz from Ix, Iy, Iz and the prep launch does not write those five planes;
  *   "smsys_march" (0/1, default 1): levels taller than 256 rows run smoothness + system as a register march
  *                        (one wave per 60 columns x 64 rows, no LDS; takes precedence over smsys2d);
  *   "prepd" (0/1, default 1): for intensity images, image warp, temporal images and the derivative filters

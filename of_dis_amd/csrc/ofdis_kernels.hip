@@ -2175,6 +2175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         q[u & 1][1] = lds_read2<o + RS, o + RS + NOC>(b);  // B, A
       }
     };
+    const f2p w32 = f2p{w3, w2}, w10 = f2p{w1, w0};
     issue(std::integral_constant<int, 0>{});
     static_for<NPP + NS>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
@@ -2194,7 +2195,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       } else {
         reg_fence(t[0]);
         reg_fence(t[1]);
-        pds[u - NPP] = ((w0 * t[1].y + w1 * t[1].x) + w2 * t[0].y) + w3 * t[0].x;
+        // the tap pairs (D, C), (B, A) as they come: two packed products, then the sum in the reference's order
+        const f2p dc = t[0] * w32, ba = t[1] * w10;  // (w3 D, w2 C), (w1 B, w0 A)
+        pds[u - NPP] = ((ba.y + ba.x) + dc.y) + dc.x;
       }
     });
     auto pdv = [&](int m) -> float {  // compile-time m: the sample of value m
@@ -3032,8 +3035,24 @@ __device__ __forceinline__ float wave_from_next(float v) {  // lane i <- lane i 
 __host__ __device__ __forceinline__ int march_segments(int rows) { return (rows + kMR - 1) / kMR; }
 __host__ __device__ __forceinline__ int march_strips(int h) { return (h + kMC - 1) / kMC; }
 
-template <int NOP, int NOC>
+// get_derivatives' 5-tap filter from the taps at offsets -2 .. 2 along one axis, replicate border: a tap past the
+// border takes the border pixel's value, one of the taps held (pos = the pixel's coordinate on the axis, n = the
+// level's extent); k_tv_smsys<.., DF>'s expression (c5h / c5v)
+__device__ __forceinline__ float conv5_clamp(const float (&t)[5], int pos, int n) {
+  const float m1 = pos >= 1 ? t[1] : t[2];
+  const float m2 = pos >= 2 ? t[0] : m1;
+  const float p1 = pos <= n - 2 ? t[3] : t[2];
+  const float p2 = pos <= n - 3 ? t[4] : p1;
+  return kK5[0] * m2 + ((kK5[1] * m1 + kK5[2] * t[2]) + (kK5[3] * p1 + kK5[4] * p2));
+}
+
+// DF (intensity images, option smsys_deriv, round 4): the march keeps rows r - 2 .. r + 2 of Ix, Iy, Iz in registers
+// and filters the five second derivatives of row r itself: a horizontal tap x + k is row r + k of the same lane, a
+// vertical tap y + k row r + k of lane + k (DPP shifts); k_tv_prepd then writes 3 of the 8 derivative planes, and a
+// step reads 5 planes instead of 10.
+template <int NOP, int NOC, bool DF = false>
 __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
+  static_assert(!DF || NOC == 1, "filtered derivatives: intensity images");
   const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
   const int nstrip = march_strips(h), nseg = march_segments(rows);
   const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (frame, segment, strip), strip fastest
@@ -3095,6 +3114,27 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
     const float vv5[5] = {vv1, l ? vv0 : vv1, rr ? vv2 : vv1, u ? vvp : vv1, d ? vvn : vv1};
     return smooth_from_uu<NOP>(a, uu5, vv5);
   };
+  struct Drow {
+    float ix, iy, iz;
+  };
+  auto load_d = [&](int r) {  // DF: Ix, Iy, Iz of row r (0 outside the plane / the level's columns)
+    Drow q{0.f, 0.f, 0.f};
+    const int pr = prow(r);
+    if (pr >= 0 && ycol) {
+      const unsigned o = f0 + (unsigned)(pr * h + y);
+      q.ix = ldu(a.Ix, o);
+      q.iy = ldu(a.Iy, o);
+      q.iz = ldu(a.Iz, o);
+    }
+    return q;
+  };
+  Drow D0{}, D1{}, D2{}, D3{}, D4{};  // DF: rows r - 2 .. r + 2
+  if constexpr (DF) {
+    D0 = load_d(R0 - 2);
+    D1 = load_d(R0 - 1);
+    D2 = load_d(R0);
+    D3 = load_d(R0 + 1);
+  }
   Row Um = load_row(R0 - 1), U0 = load_row(R0), U1 = load_row(R0 + 1);
   float Sm = smooth_row(R0 - 1, load_row(R0 - 2), Um, U0);
   float S0 = smooth_row(R0, Um, U0, U1);
@@ -3104,15 +3144,19 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
     const bool has = pix(r, x);
     float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
     const int pr = prow(r);
-    const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)(pr < 0 ? 0 : pr) * h + (ycol ? y : 0));
+    if constexpr (DF) {
+      D4 = load_d(r + 2);
+    } else {
+      const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)(pr < 0 ? 0 : pr) * h + (ycol ? y : 0));
 #pragma unroll
-    for (int ch = 0; ch < NOC; ++ch) {
-      const unsigned o = qd + (unsigned)(ch * a.sp);
-      if (has) {
-        lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
-        lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
-      } else {
-        lIx[ch] = lIy[ch] = lIz[ch] = lIxx[ch] = lIxy[ch] = lIyy[ch] = lIxz[ch] = lIyz[ch] = 0.0f;
+      for (int ch = 0; ch < NOC; ++ch) {
+        const unsigned o = qd + (unsigned)(ch * a.sp);
+        if (has) {
+          lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
+          lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
+        } else {
+          lIx[ch] = lIy[ch] = lIz[ch] = lIxx[ch] = lIxy[ch] = lIyy[ch] = lIxz[ch] = lIyz[ch] = 0.0f;
+        }
       }
     }
     const Row U2 = load_row(r + 2);
@@ -3124,6 +3168,34 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
     if (NOP == 2) {
       Yp = wave_from_prev(Um.wy);
       Yn = wave_from_next(U1.wy);
+    }
+    if constexpr (DF) {
+      // vertical taps (x, y + k): row r + k, lane + k (every lane shifts: the DPP moves are wave-wide)
+      auto vt = [&](float m2, float m1, float c, float p1, float p2, float (&t)[5]) {
+        t[0] = wave_from_prev(wave_from_prev(m2));
+        t[1] = wave_from_prev(m1);
+        t[2] = c;
+        t[3] = wave_from_next(p1);
+        t[4] = wave_from_next(wave_from_next(p2));
+      };
+      float vx[5], vy[5], vz[5];
+      vt(D0.ix, D1.ix, D2.ix, D3.ix, D4.ix, vx);
+      vt(D0.iy, D1.iy, D2.iy, D3.iy, D4.iy, vy);
+      vt(D0.iz, D1.iz, D2.iz, D3.iz, D4.iz, vz);
+      const float hx[5] = {D0.ix, D1.ix, D2.ix, D3.ix, D4.ix}, hz[5] = {D0.iz, D1.iz, D2.iz, D3.iz, D4.iz};
+      const int xc = has ? x : 0, yc = ycol ? y : 0;  // (lanes without a pixel: any valid taps)
+      lIx[0] = D2.ix;
+      lIy[0] = D2.iy;
+      lIz[0] = D2.iz;
+      lIxx[0] = conv5_clamp(hx, xc, w);
+      lIxy[0] = conv5_clamp(vx, yc, h);
+      lIyy[0] = conv5_clamp(vy, yc, h);
+      lIxz[0] = conv5_clamp(hz, xc, w);
+      lIyz[0] = conv5_clamp(vz, yc, h);
+      D0 = D1;
+      D1 = D2;
+      D2 = D3;
+      D3 = D4;
     }
     if (has && out_lane) {
       const float S5[5] = {S0, Sm, S1, Sp, Sn};
@@ -4549,14 +4621,16 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
 bool tv_smsys_ok(const TvArgs &a) {
   return a.smsys && ((smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) || a.smsys2d || a.smsys_march);
 }
-// The derivative filters move into the system kernel only where the level runs the row-block k_tv_smsys and
-// k_tv_prepd (intensity images): the march, the 2-D tiles and the two-launch form read all eight planes.
+// The derivative filters move into the system kernel where the level runs k_tv_prepd (intensity images) and the
+// row-block k_tv_smsys or the march k_tv_smsys_m (round 4); the 2-D tiles and the two-launch form read all eight planes.
 // Not where the 40 KB LDS cap of the DF form leaves fewer than 3 rows per block (levels of ~180-256 rows): a
 // block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
   if (tv_flow_ok(a)) return a.noc == 1;  // the dataflow iteration filters the second derivatives itself (gray)
-  if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys && smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024))
-    return false;
+  if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys)) return false;
+  if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) return a.smsys_march != 0;  // the march filters them too
+  {
+  }
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
   while (rb > 1 && smsys_lds_df(a.h, rb, true) > kSmsysDfCap) --rb;
   return rb >= 3;
@@ -4565,7 +4639,10 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {
     const long waves = (long)a.n * march_segments(smsys_rows(a.w, a.h, a.wrap)) * march_strips(a.h);
     const unsigned grid = ceil_div(waves, 4);
-    if (a.nop == 2) {
+    if (a.noc == 1 && a.smsys_deriv) {  // tv_deriv_fused(): k_tv_prepd wrote Ix, Iy, Iz only
+      if (a.nop == 2) k_tv_smsys_m<2, 1, true><<<grid, 256, 0, s>>>(a);
+      else k_tv_smsys_m<1, 1, true><<<grid, 256, 0, s>>>(a);
+    } else if (a.nop == 2) {
       if (a.noc == 1) k_tv_smsys_m<2, 1><<<grid, 256, 0, s>>>(a);
       else k_tv_smsys_m<2, 3><<<grid, 256, 0, s>>>(a);
     } else {
