@@ -1952,7 +1952,12 @@ struct XShape {
   // value m -> m + KP of a lane advances its taps by KROWS whole patch rows
   static constexpr int KP = (16 / gcd(16, ROWV) * ROWV) / 16;
   static constexpr int KROWS = 16 * KP / ROWV;
+  // value groups of KP: pairs of groups (2g, 2g + 1) run packed, an odd last group alone
+  static constexpr int NPG = M / KP / 2, NPP = NPG * KP, NS = M - 2 * NPP;
   static_assert(NV % 16 == 0, "sixteen-lane form: p * p * noc a multiple of 16");
+  // LDS floats of a workgroup: sixteen windows, then the gradients of the odd group's values (NOP per value and
+  // lane; in LDS they free registers the compiler otherwise spills to scratch and reloads every iteration)
+  static constexpr int lds_floats(int nop) { return 16 * WIN + NS * 256 * nop; }
 };
 
 // Eigen's chain of one packet slot, folded on the owner lanes in block order (see above).
@@ -1984,8 +1989,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   const uint3 xb = xcd_block();
   using S = XShape<P, NOC>;
   constexpr int M = S::M, RS = S::RS, KP = S::KP;
-  // value groups of KP: pairs of groups (2g, 2g + 1) run packed, an odd last group alone
-  constexpr int NPG = M / KP / 2, NPP = NPG * KP, NS = M - 2 * NPP;
+  constexpr int NPG = S::NPG, NPP = S::NPP, NS = S::NS;
   static_assert(M % KP == 0 && NS <= KP, "sixteen-lane form: whole value groups");
   extern __shared__ __attribute__((aligned(16))) float win_all[];
   const LevelGeom &g = a.g;
@@ -2085,7 +2089,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   // template and gradients as value pairs (m, m + KP) of the pair groups, and the values of an odd last group
   f2p tmp2[NPP > 0 ? NPP : 1], gx2[NPP > 0 ? NPP : 1], gy2[NOP == 2 && NPP > 0 ? NPP : 1];
-  float tmps[NS > 0 ? NS : 1], gxs[NS > 0 ? NS : 1], gys[NOP == 2 && NS > 0 ? NS : 1];
+  float tmps[NS > 0 ? NS : 1];
+  // the odd group's gradients: LDS float NOP (i 256 + tid) (+1), written and read by the lane itself only
+  float *gsl = win_all + 16 * S::WIN + NOP * threadIdx.x;
 #pragma unroll
   for (int j = 0; j < NPP; ++j) {
     const int m = (j / KP) * 2 * KP + j % KP;
@@ -2096,8 +2102,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     tmps[i] = tmp[2 * NPP + i];
-    gxs[i] = gx[2 * NPP + i];
-    if constexpr (NOP == 2) gys[i] = gy[2 * NPP + i];
+    if constexpr (NOP == 2)
+      *reinterpret_cast<f2p *>(gsl + 2 * 256 * i) = f2p{gx[2 * NPP + i], gy[2 * NPP + i]};
+    else
+      gsl[256 * i] = gx[2 * NPP + i];
   }
   const float *Bimg = a.img_b + f * fs;
   // ---- OptimizeStart (patch.cpp:117-154)
@@ -2229,10 +2237,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if constexpr (NOP == 2) return gy2[j];
       return f2p{0.0f, 0.0f};
     };
-    auto gys_ = [&](int i) -> float {
-      if constexpr (NOP == 2) return gys[i];
-      return 0.0f;
-    };
     XAcc ab, ex, ey;
     // pair groups: d of both halves packed; the .x halves (values m) go into the chains at once, the .y halves'
     // d (values m + KP) are kept until their turn, after the group's KP .x values
@@ -2276,7 +2280,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     });
     static_for<NS>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gxs[i], gys_(i));
+      if constexpr (NOP == 2) {
+        const f2p gr = *reinterpret_cast<const f2p *>(gsl + 2 * 256 * i);
+        value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gr.x, gr.y);
+      } else {
+        value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gsl[256 * i], 0.0f);
+      }
     });
     if (STORE == 0) {
       flush(M - 1);
@@ -4522,7 +4531,7 @@ static void patchq(const PatchArgs &a, hipStream_t s) {
 template <int P, int NOC, int MINW>
 static void patchx(const PatchArgs &a, hipStream_t s) {
   const long patches = (long)a.n * a.g.npatch;
-  const size_t lds = sizeof(float) * 16 * XShape<P, NOC>::WIN;
+  const size_t lds = sizeof(float) * XShape<P, NOC>::lds_floats(a.nop == 2 ? 2 : 1);
   const dim3 grid(ceil_div(patches, 16));
   switch (a.costfct * 2 + (a.nop == 2 ? 1 : 0)) {
     case 0: k_patchx<1, P, NOC, MINW, 0><<<grid, 256, lds, s>>>(a); return;
