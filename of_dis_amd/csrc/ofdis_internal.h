@@ -115,7 +115,8 @@ struct TvArgs {
   int sor_generic;             // force the generic global-memory SOR wavefront (A/B testing)
   int sor_variant;             // 0 auto (sweep-per-wave when it fits), 1 register pipeline (A/B testing)
   int sor_point;               // OpenMP build: point SOR on the raw system (solver.c:34-78) for every size
-  int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3)
+  int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3);
+                               // 2: the ring sized to the level's row groups
   int sor_rows2;               // lean SOR with two rows per lane for levels of 321..640 rows (else the pipeline)
   int smsys;                   // smoothness + system in one launch (k_tv_smsys)
   int prepd;                   // prep + derivatives in one launch (k_tv_prepd, intensity images; 0: three launches)

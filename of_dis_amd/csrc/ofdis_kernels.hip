@@ -4169,10 +4169,14 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
   }
 }
 
-template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1>
+// CG > 0: the coefficient ring holds exactly the CG row groups of the level (+ 2 halos) instead of the most a
+// workgroup of MAXT threads can hold -- less LDS per frame, more frames per CU.
+template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
-  sor_lanes_frame<S, MODE, NB, CRING ? sor_crn(S, MAXT, R) : 0, R>(a, blockIdx.x, ring_uv);
+  constexpr int crn = !CRING ? 0 : CG > 0 ? 64 * R * CG + 2 : sor_crn(S, MAXT, R);
+  static_assert(CG == 0 || CG * 64 * S <= MAXT, "row groups of the workgroup");
+  sor_lanes_frame<S, MODE, NB, crn, R>(a, blockIdx.x, ring_uv);
 }
 
 template <int TH>
@@ -4740,6 +4744,24 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
   const bool cring = crn > 0 && a.sor_cring && sor_lanes_lds(S, a.h, crn, cw, R) <= kSorLds;
   const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, cw, R);
   const int th = 64 * G * S;
+  if constexpr (S == 3 && R == 1) {
+    if (cring && a.sor_cring == 2) {  // the ring sized to the level's G row groups
+      const size_t ldsg = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R);
+      auto go = [&](auto gc) {
+        constexpr int CG = decltype(gc)::value;
+        if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+        else k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+      };
+      if constexpr (MAXT == 512) {
+        if (G == 1) return go(std::integral_constant<int, 1>{});
+        if (G == 2) return go(std::integral_constant<int, 2>{});
+      } else {
+        if (G == 3) return go(std::integral_constant<int, 3>{});
+        if (G == 4) return go(std::integral_constant<int, 4>{});
+        if (G == 5) return go(std::integral_constant<int, 5>{});
+      }
+    }
+  }
   if (cring) {
     if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true, R><<<a.n, th, lds, s>>>(a);
     else k_tv_sor_lanes<S, 2, 3, MAXT, true, R><<<a.n, th, lds, s>>>(a);
