@@ -4642,8 +4642,6 @@ bool tv_deriv_fused(const TvArgs &a) {
   if (tv_flow_ok(a)) return a.noc == 1;  // the dataflow iteration filters the second derivatives itself (gray)
   if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys)) return false;
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) return a.smsys_march != 0;  // the march filters them too
-  {
-  }
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
   while (rb > 1 && smsys_lds_df(a.h, rb, true) > kSmsysDfCap) --rb;
   return rb >= 3;
