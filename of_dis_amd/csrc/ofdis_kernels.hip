@@ -3858,7 +3858,7 @@ __device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
 // pixel each per step -- the rows of one step are independent (their top neighbours ran at step t-1 and are in
 // the ring), so R = 2 runs levels of up to 640 rows with S <= 3 in 16 waves (E's 544-row level) where R = 1
 // would need 27.  Every per-row ring / coefficient-ring offset is a compile-time multiple of 64 entries.
-template <int S, int MODE, int SI, int NB, int CRN, int R = 1>
+template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool CZ = false>
 struct SorLane {
   static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
   static_assert(CRN == 0 || S <= 3, "coefficient ring depth 6 needs S <= 3");
@@ -3894,7 +3894,12 @@ struct SorLane {
   f2v *ring_s;        // [NR][3] this sweep, lane base = entry y + 1 (entry 0 = row -1 stays zero)
   const f2v *ring_p;  // [NR][3] previous sweep
   float *sv_s;        // [NR][3] this sweep's sv (row y's sv at entry y + 1) (CRN = 0)
-  float4 *cr;         // [6][CW][CRN] coefficient ring, lane base = entry y + 1 (CRN > 0)
+  // coefficient ring (CRN > 0), lane base = entry y + 1, slot = diagonal mod 6: [6][CW][CRN] float4.  CZ (MODE 0,
+  // throughput launches): 7 of the pixel's 8 coefficient floats (c0 holds i12 twice) -- cr [6][CRN] (i11, i12, i22,
+  // hr), cr2 [6][CRN] (b1, b2), crv [6][CRN] sv: 28 instead of 32 bytes per entry, one more LDS read per step
+  float4 *cr;
+  f2v *cr2;
+  float *crv;
   int w, h, y, s, lim, rmax, hplane;
   bool border[R], notop[R];
   float omega;
@@ -3965,8 +3970,19 @@ struct SorLane {
         if (FIRST) {
           c0 = B.c0[r];
           c1 = MODE == 0 ? B.c1[r] : B.c0[r];
-          cr[cs * CW * CRN + 64 * r] = c0;
-          if (MODE == 0) cr[(cs * CW + 1) * CRN + 64 * r] = c1;
+          if constexpr (MODE == 0 && CZ) {
+            cr[cs * CRN + 64 * r] = make_float4(c0.x, c0.y, c0.w, c1.z);
+            cr2[cs * CRN + 64 * r] = f2v{c1.x, c1.y};
+            crv[cs * CRN + 64 * r] = c1.w;
+          } else {
+            cr[cs * CW * CRN + 64 * r] = c0;
+            if (MODE == 0) cr[(cs * CW + 1) * CRN + 64 * r] = c1;
+          }
+        } else if constexpr (MODE == 0 && CZ) {
+          const float4 q = cr[cs * CRN + 64 * r];
+          const f2v bq = cr2[cs * CRN + 64 * r];
+          c0 = make_float4(q.x, q.y, q.y, q.z);
+          c1 = make_float4(bq.x, bq.y, q.w, crv[cs * CRN + 64 * r]);
         } else {
           c0 = cr[cs * CW * CRN + 64 * r];
           c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN + 64 * r] : c0;
@@ -3983,11 +3999,11 @@ struct SorLane {
         tsv = dpp_from_prev_lane(pvv[r]);
         if (top_lds) {
           tp = ring_s[r * RO + m1 - 3];
-          tsv = CRN > 0 ? cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w : sv_s[r * RO + m1 - 3];
+          tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + 64 * r] : cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w) : sv_s[r * RO + m1 - 3];
         }
       } else {
         tp = ring_s[r * RO + m1 - 3];
-        tsv = CRN > 0 ? cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w : sv_s[r * RO + m1 - 3];
+        tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + 64 * r] : cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w) : sv_s[r * RO + m1 - 3];
       }
       f2v nw;
       float vv;
@@ -4084,6 +4100,7 @@ struct SorLane {
 };
 
 constexpr size_t kSorLds = 160 * 1024;  // LDS per workgroup (gfx950: 160 KB per CU)
+constexpr long kCUs = 256;               // MI355X compute units
 // Entries per slot of the coefficient ring: the most rows a workgroup of MAXT threads holds, + 2 halos
 // (a compile-time constant, so every ring offset is an immediate); 0 = no coefficient ring (S > 3).
 __host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
@@ -4091,16 +4108,19 @@ __host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
 }
 
 // LDS of the lean SOR: S (u, v) rings of NR = 64 R G + 2 entries x 3 slots of float2, then S sv rings
-// (CRN = 0) or the [6][CW][CRN] coefficient ring (16-byte aligned).
-__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1) {
+// (CRN = 0) or the coefficient ring (16-byte aligned): 6 slots x CRN entries of 28 (OF, cw = 2) / 16 (DE) bytes.
+__host__ __device__ __forceinline__ size_t sor_cring_bytes(int crn, int cw, bool cz = false) {
+  return (size_t)6 * crn * (cw == 2 ? (cz ? 28 : 32) : 16);
+}
+__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1, bool cz = false) {
   const size_t nr = (size_t)((h + 64 * R - 1) / (64 * R)) * 64 * R + 2;
   const size_t uv = sizeof(float) * 2 * 3 * (size_t)S * nr;
   if (crn == 0) return uv + sizeof(float) * 3 * (size_t)S * nr;
-  return (uv + 15) / 16 * 16 + sizeof(float4) * 6 * cw * (size_t)crn;
+  return (uv + 15) / 16 * 16 + sor_cring_bytes(crn, cw, cz);
 }
 
 // One frame's SOR call, lean form: 64 * G * S threads, R rows per lane.
-template <int S, int MODE, int NB, int CRN, int R>
+template <int S, int MODE, int NB, int CRN, int R, bool CZ = false>
 __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
   constexpr int CW = MODE == 0 ? 2 : 1;
   const int G = (a.h + 64 * R - 1) / (64 * R);
@@ -4108,13 +4128,18 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = wid / S, s = wid - g * S;
   float *svr = reinterpret_cast<float *>(ring + S * 3 * NR);
-  float4 *crr = reinterpret_cast<float4 *>(reinterpret_cast<char *>(ring) + (sizeof(f2v) * S * 3 * NR + 15) / 16 * 16);
+  char *crb = reinterpret_cast<char *>(ring) + (sizeof(f2v) * S * 3 * NR + 15) / 16 * 16;
+  float4 *crr = reinterpret_cast<float4 *>(crb);                // [6][CRN] float4
+  f2v *cr2r = reinterpret_cast<f2v *>(crb + 16 * 6 * CRN);      // MODE 0: [6][CRN] float2
+  float *crvr = reinterpret_cast<float *>(crb + 24 * 6 * CRN);  // MODE 0: [6][CRN] float
   for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) {
     ring[i] = f2v{0.f, 0.f};
     if (CRN == 0) svr[i] = 0.0f;
   }
-  if (CRN > 0)
-    for (int i = threadIdx.x; i < 6 * CW * CRN; i += blockDim.x) crr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (CRN > 0) {
+    float *z = reinterpret_cast<float *>(crb);
+    for (int i = threadIdx.x; i < (int)(sor_cring_bytes(CRN, CW, CZ) / 4); i += blockDim.x) z[i] = 0.0f;
+  }
   __syncthreads();
 #ifdef OFDIS_SOR_PROBE
   __shared__ unsigned probe_slot;
@@ -4136,6 +4161,8 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.ring_p = ring + ((s > 0 ? s - 1 : 0) * NR + y + 1) * 3;
     st.sv_s = svr + (s * NR + y + 1) * 3;
     st.cr = crr + y + 1;
+    st.cr2 = cr2r + y + 1;
+    st.crv = crvr + y + 1;
     st.w = a.w; st.h = a.h; st.y = y; st.s = s;  // s == SI
     st.lim = a.wrap ? a.w : 1 << 30;
     st.rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
@@ -4155,28 +4182,28 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.run(T, y0, ymax);
   };
   if (s == 0) {
-    SorLane<S, MODE, 0, NB, CRN, R> st;
+    SorLane<S, MODE, 0, NB, CRN, R, CZ> st;
     setup(st);
   } else if (s == 1) {
-    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R> st;
+    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, CZ> st;
     setup(st);
   } else if (s == 2) {
-    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R> st;
+    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, CZ> st;
     setup(st);
   } else {
-    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R> st;
+    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, CZ> st;
     setup(st);
   }
 }
 
 // CG > 0: the coefficient ring holds exactly the CG row groups of the level (+ 2 halos) instead of the most a
 // workgroup of MAXT threads can hold -- less LDS per frame, more frames per CU.
-template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0>
+template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool CZ = false>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
   constexpr int crn = !CRING ? 0 : CG > 0 ? 64 * R * CG + 2 : sor_crn(S, MAXT, R);
   static_assert(CG == 0 || CG * 64 * S <= MAXT, "row groups of the workgroup");
-  sor_lanes_frame<S, MODE, NB, crn, R>(a, blockIdx.x, ring_uv);
+  sor_lanes_frame<S, MODE, NB, crn, R, CZ>(a, blockIdx.x, ring_uv);
 }
 
 template <int TH>
@@ -4743,12 +4770,21 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
   const size_t lds = sor_lanes_lds(S, a.h, cring ? crn : 0, cw, R);
   const int th = 64 * G * S;
   if constexpr (S == 3 && R == 1) {
-    if (cring && a.sor_cring == 2) {  // the ring sized to the level's G row groups
-      const size_t ldsg = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R);
+    if (cring && a.sor_cring >= 2) {  // the ring sized to the level's G row groups
+      // OF launches with more frames than the chip holds at once: the 28-byte ring entries where they let more
+      // frames share a CU (throughput); else the 32-byte entries (one LDS read less on the step's critical path)
+      const size_t ld32 = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R), ld28 = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R, true);
+      const bool cz = a.nop == 2 && (a.sor_cring == 3 || (kSorLds / ld28 > kSorLds / ld32 &&
+                                                          (long)a.n > (long)(kSorLds / ld32) * kCUs));
+      const size_t ldsg = cz ? ld28 : ld32;
       auto go = [&](auto gc) {
         constexpr int CG = decltype(gc)::value;
-        if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
-        else k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+        if (a.nop == 2) {
+          if (cz) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true><<<a.n, th, ldsg, s>>>(a);
+          else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+        } else {
+          k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+        }
       };
       if constexpr (MAXT == 512) {
         if (G == 1) return go(std::integral_constant<int, 1>{});
