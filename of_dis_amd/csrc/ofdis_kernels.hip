@@ -4285,7 +4285,9 @@ __device__ __forceinline__ float up_px(const float *P, long r0, long r1, const X
 // float value.  Horizontal taps are per source row (HResizeLinear), the vertical blend per output row
 // (VResizeLinear), exactly as in OpenCV's generic float path.
 constexpr int kUpCols = 1024;
-constexpr int kUpRows = 8;
+// 4 output rows per block (round 4, profiles/r04/s17): 13 KB of staged source rows, more blocks per CU; B's
+// upsample 6.27-6.29 -> 6.00-6.01 ms per 2048-pair launch against 8 rows (2 rows: 6.73, 16 rows: 6.55)
+constexpr int kUpRows = 4;
 constexpr int kUpSrcRows = kUpRows / 2 + 3;  // source rows a block can touch (2^l >= 2)
 typedef float v4f __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
