@@ -190,8 +190,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        sample window (0: eight-lane patches gathering the taps from the L1 cache);
  *   "patch_quad" (0/1, default 1): windowed gray patches (p = 8 / 12) on four lanes per patch, the Eigen
  *                        slot pairs packed (0: eight lanes per patch);
- *   "patch_x16" (0/1, default 1): windowed RGB p = 12 patches on sixteen lanes per patch, the Eigen slot chains
- *                        folded in block order on eight owner lanes (0: eight lanes per patch);
+ *   "patch_x16" (0..2, default 1): windowed RGB p = 12 patches on sixteen lanes per patch, the Eigen slot chains
+ *                        folded in block order on eight owner lanes (0: eight lanes per patch; 2: sixteen lanes,
+ *                        every evaluation on the exact square-root form -- parity testing of the fallback);
  *   "patch_absw" (0/1, default 1): without usefbcon, the four- and sixteen-lane patch kernels store each patch
  *                        pixel's aggregation weight into slot planes ([n][A*A][h][w], A = (p-1)/steps + 1) instead
  *                        of their loss weights, so the aggregation reads coalesced plane rows (0: loss weights);

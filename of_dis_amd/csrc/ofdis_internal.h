@@ -70,7 +70,7 @@ struct PatchArgs {
   int generic;                                // 1: force the any-shape kernel k_patchg (parity testing)
   int window;                                 // LDS-windowed bilinear taps (k_patchw) where the shape has one
   int quad;                                   // four lanes per patch (k_patchq) where the shape has that form
-  int x16;                                    // sixteen lanes per patch (k_patchx) for RGB p = 12
+  int x16;                                    // sixteen lanes per patch (k_patchx) for RGB p = 12 (2: exact evaluations)
   int absw;                                   // 1: write the aggregation weight of every patch pixel into the slot
                                               // planes (agg_plane_off) instead of the loss weights, where the kernel
                                               // can (launch_patch returns whether it did)

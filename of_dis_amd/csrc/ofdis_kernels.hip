@@ -2087,6 +2087,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     if (live && s16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[M - 1] + pin0 + pin1;
     return;
   }
+  // the scaled FAST evaluation's condition (see evaluate): every nonzero gradient of the wave's patches >= 2^-51
+  bool gsmall = false;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    gsmall |= gx[m] != 0.0f && fabsf(gx[m]) < 0x1p-51f;
+    if constexpr (NOP == 2) gsmall |= gy[m] != 0.0f && fabsf(gy[m]) < 0x1p-51f;
+  }
+  const bool xok = __builtin_amdgcn_ballot_w64(gsmall) == 0;
   // template and gradients as value pairs (m, m + KP) of the pair groups, and the values of an odd last group
   f2p tmp2[NPP > 0 ? NPP : 1], gx2[NPP > 0 ? NPP : 1], gy2[NOP == 2 && NPP > 0 ? NPP : 1];
   float tmps[NS > 0 ? NS : 1];
@@ -2223,13 +2231,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       mean = div_n(mc.total());
     }
     // loss of one value: w (weight) and e (signed residual)
+    // FAST (COST > 0): w and e at the 2^32 scale (the last square root's exact rescaling moves to the totals, one
+    // multiplication per evaluation instead of per value); the products with the gradients and every partial sum
+    // then round exactly as at scale 1 -- no product is subnormal at scale 1 (xok: nonzero gradients >= 2^-51,
+    // nonzero w >= 2^-75) and a sum's subnormal result is exact -- so the rescaled totals carry the same bits
     auto loss = [&](float d, float &w, float &e) {
       if (COST == 0) {
         e = d;
         w = fabsf(d);
       } else {
         auto sq = [](float x) { return FAST ? sqrt_nonneg_s64(x) : sqrt_nonneg(x); };
-        w = COST == 1 ? sq(fabsf(d)) : sq((sq(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
+        auto sqo = [](float x) { return FAST ? sqrt_nonneg_s64_x32(x) : sqrt_nonneg(x); };
+        w = COST == 1 ? sqo(fabsf(d)) : sqo((sq(1.0f + (d * d) / 25.0f) - 1.0f) * 50.0f);
         e = copysignf(w, d);
       }
     };
@@ -2289,9 +2302,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     });
     if (STORE == 0) {
       flush(M - 1);
-      r0 = ab.total();
-      b0 = ex.total();
-      if (NOP == 2) b1 = ey.total();
+      constexpr float sc = (FAST && COST != 0) ? 0x1p-32f : 1.0f;
+      r0 = ab.total() * sc;
+      b0 = ex.total() * sc;
+      if (NOP == 2) b1 = ey.total() * sc;
     }
   };
   // absw: the patch's aggregation weights into the slot planes (agg_plane_off) instead of its loss weights
@@ -2334,9 +2348,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         }
       }
       float r0 = 0.0f;
-      evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type());
-      if (COST != 0 && __builtin_amdgcn_ballot_w64(!(r0 <= 3.402823466e38f)) != 0)
-        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type());
+      bool exact = COST != 0 && (!xok || a.x16 == 2);
+      if (!exact) {
+        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type());
+        constexpr float fmx = 3.402823466e38f;
+        exact = COST != 0 && __builtin_amdgcn_ballot_w64(!(r0 <= fmx) || !(fabsf(b0) <= fmx) ||
+                                                         (NOP == 2 && !(fabsf(b1) <= fmx))) != 0;
+      }
+      if (exact) evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type());
       // OptimizeComputeErrImg (patch.cpp:275-295)
       sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
       if (cnt == 1) sq_init = sq;

@@ -24,6 +24,17 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
 // sqrt(x) (both normal: power-of-two scales commute with the rounding).  Two multiplications instead of the
 // compare, selects and multiplication of the conditional scaling.  Bit-identical to sqrtf over [0, 2^64)
 // (tools/sqrt_probe3.hip, every float); x >= 2^64 overflows to +inf -- callers detect that and redo the exact form.
+// 2^32 sqrt(x), correctly rounded, for 0 <= x < 2^64: sqrt_nonneg_s64 before its exact final scaling (callers that
+// keep their sums at the 2^32 scale and rescale the totals)
+__device__ __forceinline__ float sqrt_nonneg_s64_x32(float x) {
+  const float xs = x * 0x1p+64f;
+  const float s = __builtin_amdgcn_sqrtf(xs);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  float r = __builtin_fmaf(-sm, s, xs) <= 0.0f ? sm : s;
+  r = __builtin_fmaf(-sp, s, xs) > 0.0f ? sp : r;
+  return r;
+}
 __device__ __forceinline__ float sqrt_nonneg_s64(float x) {
   const float xs = x * 0x1p+64f;
   const float s = __builtin_amdgcn_sqrtf(xs);

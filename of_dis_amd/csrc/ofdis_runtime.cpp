@@ -105,7 +105,8 @@ struct ofdis_context {
                                // measured slower than the two launches)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
-  int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw)
+  int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw;
+                               // 2: k_patchx with the exact square-root evaluation every iteration, parity testing)
   int opt_patch_absw = 1;      // patch kernels that can hand the aggregation its weights directly do (0: loss weights)
   int opt_patch_buf = 1;       // gray p = 12 windows by buffer loads (32-bit offsets) where the image array allows
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
@@ -1258,7 +1259,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
-      {"patch_x16", &ofdis_context::opt_patch_x16, 0, 1},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
+      {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},
       {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},      {"sor_flow", &ofdis_context::opt_sor_flow, 0, 1},
       {"sor_dma", &ofdis_context::opt_sor_dma, 0, 2},

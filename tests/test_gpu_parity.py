@@ -129,6 +129,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
     ("patch_quad", 0, 1),      # gray p = 8 / 12 on eight lanes per patch (k_patchw) instead of four (k_patchq)
     ("patch_x16", 0, 1),       # RGB p = 12 on eight lanes per patch (k_patchw) instead of sixteen (k_patchx)
+    ("patch_x16", 2, 1),       # k_patchx on its exact square-root evaluation (the fallback of the scaled fast one)
     ("patch_absw", 0, 1),      # loss weights to the aggregation instead of the aggregation-weight slot planes
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
     ("tv_flow", 1, 0),         # levels <= 64 rows: one dataflow launch per inner iteration (k_tv_flow)
