@@ -2096,7 +2096,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   const bool xok = __builtin_amdgcn_ballot_w64(gsmall) == 0;
   // template and gradients as value pairs (m, m + KP) of the pair groups, and the values of an odd last group
-  f2p tmp2[NPP > 0 ? NPP : 1], gx2[NPP > 0 ? NPP : 1], gy2[NOP == 2 && NPP > 0 ? NPP : 1];
+  // (optical flow: the gradients as (gx, gy) pairs of one value -- ga value m, gb value m + KP -- so a value's two
+  // products are one v_pk_mul_f32 and its two chains' own adds one v_pk_add_f32)
+  f2p tmp2[NPP > 0 ? NPP : 1], gx2[NOP == 1 && NPP > 0 ? NPP : 1];
+  f2p ga[NOP == 2 && NPP > 0 ? NPP : 1], gb[NOP == 2 && NPP > 0 ? NPP : 1];
   float tmps[NS > 0 ? NS : 1];
   // the odd group's gradients: LDS float NOP (i 256 + tid) (+1), written and read by the lane itself only
   float *gsl = win_all + 16 * S::WIN + NOP * threadIdx.x;
@@ -2104,8 +2107,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   for (int j = 0; j < NPP; ++j) {
     const int m = (j / KP) * 2 * KP + j % KP;
     tmp2[j] = f2p{tmp[m], tmp[m + KP]};
-    gx2[j] = f2p{gx[m], gx[m + KP]};
-    if constexpr (NOP == 2) gy2[j] = f2p{gy[m], gy[m + KP]};
+    if constexpr (NOP == 2) {
+      ga[j] = f2p{gx[m], gy[m]};
+      gb[j] = f2p{gx[m + KP], gy[m + KP]};
+    } else {
+      gx2[j] = f2p{gx[m], gx[m + KP]};
+    }
   }
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
@@ -2246,33 +2253,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         e = copysignf(w, d);
       }
     };
-    auto gyp = [&](int j) -> f2p {  // compile-time j (depth: no y gradients)
-      if constexpr (NOP == 2) return gy2[j];
-      return f2p{0.0f, 0.0f};
-    };
-    XAcc ab, ex, ey;
+    XAcc ab, ex;
+    f2p exy = f2p{0.0f, 0.0f};  // optical flow: the x and y chains side by side (own adds packed)
     // pair groups: d of both halves packed; the .x halves (values m) go into the chains at once, the .y halves'
     // d (values m + KP) are kept until their turn, after the group's KP .x values
     // chain adds run one value behind the products: a DPP source written by the instruction just before needs wait
     // states (s_nop), the previous value's products were written long before
-    float pw = 0.0f, pqx = 0.0f, pqy = 0.0f;
+    float pw = 0.0f, pqx = 0.0f;
+    f2p pq = f2p{0.0f, 0.0f};
+    auto dppf = [](float x) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
+    };
     auto flush = [&](int m) {  // compile-time m: value m's terms into the chains
       ab.own(m, pw);  // w >= +0 for every cost (|d| or a square root): |w| == w
-      ex.own(m, pqx);
-      if constexpr (NOP == 2) ey.own(m, pqy);
+      if constexpr (NOP == 2) {
+        exy = m == 0 ? pq : exy + pq;  // the x and y chains' own values (XAcc::own, two chains at once)
+      } else {
+        ex.own(m, pqx);
+      }
       ab.partner(pw);
-      ex.partner(pqx);
-      if constexpr (NOP == 2) ey.partner(pqy);
+      if constexpr (NOP == 2) {  // XAcc::partner per chain
+        exy.x = exy.x + dppf(pq.x);
+        exy.y = exy.y + dppf(pq.y);
+      } else {
+        ex.partner(pqx);
+      }
     };
-    auto value_out = [&](int m, float d, float gxv, float gyv) {  // compile-time m, in increasing order
+    // g: the value's (gx, gy) (depth: gx in .x)
+    auto value_out = [&](int m, float d, f2p g) {  // compile-time m, in increasing order
       float w, e;
       loss(d, w, e);
       if constexpr (STORE == 0) {
-        const float qx = gxv * e, qy = NOP == 2 ? gyv * e : 0.0f;
         if (m > 0) flush(m - 1);
         pw = w;
-        pqx = qx;
-        pqy = qy;
+        if constexpr (NOP == 2)
+          pq = g * f2p{e, e};
+        else
+          pqx = g.x * e;
       } else {
         out[s16 + 16 * m] = w;
       }
@@ -2284,28 +2301,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         constexpr int i = decltype(ic)::value, j = gg * KP + i;
         const f2p d = (pd2[j] - mean) - tmp2[j];
         dy[i] = d.y;
-        value_out(2 * gg * KP + i, d.x, gx2[j].x, gyp(j).x);
+        if constexpr (NOP == 2)
+          value_out(2 * gg * KP + i, d.x, ga[j]);
+        else
+          value_out(2 * gg * KP + i, d.x, f2p{gx2[j].x, 0.0f});
       });
       static_for<KP>([&](auto ic) {
         constexpr int i = decltype(ic)::value, j = gg * KP + i;
-        value_out(2 * gg * KP + KP + i, dy[i], gx2[j].y, gyp(j).y);
+        if constexpr (NOP == 2)
+          value_out(2 * gg * KP + KP + i, dy[i], gb[j]);
+        else
+          value_out(2 * gg * KP + KP + i, dy[i], f2p{gx2[j].y, 0.0f});
       });
     });
     static_for<NS>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (NOP == 2) {
         const f2p gr = *reinterpret_cast<const f2p *>(gsl + 2 * 256 * i);
-        value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gr.x, gr.y);
+        value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gr);
       } else {
-        value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], gsl[256 * i], 0.0f);
+        value_out(2 * NPP + i, (pds[i] - mean) - tmps[i], f2p{gsl[256 * i], 0.0f});
       }
     });
     if (STORE == 0) {
       flush(M - 1);
       constexpr float sc = (FAST && COST != 0) ? 0x1p-32f : 1.0f;
       r0 = ab.total() * sc;
-      b0 = ex.total() * sc;
-      if (NOP == 2) b1 = ey.total() * sc;
+      if constexpr (NOP == 2) {
+        XAcc tx, ty;
+        tx.acc = exy.x;
+        ty.acc = exy.y;
+        b0 = tx.total() * sc;
+        b1 = ty.total() * sc;
+      } else {
+        b0 = ex.total() * sc;
+      }
     }
   };
   // absw: the patch's aggregation weights into the slot planes (agg_plane_off) instead of its loss weights
