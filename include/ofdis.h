@@ -158,11 +158,13 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "sor_generic" (0/1): force the generic global-memory SOR wavefront;
  *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline (the default for tall levels)
  *                        instead of the sweep-per-wave SOR;
- *   "sor_cring" (0..3, default 2): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
+ *   "sor_cring" (0..4, default 2): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
  *                        hands them to the later sweeps through LDS (solverit <= 3); 2: the LDS ring sized to
  *                        the level's rows (more frames per CU at 3 sweeps), its optical-flow entries 28 instead
  *                        of 32 bytes in launches with more frames than the chip holds where that fits more
- *                        frames per CU; 3: always 28-byte entries; 1: sized to the workgroup limit;
+ *                        frames per CU, and in such launches the lanes outside the frame load one shared slot
+ *                        (fewer fetched lines, one more select per load); 3: always 28-byte entries and that
+ *                        select; 4: always 32-byte entries and the select; 1: sized to the workgroup limit;
  *   "sor_rows2" (0/1, default 1): levels too tall for one row per lane in a 1024-thread workgroup run the
  *                        sweep-per-wave SOR with two rows per lane -- 321..640 rows at 3 sweeps, 513..1024 at
  *                        2 (else the register pipeline);
@@ -212,17 +214,6 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
  *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
- *   "sor_flow" (0/1, default 0): levels of up to 128 rows run the exact-order SOR as sweep waves that hand the
- *                        diagonals to each other through LDS progress counters instead of workgroup barriers, fed
- *                        by an LDS-DMA loader wave (0: the barrier-synchronised sweep-per-wave SOR; opt-in: measured
- *                        ~3x slower per launch);
- *   "sor_dma" (0/1/2, default 0): levels of up to 128 rows run the exact-order SOR with its sweep-0 operands (the
- *                        coefficient row, the old (du, dv)) streamed into LDS by an LDS-DMA loader wave ahead of the
- *                        wavefront, one barrier per step (2: only for launches of at most 256 frames);
- *   "tv_flow" (0/1, default 0): levels of up to 64 rows run each TV inner iteration (smoothness, system and
- *                        the exact-order SOR) as one launch whose waves hand the diagonals to each other through
- *                        LDS (no coefficient round trip through HBM; measured slower than the system and SOR
- *                        launches: one CU issues the whole system);
  *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
@@ -242,10 +233,6 @@ int ofdis_context_enable_kernel_timing(ofdis_context *ctx, int enable);
 int ofdis_context_kernel_time(ofdis_context *ctx, const char *name, double *total_ms, long *launches);
 /* Comma-separated list of kernel names known to the timer. */
 const char *ofdis_kernel_names(void);
-
-/* Diagnostic: launches of the dataflow TV iteration (option "tv_flow") on `device` that hit their bounded wait
- * and ended early since the last call (then reset); 0 in every correct run, < 0 on a HIP error. */
-int ofdis_flow_abort_count(int device);
 
 /* Per-frame algorithmic byte counts of the §8(d) byte model for this workload. */
 int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const char *kernel, double *bytes_per_frame);

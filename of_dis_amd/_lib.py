@@ -110,7 +110,6 @@ def lib():
         "ofdis_context_enable_kernel_timing": ([vp, i], i),
         "ofdis_context_kernel_time": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_long)], i),
         "ofdis_kernel_names": ([], C.c_char_p),
-        "ofdis_flow_abort_count": ([i], i),
         "ofdis_algorithmic_bytes": ([P, i, i, C.c_char_p, C.POINTER(C.c_double)], i),
         "ofdis_max_frames_per_launch": ([P, i, i, C.POINTER(i)], i),
         "ofdis_write_flo": ([C.c_char_p, vp, i, i, i], i),

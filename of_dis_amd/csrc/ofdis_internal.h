@@ -128,11 +128,6 @@ struct TvArgs {
                                // (k_tv_prepd then writes only Ix, Iy, Iz of the derivative planes); set by the
                                // runtime only where tv_deriv_fused() holds
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)
-  int tv_flow;                 // one dataflow launch per inner iteration (k_tv_flow: smoothness + system + SOR,
-                               // intermediates in LDS) where tv_flow_ok() holds
-  int *flow_err;               // device counter of k_tv_flow launches that hit their spin bound (0 = none)
-  int sor_flow;                // exact-order SOR as the barrier-free k_tv_sorflow where tv_sorflow_ok() holds
-  int sor_dma;                 // exact-order SOR as k_tv_sordma (barriers, LDS-DMA loader) where tv_sordma_ok() holds
 };
 
 struct UpArgs {
@@ -169,14 +164,6 @@ bool tv_smsys_ok(const TvArgs &a);
 bool tv_deriv_fused(const TvArgs &a);  // the level's derivative filters can move into k_tv_smsys (smsys_deriv)
 void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
-bool tv_flow_ok(const TvArgs &a);  // ofdis_tvflow.hip
-void launch_tv_flow(const TvArgs &a, hipStream_t s);
-bool tv_sorflow_ok(const TvArgs &a);
-bool tv_sordma_ok(const TvArgs &a);
-void launch_tv_sordma(const TvArgs &a, hipStream_t s);
-void launch_tv_sorflow(const TvArgs &a, hipStream_t s);
-int *tv_flow_err_counter();        // device address of the current device's k_tv_flow abort counter
-int tv_flow_err_take();            // its value (synchronous read), reset to 0
 void launch_tv_final(const TvArgs &a, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);
 

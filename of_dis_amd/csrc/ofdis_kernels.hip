@@ -22,6 +22,7 @@
 #include "ofdis_internal.h"
 #include "ofdis_math.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -3907,7 +3908,8 @@ __device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
 // pixel each per step -- the rows of one step are independent (their top neighbours ran at step t-1 and are in
 // the ring), so R = 2 runs levels of up to 640 rows with S <= 3 in 16 waves (E's 544-row level) where R = 1
 // would need 27.  Every per-row ring / coefficient-ring offset is a compile-time multiple of 64 entries.
-template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool CZ = false>
+// SEL: load form of the lanes outside the frame (see load()).
+template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool CZ = false, bool SEL = false>
 struct SorLane {
   static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
   static_assert(CRN == 0 || S <= 3, "coefficient ring depth 6 needs S <= 3");
@@ -3962,13 +3964,17 @@ struct SorLane {
     const unsigned r1 = FIRST ? (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane : 0u;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      // only the lanes whose pixel (d - yr, yr) is inside the frame fetch their own slot: a plane row holds h
-      // slots, of which the folded layout gives the others to diagonal d -+ w, so every slot was fetched
-      // (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels (the PMC fetch excess).  The
-      // other lanes read the row's first slot (one line they share; every use of their values is discarded by a
-      // select).  A select, not an exec-masked load: loads under a branch cost the prefetch (the wait-count pass
-      // then waits for them at the join, measured: tv_sor 135 -> 166 us per launch).
-      const unsigned yr = ((unsigned)(d - (y + 64 * r)) < (unsigned)w && y + 64 * r < h) ? (unsigned)(y + 64 * r) : 0u;
+      // SEL (launches with more frames than the chip holds at once): only the lanes whose pixel (d - yr, yr) is
+      // inside the frame fetch their own slot -- a plane row holds h slots, of which the folded layout gives the
+      // others to diagonal d -+ w, so every slot was fetched (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels
+      // (the PMC fetch excess); the other lanes read the row's first slot (one line they share;
+      // every use of their values is discarded by a select).  A select, not an exec-masked load: loads under a
+      // branch cost the prefetch (the wait-count pass then waits for them at the join: tv_sor 135 -> 166 us per
+      // launch).  !SEL (launches whose frames all fit the chip -- the latency regime): the lane-constant slot y + 64 r,
+      // no per-step vector address arithmetic on the step's critical path (the select cost the single pair's 18 SOR
+      // launches 0.50 -> 0.58 ms); its extra lines cost nothing when the chip is not full.
+      const unsigned yr = SEL ? (((unsigned)(d - (y + 64 * r)) < (unsigned)w && y + 64 * r < h) ? (unsigned)(y + 64 * r) : 0u)
+                              : (unsigned)(y + 64 * r);
       if (FIRST || CRN == 0) {
         const float4 *cp = C + (size_t)r0 * CW;
         B.c0[r] = cp[yr * CW];
@@ -4149,7 +4155,22 @@ struct SorLane {
 };
 
 constexpr size_t kSorLds = 160 * 1024;  // LDS per workgroup (gfx950: 160 KB per CU)
-constexpr long kCUs = 256;               // MI355X compute units
+constexpr int kCuWaves = 32;             // wave slots per CU (8 per SIMD)
+// Compute units of the current device (hipDeviceProp_t::multiProcessorCount; 256 on MI355X), cached per device.
+static long device_cus() {
+  static long cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int v = 0;
+    cus[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  return cus[dev];
+}
+// Frames of the sweep-per-wave SOR one CU holds at once: the LDS limit and the wave-slot limit (waves per frame).
+static long sor_frames_per_cu(size_t lds, int waves) {
+  return std::max(1L, std::min((long)(kSorLds / std::max<size_t>(lds, 1)), (long)(kCuWaves / std::max(waves, 1))));
+}
 // Entries per slot of the coefficient ring: the most rows a workgroup of MAXT threads holds, + 2 halos
 // (a compile-time constant, so every ring offset is an immediate); 0 = no coefficient ring (S > 3).
 __host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
@@ -4169,7 +4190,7 @@ __host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, 
 }
 
 // One frame's SOR call, lean form: 64 * G * S threads, R rows per lane.
-template <int S, int MODE, int NB, int CRN, int R, bool CZ = false>
+template <int S, int MODE, int NB, int CRN, int R, bool CZ = false, bool SEL = false>
 __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
   constexpr int CW = MODE == 0 ? 2 : 1;
   const int G = (a.h + 64 * R - 1) / (64 * R);
@@ -4231,28 +4252,28 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.run(T, y0, ymax);
   };
   if (s == 0) {
-    SorLane<S, MODE, 0, NB, CRN, R, CZ> st;
+    SorLane<S, MODE, 0, NB, CRN, R, CZ, SEL> st;
     setup(st);
   } else if (s == 1) {
-    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, CZ> st;
+    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, CZ, SEL> st;
     setup(st);
   } else if (s == 2) {
-    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, CZ> st;
+    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, CZ, SEL> st;
     setup(st);
   } else {
-    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, CZ> st;
+    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, CZ, SEL> st;
     setup(st);
   }
 }
 
 // CG > 0: the coefficient ring holds exactly the CG row groups of the level (+ 2 halos) instead of the most a
 // workgroup of MAXT threads can hold -- less LDS per frame, more frames per CU.
-template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool CZ = false>
+template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool CZ = false, bool SEL = false>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
   constexpr int crn = !CRING ? 0 : CG > 0 ? 64 * R * CG + 2 : sor_crn(S, MAXT, R);
   static_assert(CG == 0 || CG * 64 * S <= MAXT, "row groups of the workgroup");
-  sor_lanes_frame<S, MODE, NB, crn, R, CZ>(a, blockIdx.x, ring_uv);
+  sor_lanes_frame<S, MODE, NB, crn, R, CZ, SEL>(a, blockIdx.x, ring_uv);
 }
 
 template <int TH>
@@ -4717,7 +4738,6 @@ bool tv_smsys_ok(const TvArgs &a) {
 // Not where the 40 KB LDS cap of the DF form leaves fewer than 3 rows per block (levels of ~180-256 rows): a
 // block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
-  if (tv_flow_ok(a)) return a.noc == 1;  // the dataflow iteration filters the second derivatives itself (gray)
   if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys)) return false;
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) return a.smsys_march != 0;  // the march filters them too
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
@@ -4823,18 +4843,27 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
   if constexpr (S == 3 && R == 1) {
     if (cring && a.sor_cring >= 2) {  // the ring sized to the level's G row groups
       // OF launches with more frames than the chip holds at once: the 28-byte ring entries where they let more
-      // frames share a CU (throughput); else the 32-byte entries (one LDS read less on the step's critical path)
+      // frames share a CU (throughput); else the 32-byte entries (one LDS read less on the step's critical path).
+      // Frames per CU: the lesser of the LDS and the wave-slot limits (G S waves per frame), CUs of the device.
       const size_t ld32 = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R), ld28 = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R, true);
-      const bool cz = a.nop == 2 && (a.sor_cring == 3 || (kSorLds / ld28 > kSorLds / ld32 &&
-                                                          (long)a.n > (long)(kSorLds / ld32) * kCUs));
+      const long cus = device_cus(), f32 = sor_frames_per_cu(ld32, G * S), f28 = sor_frames_per_cu(ld28, G * S);
+      const bool cz = a.nop == 2 && (a.sor_cring == 3 || (a.sor_cring != 4 && f28 > f32 && (long)a.n > f32 * cus));
       const size_t ldsg = cz ? ld28 : ld32;
+      // the in-frame load select only where the launch oversubscribes the chip (sor_cring 3 / 4: everywhere, parity)
+      const bool sel = a.sor_cring >= 3 || (long)a.n > (cz ? f28 : f32) * cus;
       auto go = [&](auto gc) {
         constexpr int CG = decltype(gc)::value;
         if (a.nop == 2) {
-          if (cz) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true><<<a.n, th, ldsg, s>>>(a);
-          else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+          if (cz) {
+            if (sel) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true, true><<<a.n, th, ldsg, s>>>(a);
+            else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true, false><<<a.n, th, ldsg, s>>>(a);
+          } else {
+            if (sel) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, false, true><<<a.n, th, ldsg, s>>>(a);
+            else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, false, false><<<a.n, th, ldsg, s>>>(a);
+          }
         } else {
-          k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG><<<a.n, th, ldsg, s>>>(a);
+          if (sel) k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG, false, true><<<a.n, th, ldsg, s>>>(a);
+          else k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG, false, false><<<a.n, th, ldsg, s>>>(a);
         }
       };
       if constexpr (MAXT == 512) {
@@ -4869,14 +4898,6 @@ static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
 // global-memory wavefront for the point SOR of the OpenMP build and degenerate sizes.
 void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   if (a.solverit < 1) return;
-  if (tv_sordma_ok(a)) {  // latency regime: sweep waves fed by an LDS-DMA loader, barrier per step (ofdis_tvflow.hip)
-    launch_tv_sordma(a, s);
-    return;
-  }
-  if (tv_sorflow_ok(a)) {  // barrier-free sweep waves fed by an LDS-DMA loader (ofdis_tvflow.hip)
-    launch_tv_sorflow(a, s);
-    return;
-  }
   const bool tiny = a.nop == 2 && (a.w < 2 || a.h < 2 || a.sor_point);  // point SOR (solver.c:34-78)
   if (a.sor_redblack && !tiny) {  // opt-in red-black order (not the reference's bits)
     const int n = a.w * a.h;

@@ -26,7 +26,7 @@ using namespace ofdis;
 namespace {
 
 const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_flow"};
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -93,16 +93,13 @@ struct ofdis_context {
   int call_frames = 1;         // pairs of the current call (auto options)
   int opt_sor_cring = 2;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients;
                                // 2: ring sized to the level's row groups (28-byte OF entries in throughput
-                               // launches where they fit more frames per CU), 3: always 28-byte, 1: workgroup limit)
+                               // launches where they fit more frames per CU; the in-frame load select in launches
+                               // that oversubscribe the chip), 3: always 28-byte + select, 4: always 32-byte +
+                               // select, 1: workgroup limit)
   int opt_prepd = 1;           // prep + derivatives in one launch for intensity images (0: three launches, A/B)
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
-  int opt_sor_flow = 0;        // exact-order SOR of levels <= 128 rows as the barrier-free k_tv_sorflow (opt-in:
-                               // measured ~3x slower per launch than k_tv_sor_lanes)
-  int opt_sor_dma = 0;         // levels <= 128 rows: k_tv_sordma (1 always, 2 when a launch has at most 256 frames)
-  int opt_tv_flow = 0;         // one dataflow launch per TV inner iteration (k_tv_flow) where it fits (opt-in:
-                               // measured slower than the two launches)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw;
@@ -531,10 +528,6 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
-      tv.tv_flow = c->opt_tv_flow;
-      tv.sor_flow = c->opt_sor_flow;
-      tv.sor_dma = c->opt_sor_dma == 2 ? n <= 256 : c->opt_sor_dma;
-      tv.flow_err = tv_flow_err_counter();
       tv.smsys_deriv = tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
@@ -545,13 +538,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
           launch_tv_deriv2(tv, s);
         });
       }
-      const bool flow = tv_flow_ok(tv);
       for (int it = 0; it < n_inner; ++it) {
         tv.first_iter = it == 0;
-        if (flow) {  // smoothness + system + SOR of the iteration in one launch, intermediates in LDS
-          timed(c, 11, s, [&] { launch_tv_flow(tv, s); });
-          continue;
-        }
         timed(c, 7, s, [&] {
           if (tv_smsys_ok(tv)) {
             launch_tv_smsys(tv, s);
@@ -1249,7 +1237,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
-      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 3},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
+      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},
       {"smsys_prefetch", &ofdis_context::opt_smsys_prefetch, 0, 1},
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
@@ -1261,8 +1249,6 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},
-      {"tv_flow", &ofdis_context::opt_tv_flow, 0, 1},      {"sor_flow", &ofdis_context::opt_sor_flow, 0, 1},
-      {"sor_dma", &ofdis_context::opt_sor_dma, 0, 2},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {
@@ -1296,11 +1282,6 @@ int ofdis_context_kernel_time(ofdis_context *c, const char *name, double *total_
   if (total_ms) *total_ms = it == c->acc.end() ? 0.0 : it->second.first;
   if (launches) *launches = it == c->acc.end() ? 0 : it->second.second;
   return OFDIS_OK;
-}
-
-int ofdis_flow_abort_count(int device) {
-  if (hipSetDevice(device) != hipSuccess) return -1;
-  return tv_flow_err_take();
 }
 
 const char *ofdis_kernel_names(void) {
