@@ -214,6 +214,11 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
  *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
+ *   "sysor" (0/1, default 0): optical flow on intensity images, levels of up to 128 rows, 2 or 3 sweeps: each TV
+ *                        inner iteration as ONE launch -- smoothness, system and the 2x2 inverse produced three
+ *                        anti-diagonals ahead of the exact-order SOR wavefront by producer waves of the same
+ *                        workgroup, the coefficients handed over in LDS, one barrier per step (0: the system and
+ *                        the SOR as two launches, the coefficients through memory);
  *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
  *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
  *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).

@@ -128,6 +128,8 @@ struct TvArgs {
                                // (k_tv_prepd then writes only Ix, Iy, Iz of the derivative planes); set by the
                                // runtime only where tv_deriv_fused() holds
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)
+  int sysor;                   // levels <= 128 rows (optical flow, intensity images): smoothness + system + SOR of an
+                               // inner iteration in one launch (k_tv_sysor) where tv_sysor_ok() holds
 };
 
 struct UpArgs {
@@ -164,6 +166,8 @@ bool tv_smsys_ok(const TvArgs &a);
 bool tv_deriv_fused(const TvArgs &a);  // the level's derivative filters can move into k_tv_smsys (smsys_deriv)
 void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
+bool tv_sysor_ok(const TvArgs &a);  // ofdis_tvsysor.hip
+void launch_tv_sysor(const TvArgs &a, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);
 

@@ -26,7 +26,7 @@ using namespace ofdis;
 namespace {
 
 const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample"};
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_sysor"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -100,6 +100,8 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
+  int opt_sysor = 0;           // levels <= 128 rows (optical flow, intensity images): smoothness + system + SOR of an
+                               // inner iteration in one launch (k_tv_sysor)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw;
@@ -528,7 +530,9 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
-      tv.smsys_deriv = tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
+      tv.sysor = c->opt_sysor;
+      const bool sysor = tv_sysor_ok(tv);  // the fused launch reads the eight derivative planes: prepd writes them all
+      tv.smsys_deriv = !sysor && tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
       } else {
@@ -540,6 +544,10 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       }
       for (int it = 0; it < n_inner; ++it) {
         tv.first_iter = it == 0;
+        if (sysor) {  // smoothness + system + SOR of the iteration in one launch, the coefficients in LDS
+          timed(c, 11, s, [&] { launch_tv_sysor(tv, s); });
+          continue;
+        }
         timed(c, 7, s, [&] {
           if (tv_smsys_ok(tv)) {
             launch_tv_smsys(tv, s);
@@ -1249,6 +1257,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},
+      {"sysor", &ofdis_context::opt_sysor, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {
@@ -1307,6 +1316,8 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
     const double px = (double)g.w * g.h;
     const int n_inner = p->usetvref ? p->tv_innerit * (g.level + 1) : 0;
     if (k == "tv_sor") b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
+    // fused system + SOR: wx, wy, du, dv and the eight derivative planes in, du, dv out -- once per inner iteration
+    if (k == "tv_sysor") b += n_inner * px * 4.0 * (2 * nop + 8 * noc + nop);
     if (k == "tv_system") b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
     // patch: per patch the template + gradients, ONE (p+1)^2 target window, the outputs (the compulsory bytes;
     // re-reads of the window over the iterations are cache-resident, and the kernel is VALU-issue bound)

@@ -130,6 +130,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_x16", 2, 1),       # k_patchx on its exact square-root evaluation (the fallback of the scaled fast one)
     ("patch_absw", 0, 1),      # loss weights to the aggregation instead of the aggregation-weight slot planes
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
+    ("sysor", 1, 0),           # levels <= 128 rows: system + SOR of an inner iteration in one launch (k_tv_sysor)
 ]
 
 
