@@ -219,9 +219,14 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        anti-diagonals ahead of the exact-order SOR wavefront by producer waves of the same
  *                        workgroup, the coefficients handed over in LDS, one barrier per step (0: the system and
  *                        the SOR as two launches, the coefficients through memory);
- *   "pipeline" (0/1, default 0): with several chunks, a two-stream software pipeline instead: one stream runs
- *                        the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of chunks ch+1
- *                        and ch-1 while the other runs chunk ch's DIS + TV chain (event hand-overs).
+ *   "pipeline" (0..4, default 0): with several chunks, a software pipeline instead of the round robin: one stream
+ *                        runs the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of every chunk while
+ *                        L = "pipeline" chain lanes run the chunks' DIS + TV chains (chunk ch on lane ch mod L, event
+ *                        hand-overs, L + 1 workspaces);
+ *   "split_cus" (0..7, default 0): pipeline: the streaming stream runs on that many eighths of the CUs (a CU-masked
+ *                        stream; the eighths spread evenly over the XCDs), 0 = all CUs;
+ *   "chain_cus" (0..8, default 0): pipeline: the chain lanes run on the last that many eighths (complementary to
+ *                        "split_cus" when the two add up to 8), 0 or 8 = all CUs.
  * Setting any option drops the captured graph.  Unknown keys and out-of-range values return
  * OFDIS_ERR_INVALID_ARGUMENT.  Apart from "sor_mode", results never depend on these settings. */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);

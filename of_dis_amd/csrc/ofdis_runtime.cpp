@@ -114,13 +114,17 @@ struct ofdis_context {
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
   // chains on two streams), else 1; chunk 0 = the batch split evenly over the streams.
   int opt_streams = 0, opt_chunk = 0;
-  int opt_pipeline = 0;              // two-stream pipeline: streaming stages beside the DIS + TV chain
+  int opt_pipeline = 0;              // software pipeline: the streaming stages on one stream beside `opt_pipeline`
+                                     // chain lanes (DIS + TV), chunk ch on chain lane ch % L (0: off)
+  int opt_split_cus = 0;             // pipeline: the streaming stream on this many eighths of the CUs (0: all)
+  int opt_chain_cus = 0;             // pipeline: the chain lanes on the complementary eighths (0: all CUs)
   std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
     hipStream_t s = nullptr;
     char *ws = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;
+    int mask = 0;  // CU mask the stream was created with: 0 none, +k the first k eighths, -k the last k eighths
   };
   std::vector<Lane> lanes;
   hipEvent_t entry = nullptr;
@@ -798,12 +802,47 @@ int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, 
   return run_upsample(c, ws, P, p, flow_out, s);
 }
 
-int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
+// CU mask of k eighths of the device's CUs (k > 0: classes 0 .. k-1, k < 0: classes 8+k .. 7), CU i of class
+// ((i mod 8) + i / 8) mod 8.  Every class holds an equal share of each aligned group of 32 CUs and of each residue
+// mod 8, so the subset spreads evenly over the eight XCDs whether the mask's bits enumerate the CUs XCD by XCD or
+// interleave them.
+void cu_mask(int k, std::vector<uint32_t> &m) {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  m.assign((ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i) {
+    const int cls = ((i % 8) + i / 8) % 8;
+    if (k > 0 ? cls < k : cls >= 8 + k) m[i / 32] |= 1u << (i % 32);
+  }
+}
+
+// k lanes (stream, done event, workspace of `bytes`); masks[i] (when given): the CU mask of lane i's stream, which is
+// re-created when it differs from the one it has.
+int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *masks = nullptr) {
   if ((int)c->lanes.size() < k) c->lanes.resize(k);
   if (!c->entry) HIP_OK(hipEventCreateWithFlags(&c->entry, hipEventDisableTiming));
   for (int i = 0; i < k; ++i) {
     auto &L = c->lanes[i];
-    if (!L.s) HIP_OK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+    const int want = masks ? (*masks)[i] : L.mask;
+    if (L.s && L.mask != want) {  // a different CU mask: a new stream (after all queued work)
+      int rc = drop_graph(c);
+      if (rc) return rc;
+      HIP_OK(hipDeviceSynchronize());
+      HIP_OK(hipStreamDestroy(L.s));
+      L.s = nullptr;
+    }
+    if (!L.s) {
+      if (want == 0) {
+        HIP_OK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+      } else {
+        std::vector<uint32_t> m;
+        cu_mask(want, m);
+        HIP_OK(hipExtStreamCreateWithCUMask(&L.s, (uint32_t)m.size(), m.data()));
+      }
+      L.mask = want;
+    }
     if (!L.done) HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     if (L.cap < bytes) {
       if (L.ws) {
@@ -880,8 +919,15 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
   cp.kind = c->opt_pipeline && !c->timing ? CallPlan::kPipeline : CallPlan::kRoundRobin;
   for (int ch = 0; ch < cp.nchunks; ++ch)
     cp.parts.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height, init));
-  cp.lanes = cp.kind == CallPlan::kPipeline ? 2 : std::min(nstreams, cp.nchunks);
-  int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total);
+  // the pipeline: chain lanes 0 .. L-1 (CU mask: the last opt_chain_cus eighths), workspaces of lanes 0 .. L (chunk ch
+  // in workspace ch mod (L + 1)), the streaming stream = lane L (the first opt_split_cus eighths)
+  cp.lanes = cp.kind == CallPlan::kPipeline ? c->opt_pipeline + 1 : std::min(nstreams, cp.nchunks);
+  std::vector<int> masks(cp.lanes, 0);
+  if (cp.kind == CallPlan::kPipeline) {
+    for (int i = 0; i < c->opt_pipeline; ++i) masks[i] = c->opt_chain_cus > 0 && c->opt_chain_cus < 8 ? -c->opt_chain_cus : 0;
+    masks[c->opt_pipeline] = c->opt_split_cus;
+  }  // round robin: unmasked lanes (a lane a pipeline call masked gets a new stream)
+  int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total, &masks);
   if (rc) return rc;
   if (cp.kind == CallPlan::kPipeline)
     while ((int)c->pipe_ev.size() < 2 * cp.nchunks) {
@@ -914,58 +960,61 @@ int issue_round_robin(ofdis_context *c, const CallPlan &cp, hipStream_t s, const
   return OFDIS_OK;
 }
 
-// Two-stream software pipeline over chunks ("pipeline" option).  Lane 0 runs the HBM-streaming stages --
-// the pyramid from the u8 frames and the full-resolution upsample -- and lane 1 the latency-bound
-// DIS + TV chain (run_levels), so chunk ch's chain overlaps chunk ch+1's pyramid and chunk ch-1's
-// upsample.  Issue order on lane 0: pyr 0, pyr 1, up 0, pyr 2, up 1, ...; chunk ch uses workspace
-// ch % 2, which pyr(ch+2) reuses only after up(ch) (same stream, issued before it), which waits for
-// levels(ch).  Every hand-over is an event recorded and waited on within this call (and so within a
-// capture), and both lanes join s at the end.
+// Software pipeline over chunks ("pipeline" option = L chain lanes).  One stream (lane L) runs the HBM-streaming
+// stages -- the pyramid from the u8 frames and the full-resolution upsample -- and L chain lanes the latency-bound
+// DIS + TV chain (run_levels) of chunk ch on lane ch mod L, so chains overlap the streaming of other chunks.  W = L + 1
+// workspaces: chunk ch uses workspace ch mod W.  Issue order on the streaming stream: pyr 0 .. W-1, then up c and
+// pyr c + W for c = 0, 1, ...: pyr c + W reuses the workspace of chunk c only after up c (same stream, issued before
+// it), which waits for levels c.  With "split_cus" / "chain_cus" the streaming stream and the chain lanes run on
+// disjoint CU subsets (hipExtStreamCreateWithCUMask), so the streaming kernels' workgroups never queue behind the
+// chains' (VERDICT r04 next 4).  Every hand-over is an event recorded before it is waited on (in host issue order)
+// within this call (and so within a capture), and all lanes join s at the end.
 int issue_pipeline(ofdis_context *c, const CallPlan &cp, hipStream_t s, const ofdis_params *p,
                    const uint8_t *img_a, const uint8_t *img_b, const float *init, float *flow_out) {
   const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
   const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
-  hipStream_t S = c->lanes[0].s, L = c->lanes[1].s;
+  const int L = cp.lanes - 1, W = cp.lanes;
+  hipStream_t S = c->lanes[L].s;
   hipEvent_t *ev_pyr = c->pipe_ev.data(), *ev_lev = c->pipe_ev.data() + cp.nchunks;
   // OFDIS_PIPE_SKIP (debugging the capture of this issue, tools/graph_probe.py): bit 0 leaves out the pyramid
   // launches, bit 1 the levels, bit 2 the upsample (the output is then wrong; the event pattern is kept)
   static const int skip = std::getenv("OFDIS_PIPE_SKIP") ? std::atoi(std::getenv("OFDIS_PIPE_SKIP")) : 0;
   HIP_OK(hipEventRecord(c->entry, s));
-  HIP_OK(hipStreamWaitEvent(S, c->entry, 0));
-  HIP_OK(hipStreamWaitEvent(L, c->entry, 0));
+  for (int i = 0; i <= L; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
   auto pyr = [&](int ch) -> int {
     const size_t f0 = (size_t)ch * cp.chunk;
-    char *ws = c->lanes[ch & 1].ws;
+    char *ws = c->lanes[ch % W].ws;
     int r = (skip & 1) ? 0 : run_pyramid(c, ws, cp.parts[ch], img_a + f0 * in_frame, img_b + f0 * in_frame, S);
     if (r) return r;
     if (init && (r = run_init(c, ws, cp.parts[ch], p, init + f0 * out_frame, S))) return r;
     HIP_OK(hipEventRecord(ev_pyr[ch], S));
     return OFDIS_OK;
   };
-  int rc = pyr(0);
-  if (rc) return rc;
+  int rc = OFDIS_OK;
+  for (int ch = 0; ch < std::min(W, cp.nchunks); ++ch)
+    if ((rc = pyr(ch))) return rc;
   for (int ch = 0; ch < cp.nchunks; ++ch) {
-    char *ws = c->lanes[ch & 1].ws;
+    char *ws = c->lanes[ch % W].ws;
     const Plan &P = cp.parts[ch];
-    HIP_OK(hipStreamWaitEvent(L, ev_pyr[ch], 0));
-    if (!(skip & 2) && (rc = run_levels(c, ws, P, p, L, init ? (const float *)(ws + P.off_init) : nullptr, nullptr)))
+    hipStream_t Lc = c->lanes[ch % L].s;
+    HIP_OK(hipStreamWaitEvent(Lc, ev_pyr[ch], 0));
+    if (!(skip & 2) && (rc = run_levels(c, ws, P, p, Lc, init ? (const float *)(ws + P.off_init) : nullptr, nullptr)))
       return rc;
-    HIP_OK(hipEventRecord(ev_lev[ch], L));
-    if (ch + 1 < cp.nchunks && (rc = pyr(ch + 1))) return rc;
+    HIP_OK(hipEventRecord(ev_lev[ch], Lc));
     HIP_OK(hipStreamWaitEvent(S, ev_lev[ch], 0));
     if (!(skip & 4) && (rc = run_upsample(c, ws, P, p, flow_out + (size_t)ch * cp.chunk * out_frame, S))) return rc;
+    if (ch + W < cp.nchunks && (rc = pyr(ch + W))) return rc;
   }
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i <= L; ++i) {
     HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
     HIP_OK(hipStreamWaitEvent(s, c->lanes[i].done, 0));
   }
   if (trace_on()) {
-    const hipStream_t ss[3] = {s, S, L};
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i <= L; ++i) {
       hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
       unsigned long long id = 0;
-      const hipError_t e = hipStreamGetCaptureInfo(ss[i], &st, &id);
-      OFDIS_TRACE("pipeline: stream %d (%p) capture status %d id %llu (err %d)", i, (void *)ss[i], (int)st, id, (int)e);
+      const hipError_t e = hipStreamGetCaptureInfo(c->lanes[i].s, &st, &id);
+      OFDIS_TRACE("pipeline: lane %d (%p) capture status %d id %llu (err %d)", i, (void *)c->lanes[i].s, (int)st, id, (int)e);
     }
   }
   return OFDIS_OK;
@@ -1243,7 +1292,8 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     int lo, hi;
   };
   static const Opt opts[] = {
-      {"pipeline", &ofdis_context::opt_pipeline, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
+      {"pipeline", &ofdis_context::opt_pipeline, 0, 4},     {"split_cus", &ofdis_context::opt_split_cus, 0, 7},
+      {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},

@@ -1,6 +1,6 @@
 // ofdis_tvsysor.hip -- one TV inner iteration of a level of at most 128 rows as ONE launch: the system
 // (compute_smoothness, compute_data, sub_laplacian and the 2x2 inverse of sor_coupled's first sweep) is produced
-// three anti-diagonals ahead of the exact-order SOR wavefront, inside the SOR's own barrier steps, and handed to the
+// four anti-diagonals ahead of the exact-order SOR wavefront, inside the SOR's own barrier steps, and handed to the
 // sweeps through LDS -- no coefficient round trip through HBM, no separate system launch.
 //
 // Reference: refine_variational.cpp:192-222 (the inner iteration), FDF1.0.1/opticalflow_aux.c:138-187
@@ -16,13 +16,14 @@
 // One workgroup per frame; lane = row y of a row group g (G = ceil(h / 64) <= 2), every wave joins every barrier:
 //   S x G sweep waves, wave (g, s) = sweep s of rows 64 g .. 64 g + 63 (k_tv_sor_lanes' schedule: pixel (x, y) of
 //     sweep s at step t = x + y + 2 s; interval t >= 0 is SOR step t);
-//   3 x G producer waves, wave (g, j) = the system of the diagonals d = j (mod 3), spread over three intervals:
-//     A at d - 3: writes row d + 4 into the row ring (loaded at its previous A), computes s(d + 2) into the s ring
-//       and the colour half of the data term, issues the loads of row d + 7 and of diagonal d + 3's derivatives;
-//     B at d - 2: the gradient half of the data term;
-//     C at d - 1: sub_laplacian from the s and wx / wy rings, the inverse (sys_finish), the coefficient ring write.
-//   Row r is written at interval r - 7 and read until r (sweep 0 takes the old (du, dv) from the row ring), s(e) lives
-//   from e - 5 to e, the coefficients of d from d - 1 to d + 2 (S - 1): eight slots each.
+//   4 x G producer waves, wave (g, j) = the system of the diagonals d = j (mod 4), spread over four intervals:
+//     A at d - 4: writes row d + 4 into the row ring (loaded at its previous A), computes s(d + 2) into the s ring,
+//       issues the loads of row d + 8 and of diagonal d + 4's derivatives;
+//     B at d - 3: the pixel's own values, the mask and the colour half of the data term;
+//     C at d - 2: the gradient half of the data term;
+//     D at d - 1: sub_laplacian from the s and wx / wy rings, the inverse (sys_finish), the coefficient ring write.
+//   Row r is written at interval r - 8 and read until r (sweep 0 takes the old (du, dv) from the row ring: 16 slots),
+//   s(e) lives from e - 6 to e, the coefficients of d from d - 1 to d + 2 (S - 1): eight slots each.
 // LDS rings are lane-major -- [entry y][slot], slot = diagonal mod 8, strides padded to an odd number of 16-byte
 // (or 4-byte) units, so a wave's ds_read_b128 / b64 / b32 of one slot is conflict-free; every SOR slot offset is an
 // immediate of the 8-step unrolled block.  Entries exist for rows 0 .. h - 1 (lanes beyond h read row h - 1: their
@@ -39,8 +40,10 @@ namespace {
 
 #include "ofdis_tv_dev.inc"
 
-constexpr int kYS = 8;                       // ring slots (power of 2)
-constexpr int kRowStride = 16 * (kYS + 1);   // bytes per row-ring entry: 8 float4 slots + 1 pad
+constexpr int kYS = 8;                       // s / coefficient ring slots (power of 2)
+constexpr int kRS = 16;                      // row ring slots (power of 2)
+constexpr int kRowStride = 16 * (kRS + 1);   // bytes per row-ring entry: 16 float4 slots + 1 pad
+constexpr int kPh = 4;                       // producer phases = producer waves per row group
 constexpr int kSStride = 4 * (kYS + 1);      // s ring: 8 floats + 1 pad
 constexpr int kCStride = 32 * kYS + 16;      // coefficient ring: 8 x (c0, c1) + 1 float4 pad
 constexpr int kUVSlots = 4;                  // (u, v) ring depth (steps t, t-1, t-2; a power of 2)
@@ -68,6 +71,15 @@ struct SysSorLds {
   }
 };
 
+// Register pins: the values are "redefined" here, so no computation that uses them can move above this point and
+// none that produces them below it.  Around each barrier they keep a phase's arithmetic inside its interval (the
+// barrier orders memory only: the compiler otherwise hoisted phase B's register-only work into phase A).
+__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+template <class... T>
+__device__ __forceinline__ void pins(T &...x) {
+  (pin(x), ...);
+}
+
 // ------------------------------------------------------------------------------------------------ producer
 struct Producer {
   TvArgs a;  // a copy: its fields live in scalar registers
@@ -84,7 +96,7 @@ struct Producer {
   bool first;
 
   __device__ __forceinline__ float4 &row_at(int r, unsigned oe) const {
-    return *reinterpret_cast<float4 *>(rows + oe * kRowStride + (unsigned)(r & (kYS - 1)) * 16u);
+    return *reinterpret_cast<float4 *>(rows + oe * kRowStride + (unsigned)(r & (kRS - 1)) * 16u);
   }
   __device__ __forceinline__ float &s_at(int e, unsigned oe) const {
     return *reinterpret_cast<float *>(sr + oe * kSStride + (unsigned)(e & (kYS - 1)) * 4u);
@@ -110,28 +122,38 @@ struct Producer {
     const float sv = smooth_compute<2>(a, first, wx5, du5, wy5, dv5);
     if (yin) s_at(e, o_ye) = (unsigned)x < (unsigned)w ? sv : 0.0f;
   }
+  // A (interval d - 4): the row loaded four intervals ago into the ring, s(d + 2), the loads of row d + 8 and of
+  // diagonal d + 4's derivatives (this wave's next diagonal)
   __device__ __forceinline__ void phase_a(int d) {
     if (yin) row_at(d + 4, o_ye) = rowv;
     smooth(d + 2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = dq[k];
+    load_row(d + 8);
+    load_deriv(d + 4);
+  }
+  // B (d - 3): the pixel's own values, image_warp's mask, the colour half of the data term
+  __device__ __forceinline__ void phase_b(int d) {
     const float4 own = row_at(d, o_ye);
     wxc = own.x;
     wyc = own.y;
     u = own.z;
     v = own.w;
     m = warp_mask(d - y, y, wxc, wyc, w, h);
-    data_of_gray_colour(u, v, m, dq[0], dq[1], dq[2], a.hdo3, A11, A12, A22, B1, B2);
-    float g5[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) g5[k] = dq[3 + k];
-    load_row(d + 7);
-    load_deriv(d + 3);
-    gIxx = g5[0]; gIxy = g5[1]; gIyy = g5[2]; gIxz = g5[3]; gIyz = g5[4];
+    data_of_gray_colour(u, v, m, cur[0], cur[1], cur[2], a.hdo3, A11, A12, A22, B1, B2);
   }
-  float gIxx, gIxy, gIyy, gIxz, gIyz;
-  __device__ __forceinline__ void phase_b() {
-    data_of_gray_gradient(u, v, m, gIxx, gIxy, gIyy, gIxz, gIyz, a.hgo3, A11, A12, A22, B1, B2);
+  float cur[8];
+  __device__ __forceinline__ void pin_ab() { pins(cur[0], cur[1], cur[2], cur[3], cur[4], cur[5], cur[6], cur[7]); }
+  __device__ __forceinline__ void pin_bc() {
+    pins(u, v, m, wxc, wyc, A11, A12, A22, B1, B2, cur[3], cur[4], cur[5], cur[6], cur[7]);
   }
-  __device__ __forceinline__ void phase_c(int d) {
+  __device__ __forceinline__ void pin_cd() { pins(wxc, wyc, A11, A12, A22, B1, B2); }
+  // C (d - 2): the gradient half
+  __device__ __forceinline__ void phase_c() {
+    data_of_gray_gradient(u, v, m, cur[3], cur[4], cur[5], cur[6], cur[7], a.hgo3, A11, A12, A22, B1, B2);
+  }
+  // D (d - 1): sub_laplacian, the inverse, the coefficient ring write
+  __device__ __forceinline__ void phase_d(int d) {
     const int x = d - y;
     const float S5[5] = {s_at(d, o_ye), s_at(d - 1, o_ye), s_at(d + 1, o_ye), s_at(d - 1, o_yu), s_at(d + 1, o_yd)};
     const float4 ql = row_at(d - 1, o_ye), qr = row_at(d + 1, o_ye), qu = row_at(d - 1, o_yu), qd = row_at(d + 1, o_yd);
@@ -233,7 +255,7 @@ struct Sweep {
 };
 
 template <int S, int G>
-__global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
+__global__ __launch_bounds__(64 * G * (S + kPh)) void k_tv_sysor(TvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int h = a.h, w = a.w;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -244,7 +266,7 @@ __global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
   const long fo = (long)f * a.sp;
   const int lim = a.wrap ? w : 1 << 30, rmax = a.wrap ? w - 1 : w + h - 2;
   const int T = ((w - 1) + (h - 1) + 2 * (S - 1) + 1 + kSU - 1) / kSU * kSU;  // SOR steps
-  const int NI = 3 + T;                                                      // intervals -3 .. T - 1
+  const int NI = kPh + T;                                                    // intervals -kPh .. T - 1
   if (wid < S * G) {
     // ---------------------------------------------------------------- sweep wave (g, s)
     const int g = wid / S, s = wid - g * S;
@@ -271,7 +293,7 @@ __global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
       st.omega = a.omega;
       __syncthreads();  // prologue: the producers' first rows
       __syncthreads();  // prologue: s(0), s(1)
-      for (int i = 0; i < 3; ++i) __syncthreads();  // intervals -3 .. -1: the first coefficients
+      for (int i = 0; i < kPh; ++i) __syncthreads();  // intervals -kPh .. -1: the first coefficients
       st.run(T, y0, ymax);
     };
     if (s == 0) {
@@ -287,7 +309,7 @@ __global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
     return;
   }
   // ------------------------------------------------------------------ producer wave (g, j)
-  const int k = wid - S * G, g = k / 3, j = k - 3 * g;
+  const int k = wid - S * G, g = k / kPh, j = k - kPh * g;
   Producer P;
   P.a = a;
   P.y = 64 * g + lane;
@@ -308,8 +330,8 @@ __global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
   const long fd = (long)f * a.sp;  // intensity images: one channel plane per frame
   P.pd[0] = a.Ix + fd; P.pd[1] = a.Iy + fd; P.pd[2] = a.Iz + fd; P.pd[3] = a.Ixx + fd;
   P.pd[4] = a.Ixy + fd; P.pd[5] = a.Iyy + fd; P.pd[6] = a.Ixz + fd; P.pd[7] = a.Iyz + fd;
-  // prologue: rows 0 .. 3 (wave j: rows j and j + 3), then the loads of this wave's first A (row j + 4, diagonal j)
-  for (int r = j; r < 4; r += 3) {
+  // prologue: rows 0 .. 3 (wave j: row j), then the loads of this wave's first A (row j + 4, diagonal j)
+  for (int r = j; r < 4; r += kPh) {
     P.load_row(r);
     if (P.yin) P.row_at(r, P.o_ye) = P.rowv;
   }
@@ -318,15 +340,23 @@ __global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
   __syncthreads();
   if (j < 2) P.smooth(j);  // s(0), s(1): phase A of diagonal d computes s(d + 2)
   __syncthreads();
-  // intervals: wave j starts diagonal j at interval j - 3, then every third diagonal
+  // intervals: wave j starts diagonal j at interval j - kPh, then every kPh-th diagonal
   int left = NI;
   for (int i = 0; i < j; ++i, --left) __syncthreads();
-  for (int d = j; left >= 3; d += 3, left -= 3) {
+  for (int d = j; left >= kPh; d += kPh, left -= kPh) {
     P.phase_a(d);
+    P.pin_ab();
     __syncthreads();
-    P.phase_b();
+    P.pin_ab();
+    P.phase_b(d);
+    P.pin_bc();
     __syncthreads();
-    P.phase_c(d);
+    P.pin_bc();
+    P.phase_c();
+    P.pin_cd();
+    __syncthreads();
+    P.pin_cd();
+    P.phase_d(d);
     __syncthreads();
   }
   for (; left > 0; --left) __syncthreads();
@@ -334,7 +364,7 @@ __global__ __launch_bounds__(64 * G * (S + 3)) void k_tv_sysor(TvArgs a) {
 
 template <int S, int G>
 void launch_sysor_sg(const TvArgs &a, hipStream_t s) {
-  k_tv_sysor<S, G><<<a.n, 64 * G * (S + 3), sysor_lds(S, a.h), s>>>(a);
+  k_tv_sysor<S, G><<<a.n, 64 * G * (S + kPh), sysor_lds(S, a.h), s>>>(a);
 }
 
 }  // namespace
