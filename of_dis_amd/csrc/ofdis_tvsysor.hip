@@ -17,13 +17,13 @@
 //   S x G sweep waves, wave (g, s) = sweep s of rows 64 g .. 64 g + 63 (k_tv_sor_lanes' schedule: pixel (x, y) of
 //     sweep s at step t = x + y + 2 s; interval t >= 0 is SOR step t);
 //   4 x G producer waves, wave (g, j) = the system of the diagonals d = j (mod 4), spread over four intervals:
-//     A at d - 4: writes row d + 4 into the row ring (loaded at its previous A), computes s(d + 2) into the s ring,
-//       issues the loads of row d + 8 and of diagonal d + 4's derivatives;
-//     B at d - 3: the pixel's own values, the mask and the colour half of the data term;
+//     A at d - 4: writes row d + 3 into the row ring (loaded at its previous A), the pixel's own values, the mask and
+//       the colour half of the data term, issues the loads of row d + 7 and of diagonal d + 4's derivatives;
+//     B at d - 3: s(d + 2) into the s ring;
 //     C at d - 2: the gradient half of the data term;
 //     D at d - 1: sub_laplacian from the s and wx / wy rings, the inverse (sys_finish), the coefficient ring write.
-//   Row r is written at interval r - 8 and read until r (sweep 0 takes the old (du, dv) from the row ring: 16 slots),
-//   s(e) lives from e - 6 to e, the coefficients of d from d - 1 to d + 2 (S - 1): eight slots each.
+//   Row r is written at interval r - 7 and read until r (sweep 0 takes the old (du, dv) from the row ring), s(e) lives
+//   from e - 5 to e, the coefficients of d from d - 1 to d + 2 (S - 1): eight slots each.
 // LDS rings are lane-major -- [entry y][slot], slot = diagonal mod 8, strides padded to an odd number of 16-byte
 // (or 4-byte) units, so a wave's ds_read_b128 / b64 / b32 of one slot is conflict-free; every SOR slot offset is an
 // immediate of the 8-step unrolled block.  Entries exist for rows 0 .. h - 1 (lanes beyond h read row h - 1: their
@@ -41,8 +41,8 @@ namespace {
 #include "ofdis_tv_dev.inc"
 
 constexpr int kYS = 8;                       // s / coefficient ring slots (power of 2)
-constexpr int kRS = 16;                      // row ring slots (power of 2)
-constexpr int kRowStride = 16 * (kRS + 1);   // bytes per row-ring entry: 16 float4 slots + 1 pad
+constexpr int kRS = kYS;                     // row ring slots (the sweeps index it with the coefficient slot)
+constexpr int kRowStride = 16 * (kRS + 1);   // bytes per row-ring entry: 8 float4 slots + 1 pad
 constexpr int kPh = 4;                       // producer phases = producer waves per row group
 constexpr int kSStride = 4 * (kYS + 1);      // s ring: 8 floats + 1 pad
 constexpr int kCStride = 32 * kYS + 16;      // coefficient ring: 8 x (c0, c1) + 1 float4 pad
@@ -122,18 +122,13 @@ struct Producer {
     const float sv = smooth_compute<2>(a, first, wx5, du5, wy5, dv5);
     if (yin) s_at(e, o_ye) = (unsigned)x < (unsigned)w ? sv : 0.0f;
   }
-  // A (interval d - 4): the row loaded four intervals ago into the ring, s(d + 2), the loads of row d + 8 and of
-  // diagonal d + 4's derivatives (this wave's next diagonal)
+  // A (interval d - 4): the row loaded four intervals ago into the ring (row d + 3), the pixel's own values, image_warp's
+  // mask, the colour half of the data term; the loads of row d + 7 and of diagonal d + 4's derivatives (this wave's
+  // next diagonal)
   __device__ __forceinline__ void phase_a(int d) {
-    if (yin) row_at(d + 4, o_ye) = rowv;
-    smooth(d + 2);
+    if (yin) row_at(d + 3, o_ye) = rowv;
 #pragma unroll
     for (int k = 0; k < 8; ++k) cur[k] = dq[k];
-    load_row(d + 8);
-    load_deriv(d + 4);
-  }
-  // B (d - 3): the pixel's own values, image_warp's mask, the colour half of the data term
-  __device__ __forceinline__ void phase_b(int d) {
     const float4 own = row_at(d, o_ye);
     wxc = own.x;
     wyc = own.y;
@@ -141,12 +136,16 @@ struct Producer {
     v = own.w;
     m = warp_mask(d - y, y, wxc, wyc, w, h);
     data_of_gray_colour(u, v, m, cur[0], cur[1], cur[2], a.hdo3, A11, A12, A22, B1, B2);
+    load_row(d + 7);
+    load_deriv(d + 4);
   }
+  // B (d - 3): s(d + 2) into the s ring (rows d + 1 .. d + 3)
+  __device__ __forceinline__ void phase_b(int d) { smooth(d + 2); }
   float cur[8];
-  __device__ __forceinline__ void pin_ab() { pins(cur[0], cur[1], cur[2], cur[3], cur[4], cur[5], cur[6], cur[7]); }
-  __device__ __forceinline__ void pin_bc() {
+  __device__ __forceinline__ void pin_ab() {
     pins(u, v, m, wxc, wyc, A11, A12, A22, B1, B2, cur[3], cur[4], cur[5], cur[6], cur[7]);
   }
+  __device__ __forceinline__ void pin_bc() { pin_ab(); }
   __device__ __forceinline__ void pin_cd() { pins(wxc, wyc, A11, A12, A22, B1, B2); }
   // C (d - 2): the gradient half
   __device__ __forceinline__ void phase_c() {
@@ -330,12 +329,12 @@ __global__ __launch_bounds__(64 * G * (S + kPh)) void k_tv_sysor(TvArgs a) {
   const long fd = (long)f * a.sp;  // intensity images: one channel plane per frame
   P.pd[0] = a.Ix + fd; P.pd[1] = a.Iy + fd; P.pd[2] = a.Iz + fd; P.pd[3] = a.Ixx + fd;
   P.pd[4] = a.Ixy + fd; P.pd[5] = a.Iyy + fd; P.pd[6] = a.Ixz + fd; P.pd[7] = a.Iyz + fd;
-  // prologue: rows 0 .. 3 (wave j: row j), then the loads of this wave's first A (row j + 4, diagonal j)
-  for (int r = j; r < 4; r += kPh) {
+  // prologue: rows 0 .. 2 (wave j < 3: row j), then the loads of this wave's first A (row j + 3, diagonal j)
+  for (int r = j; r < 3; r += kPh) {
     P.load_row(r);
     if (P.yin) P.row_at(r, P.o_ye) = P.rowv;
   }
-  P.load_row(j + 4);
+  P.load_row(j + 3);
   P.load_deriv(j);
   __syncthreads();
   if (j < 2) P.smooth(j);  // s(0), s(1): phase A of diagonal d computes s(d + 2)
