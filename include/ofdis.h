@@ -180,8 +180,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        Ixz, Iyz from Ix, Iy, Iz and the prep launch does not write those five planes;
  *   "smsys_march" (0/1, default 1): levels taller than 256 rows run smoothness + system as a register march
  *                        (one wave per 60 columns x 64 rows, no LDS; takes precedence over smsys2d);
- *   "prepd" (0/1, default 1): for intensity images, image warp, temporal images and the derivative filters
- *                        of a level in one launch (0: three launches);
+ *   "prepd" (0..2, default 2): image warp, temporal images and the derivative filters of a level in one launch
+ *                        (1: intensity images only, colour images in three launches; 0: three launches);
  *   "sor_mode" (0/1, default 0): 0 = sor_coupled's exact lexicographic order (the reference's bits);
  *                        1 = red-black order (SURVEY §7 4(ii) throughput mode: every half-sweep fully
  *                        parallel; a different iteration -- NOT the reference's bits, end-point error

@@ -2675,80 +2675,90 @@ __device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int
 }
 
 
-// ---- prep + derivatives in one launch (intensity images): image_warp and get_derivatives' t / It
-// (opticalflow_aux.c:31-132) on a row-major tile with a 4-pixel halo in LDS, the first derivatives Ix, Iy of t
-// on the tile with a 2-pixel halo, then per core pixel the remaining 5-tap filters (Ixz, Iyz of It; Ixx, Ixy of
-// Ix; Iyy of Iy) straight from LDS and every plane written in skewed order (threads walk the tile's
-// anti-diagonals: contiguous skewed rows).  A halo position outside the level holds the value of the clamped
-// position, which is exactly the filters' replicate border; every value is the same expression as in
-// k_tv_prep / k_tv_deriv1 / k_tv_deriv2: same bits, t / It / Ix / Iy never go through memory.
+// ---- prep + derivatives in one launch: image_warp and get_derivatives' t / It (opticalflow_aux.c:31-132) on a
+// row-major tile with a 4-pixel halo in LDS, the first derivatives Ix, Iy of t on the tile with a 2-pixel halo, then
+// per core pixel the remaining 5-tap filters (Ixz, Iyz of It; Ixx, Ixy of Ix; Iyy of Iy) straight from LDS and every
+// plane written in skewed order (threads walk the tile's anti-diagonals: contiguous skewed rows).  A halo position
+// outside the level holds the value of the clamped position, which is exactly the filters' replicate border; every
+// value is the same expression as in k_tv_prep / k_tv_deriv1 / k_tv_deriv2: same bits, t / It / Ix / Iy never go
+// through memory.  Colour images (NOC 3, color_image_convolve_hv filters every channel alike: image.cpp:737-760) run
+// the three phases once per channel on the same LDS tiles (the warp positions are recomputed per channel: cheap),
+// writing that channel's eight planes.
 constexpr int kPdW = 64, kPdH = 16;
+template <int NOC>
 __global__ __launch_bounds__(256) void k_tv_prepd(TvArgs a) {
   const uint3 xb = xcd_block();
   constexpr int H4 = kPdH + 8, W4 = kPdW + 8, H2 = kPdH + 4, W2 = kPdW + 4;
   __shared__ float T[H4][W4], DT[H4][W4], IX[H2][W2], IY[H2][W2], WX[kPdH][kPdW], WY[kPdH][kPdW];
   const int x0 = xb.x * kPdW, y0 = xb.y * kPdH, f = xb.z;
   const int w = a.w, h = a.h;
-  // phase A: t, It at every halo-4 position (the clamped pixel's values), the flow of the core
-  for (int i = threadIdx.x; i < H4 * W4; i += 256) {
-    const int ly = i / W4, lx = i - ly * W4;
-    const int xx = x0 - 4 + lx, yy = y0 - 4 + ly;
-    const int cx = clampi(xx, 0, w - 1), cy = clampi(yy, 0, h - 1);
-    float v[5];
-    tv_prep_values(a, cx, cy, f, v);
-    T[ly][lx] = v[3];
-    DT[ly][lx] = v[4];
-    const int cxl = lx - 4, cyl = ly - 4;
-    if (cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < kPdH) {
-      WX[cyl][cxl] = v[1];
-      WY[cyl][cxl] = v[2];
+#pragma unroll 1
+  for (int ch = 0; ch < NOC; ++ch) {
+    if (ch > 0) __syncthreads();  // the previous channel's phase C has read the tiles
+    // phase A: t, It at every halo-4 position (the clamped pixel's values), the flow of the core
+    for (int i = threadIdx.x; i < H4 * W4; i += 256) {
+      const int ly = i / W4, lx = i - ly * W4;
+      const int xx = x0 - 4 + lx, yy = y0 - 4 + ly;
+      const int cx = clampi(xx, 0, w - 1), cy = clampi(yy, 0, h - 1);
+      float v[3 + 2 * NOC];
+      tv_prep_values(a, cx, cy, f, v);
+      T[ly][lx] = v[3 + ch];
+      DT[ly][lx] = v[3 + NOC + ch];
+      const int cxl = lx - 4, cyl = ly - 4;
+      if (ch == 0 && cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < kPdH) {
+        WX[cyl][cxl] = v[1];
+        WY[cyl][cxl] = v[2];
+      }
     }
-  }
-  __syncthreads();
-  // phase B: Ix, Iy at every halo-2 position (of the clamped pixel): conv5h / conv5v of t
-  for (int i = threadIdx.x; i < H2 * W2; i += 256) {
-    const int ly = i / W2, lx = i - ly * W2;
-    const int cx = clampi(x0 - 2 + lx, 0, w - 1), cy = clampi(y0 - 2 + ly, 0, h - 1);
-    const int tx = cx - x0 + 4, ty = cy - y0 + 4;  // the clamped pixel in T (within the halo)
-    IX[ly][lx] = kK5[0] * T[ty][tx - 2] + ((kK5[1] * T[ty][tx - 1] + kK5[2] * T[ty][tx]) +
-                                          (kK5[3] * T[ty][tx + 1] + kK5[4] * T[ty][tx + 2]));
-    IY[ly][lx] = kK5[0] * T[ty - 2][tx] + ((kK5[1] * T[ty - 1][tx] + kK5[2] * T[ty][tx]) +
-                                          (kK5[3] * T[ty + 1][tx] + kK5[4] * T[ty + 2][tx]));
-  }
-  __syncthreads();
-  // phase C: the core pixels in anti-diagonal order
-  constexpr int TD = kPdW + kPdH - 1;
-  for (int i = threadIdx.x; i < TD * kPdH; i += 256) {
-    const int yy = i & (kPdH - 1), dd = i / kPdH, xl = dd - yy;
-    const int x = x0 + xl, y = y0 + yy;
-    if (xl < 0 || xl >= kPdW || x >= w || y >= h) continue;
-    const int tx = xl + 4, ty = yy + 4, ix = xl + 2, iy = yy + 2;
-    const float ixz = kK5[0] * DT[ty][tx - 2] + ((kK5[1] * DT[ty][tx - 1] + kK5[2] * DT[ty][tx]) +
-                                               (kK5[3] * DT[ty][tx + 1] + kK5[4] * DT[ty][tx + 2]));
-    const float iyz = kK5[0] * DT[ty - 2][tx] + ((kK5[1] * DT[ty - 1][tx] + kK5[2] * DT[ty][tx]) +
-                                               (kK5[3] * DT[ty + 1][tx] + kK5[4] * DT[ty + 2][tx]));
-    const float ixx = kK5[0] * IX[iy][ix - 2] + ((kK5[1] * IX[iy][ix - 1] + kK5[2] * IX[iy][ix]) +
-                                               (kK5[3] * IX[iy][ix + 1] + kK5[4] * IX[iy][ix + 2]));
-    const float ixy = kK5[0] * IX[iy - 2][ix] + ((kK5[1] * IX[iy - 1][ix] + kK5[2] * IX[iy][ix]) +
-                                               (kK5[3] * IX[iy + 1][ix] + kK5[4] * IX[iy + 2][ix]));
-    const float iyy = kK5[0] * IY[iy - 2][ix] + ((kK5[1] * IY[iy - 1][ix] + kK5[2] * IY[iy][ix]) +
-                                               (kK5[3] * IY[iy + 1][ix] + kK5[4] * IY[iy + 2][ix]));
-    const long k = (long)f * a.sp + skw(x, y, h, w, a.wrap);
-    a.wxs[k] = WX[yy][xl];
-    a.du[k] = 0.0f;
-    if (a.nop == 2) {
-      a.wys[k] = WY[yy][xl];
-      a.dv[k] = 0.0f;
+    __syncthreads();
+    // phase B: Ix, Iy at every halo-2 position (of the clamped pixel): conv5h / conv5v of t
+    for (int i = threadIdx.x; i < H2 * W2; i += 256) {
+      const int ly = i / W2, lx = i - ly * W2;
+      const int cx = clampi(x0 - 2 + lx, 0, w - 1), cy = clampi(y0 - 2 + ly, 0, h - 1);
+      const int tx = cx - x0 + 4, ty = cy - y0 + 4;  // the clamped pixel in T (within the halo)
+      IX[ly][lx] = kK5[0] * T[ty][tx - 2] + ((kK5[1] * T[ty][tx - 1] + kK5[2] * T[ty][tx]) +
+                                            (kK5[3] * T[ty][tx + 1] + kK5[4] * T[ty][tx + 2]));
+      IY[ly][lx] = kK5[0] * T[ty - 2][tx] + ((kK5[1] * T[ty - 1][tx] + kK5[2] * T[ty][tx]) +
+                                            (kK5[3] * T[ty + 1][tx] + kK5[4] * T[ty + 2][tx]));
     }
-    a.Iz[k] = DT[ty][tx];
-    a.Ix[k] = IX[iy][ix];
-    a.Iy[k] = IY[iy][ix];
-    if (a.smsys_deriv) continue;  // the system kernel filters Ix, Iy, Iz itself
-    a.Ixx[k] = ixx;
-    a.Ixy[k] = ixy;
-    a.Iyy[k] = iyy;
-    a.Ixz[k] = ixz;
-    a.Iyz[k] = iyz;
+    __syncthreads();
+    // phase C: the core pixels in anti-diagonal order
+    constexpr int TD = kPdW + kPdH - 1;
+    for (int i = threadIdx.x; i < TD * kPdH; i += 256) {
+      const int yy = i & (kPdH - 1), dd = i / kPdH, xl = dd - yy;
+      const int x = x0 + xl, y = y0 + yy;
+      if (xl < 0 || xl >= kPdW || x >= w || y >= h) continue;
+      const int tx = xl + 4, ty = yy + 4, ix = xl + 2, iy = yy + 2;
+      const float ixz = kK5[0] * DT[ty][tx - 2] + ((kK5[1] * DT[ty][tx - 1] + kK5[2] * DT[ty][tx]) +
+                                                 (kK5[3] * DT[ty][tx + 1] + kK5[4] * DT[ty][tx + 2]));
+      const float iyz = kK5[0] * DT[ty - 2][tx] + ((kK5[1] * DT[ty - 1][tx] + kK5[2] * DT[ty][tx]) +
+                                                 (kK5[3] * DT[ty + 1][tx] + kK5[4] * DT[ty + 2][tx]));
+      const float ixx = kK5[0] * IX[iy][ix - 2] + ((kK5[1] * IX[iy][ix - 1] + kK5[2] * IX[iy][ix]) +
+                                                 (kK5[3] * IX[iy][ix + 1] + kK5[4] * IX[iy][ix + 2]));
+      const float ixy = kK5[0] * IX[iy - 2][ix] + ((kK5[1] * IX[iy - 1][ix] + kK5[2] * IX[iy][ix]) +
+                                                 (kK5[3] * IX[iy + 1][ix] + kK5[4] * IX[iy + 2][ix]));
+      const float iyy = kK5[0] * IY[iy - 2][ix] + ((kK5[1] * IY[iy - 1][ix] + kK5[2] * IY[iy][ix]) +
+                                                 (kK5[3] * IY[iy + 1][ix] + kK5[4] * IY[iy + 2][ix]));
+      const long sk = skw(x, y, h, w, a.wrap), k = (long)f * a.sp + sk;
+      if (ch == 0) {
+        a.wxs[k] = WX[yy][xl];
+        a.du[k] = 0.0f;
+        if (a.nop == 2) {
+          a.wys[k] = WY[yy][xl];
+          a.dv[k] = 0.0f;
+        }
+      }
+      const long q = ((long)f * NOC + ch) * a.sp + sk;
+      a.Iz[q] = DT[ty][tx];
+      a.Ix[q] = IX[iy][ix];
+      a.Iy[q] = IY[iy][ix];
+      if (a.smsys_deriv) continue;  // the system kernel filters Ix, Iy, Iz itself
+      a.Ixx[q] = ixx;
+      a.Ixy[q] = ixy;
+      a.Iyy[q] = iyy;
+      a.Ixz[q] = ixz;
+      a.Iyz[q] = iyz;
+    }
   }
 }
 
@@ -4711,9 +4721,12 @@ void launch_tv_prep(const TvArgs &a, hipStream_t s) {
   else
     k_tv_prep<9, 16><<<dim3(ceil_div(a.w, kTileW), ceil_div(a.h, 16), a.n), 256, 0, s>>>(a);
 }
-bool tv_prepd_ok(const TvArgs &a) { return a.prepd && a.noc == 1; }
+// prep + derivatives in one launch: intensity images (option prepd), colour images too with prepd = 2 (default)
+bool tv_prepd_ok(const TvArgs &a) { return a.prepd && (a.noc == 1 || a.prepd == 2); }
 void launch_tv_prepd(const TvArgs &a, hipStream_t s) {
-  k_tv_prepd<<<dim3(ceil_div(a.w, kPdW), ceil_div(a.h, kPdH), a.n), 256, 0, s>>>(a);
+  const dim3 grid(ceil_div(a.w, kPdW), ceil_div(a.h, kPdH), a.n);
+  if (a.noc == 1) k_tv_prepd<1><<<grid, 256, 0, s>>>(a);
+  else k_tv_prepd<3><<<grid, 256, 0, s>>>(a);
 }
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
   k_tv_deriv1<<<dim3(ceil_div(a.sp, 256), a.n * a.noc), 256, 0, s>>>(a);

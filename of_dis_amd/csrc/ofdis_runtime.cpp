@@ -96,7 +96,7 @@ struct ofdis_context {
                                // launches where they fit more frames per CU; the in-frame load select in launches
                                // that oversubscribe the chip), 3: always 28-byte + select, 4: always 32-byte +
                                // select, 1: workgroup limit)
-  int opt_prepd = 1;           // prep + derivatives in one launch for intensity images (0: three launches, A/B)
+  int opt_prepd = 2;           // prep + derivatives in one launch: 1 intensity images, 2 colour images too (0: three launches)
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
@@ -1300,7 +1300,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_prefetch", &ofdis_context::opt_smsys_prefetch, 0, 1},
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
-      {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 1},
+      {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},

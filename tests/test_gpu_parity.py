@@ -123,7 +123,8 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("smsys_deriv", 0, 1),     # fused launch reads all eight derivative planes (prepd writes them)
     ("smsys_march", 0, 1),     # tall levels: the 2-D tiled fused launch (smsys2d auto: on below 512 pairs)
     (("smsys_march", "smsys2d"), (0, 0), (1, 2)),  # tall levels: two launches (smoothness, then system)
-    ("prepd", 0, 1),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
+    ("prepd", 0, 2),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
+    ("prepd", 1, 2),           # ... three launches for colour images only
     ("patch_generic", 1, 0),   # every patch shape on the any-shape kernel k_patchg
     ("patch_quad", 0, 1),      # gray p = 8 / 12 on eight lanes per patch (k_patchw) instead of four (k_patchq)
     ("patch_x16", 0, 1),       # RGB p = 12 on eight lanes per patch (k_patchw) instead of sixteen (k_patchx)
