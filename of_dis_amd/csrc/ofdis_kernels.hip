@@ -2607,6 +2607,28 @@ __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, in
   }
 #undef SB
 }
+// The same for channel ch alone: t, It of that channel, the flow (tv_prep_values' expressions: same bits).
+__device__ __forceinline__ void tv_prep_values_ch(const TvArgs &a, int x, int y, int f, int ch, float &t, float &it,
+                                                  float &wx, float &wy) {
+  const long plane = (long)a.w * a.h;
+  const long o = (long)y * a.w + x;
+  wx = a.flow[(long)f * a.nop * plane + o];
+  wy = a.nop == 2 ? a.flow[(long)f * a.nop * plane + plane + o] : 0.0f;
+  const float xx = (float)x + wx, yy = (float)y + wy;
+  const int xi = (int)floorf(xx), yi = (int)floorf(yy);
+  const float dx = xx - (float)xi, dy = yy - (float)yi;
+  const int x1 = clampi(xi, 0, a.w - 1), x2 = clampi(xi + 1, 0, a.w - 1);
+  const int y1 = clampi(yi, 0, a.h - 1), y2 = clampi(yi + 1, 0, a.h - 1);
+  const long fs = (long)a.W * (a.h + 2 * a.pad) * a.noc;
+  const float *B = a.img_b + f * fs, *A = a.img_a + f * fs;
+#define SB(xq, yq) B[((long)((yq) + a.pad) * a.W + (xq) + a.pad) * a.noc + ch]
+  const float w2 = SB(x1, y1) * (1.0f - dx) * (1.0f - dy) + SB(x2, y1) * dx * (1.0f - dy) +
+                   SB(x1, y2) * (1.0f - dx) * dy + SB(x2, y2) * dx * dy;
+#undef SB
+  const float i1 = A[((long)(y + a.pad) * a.W + x + a.pad) * a.noc + ch];
+  t = 0.5f * (w2 + i1);
+  it = w2 - i1;
+}
 // The values of pixel (x, y) into the skewed planes (du = dv = 0: the increment starts at zero).  The mask
 // is not stored: it is a function of (x, y, wx, wy), which the system kernels recompute (warp_mask) from the
 // skewed flow copies they read anyway -- 4 bytes per pixel and inner iteration less.
@@ -2700,14 +2722,14 @@ __global__ __launch_bounds__(256) void k_tv_prepd(TvArgs a) {
       const int ly = i / W4, lx = i - ly * W4;
       const int xx = x0 - 4 + lx, yy = y0 - 4 + ly;
       const int cx = clampi(xx, 0, w - 1), cy = clampi(yy, 0, h - 1);
-      float v[3 + 2 * NOC];
-      tv_prep_values(a, cx, cy, f, v);
-      T[ly][lx] = v[3 + ch];
-      DT[ly][lx] = v[3 + NOC + ch];
+      float t, it, wx, wy;
+      tv_prep_values_ch(a, cx, cy, f, ch, t, it, wx, wy);
+      T[ly][lx] = t;
+      DT[ly][lx] = it;
       const int cxl = lx - 4, cyl = ly - 4;
       if (ch == 0 && cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < kPdH) {
-        WX[cyl][cxl] = v[1];
-        WY[cyl][cxl] = v[2];
+        WX[cyl][cxl] = wx;
+        WY[cyl][cxl] = wy;
       }
     }
     __syncthreads();
