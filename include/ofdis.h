@@ -225,6 +225,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        hand-overs, L + 1 workspaces);
  *   "split_cus" (0..7, default 0): pipeline: the streaming stream runs on that many eighths of the CUs (a CU-masked
  *                        stream; the eighths spread evenly over the XCDs), 0 = all CUs;
+ *   "stagger" (0/1, default 0): round robin over several streams: chunk ch's DIS + TV chain starts only after
+ *                        chunk ch - 1's, so chains never share the GPU while each overlaps the other streams' pyramid
+ *                        and upsample;
  *   "chain_cus" (0..8, default 0): pipeline: the chain lanes run on the last that many eighths (complementary to
  *                        "split_cus" when the two add up to 8), 0 or 8 = all CUs.
  * Setting any option drops the captured graph.  Unknown keys and out-of-range values return

@@ -118,6 +118,7 @@ struct ofdis_context {
                                      // chain lanes (DIS + TV), chunk ch on chain lane ch % L (0: off)
   int opt_split_cus = 0;             // pipeline: the streaming stream on this many eighths of the CUs (0: all)
   int opt_chain_cus = 0;             // pipeline: the chain lanes on the complementary eighths (0: all CUs)
+  int opt_stagger = 0;               // round robin: chunk ch's chain starts after chunk ch - 1's
   std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
     hipStream_t s = nullptr;
@@ -792,12 +793,16 @@ int run_init(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, c
 }
 
 // One chunk of frames through the whole pipeline on stream s with workspace ws.
+// chain_wait / chain_done (optional): an event the chain (run_levels) waits for first / is recorded after it.
 int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
-              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s) {
+              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s,
+              hipEvent_t chain_wait = nullptr, hipEvent_t chain_done = nullptr) {
   int rc = run_pyramid(c, ws, P, img_a, img_b, s);
   if (rc) return rc;
   if (init && (rc = run_init(c, ws, P, p, init, s))) return rc;
+  if (chain_wait) HIP_OK(hipStreamWaitEvent(s, chain_wait, 0));
   rc = run_levels(c, ws, P, p, s, init ? (const float *)(ws + P.off_init) : nullptr, nullptr);
+  if (chain_done) HIP_OK(hipEventRecord(chain_done, s));
   if (rc) return rc;
   return run_upsample(c, ws, P, p, flow_out, s);
 }
@@ -929,7 +934,7 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
   }  // round robin: unmasked lanes (a lane a pipeline call masked gets a new stream)
   int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total, &masks);
   if (rc) return rc;
-  if (cp.kind == CallPlan::kPipeline)
+  if (cp.kind == CallPlan::kPipeline || c->opt_stagger)
     while ((int)c->pipe_ev.size() < 2 * cp.nchunks) {
       hipEvent_t e = nullptr;
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -946,11 +951,15 @@ int issue_round_robin(ofdis_context *c, const CallPlan &cp, hipStream_t s, const
   for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
   const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
   const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
+  // stagger: chunk ch's chain (DIS + TV levels) starts only after chunk ch - 1's, so the chains never share the
+  // GPU while each overlaps the other lanes' streaming stages (pyramid, upsample)
+  hipEvent_t *ev_chain = c->opt_stagger && k > 1 ? c->pipe_ev.data() : nullptr;
   for (int ch = 0; ch < cp.nchunks; ++ch) {
     const size_t f0 = (size_t)ch * cp.chunk;
     auto &L = c->lanes[ch % k];
     int rc = run_chunk(c, L.ws, cp.parts[ch], p, img_a + f0 * in_frame, img_b + f0 * in_frame,
-                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s);
+                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s,
+                       ev_chain && ch > 0 ? ev_chain[ch - 1] : nullptr, ev_chain ? ev_chain[ch] : nullptr);
     if (rc) return rc;
   }
   for (int i = 0; i < k; ++i) {
@@ -1293,7 +1302,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   };
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 4},     {"split_cus", &ofdis_context::opt_split_cus, 0, 7},
-      {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
+      {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},   {"stagger", &ofdis_context::opt_stagger, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},
