@@ -168,8 +168,6 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "sor_rows2" (0/1, default 1): levels too tall for one row per lane in a 1024-thread workgroup run the
  *                        sweep-per-wave SOR with two rows per lane -- 321..640 rows at 3 sweeps, 513..1024 at
  *                        2 (else the register pipeline);
- *   "sor_half" (0/1, default 0): levels of 65..128 rows run the sweep-per-wave SOR with two rows per lane, lane y
- *                        running rows y and y + HS (HS ~ h / 2): one wave per sweep instead of two row groups;
  *   "smsys" (0/1, default 1): smoothness and system of a TV iteration in one launch;
  *   "smsys2d" (0/1/2, default 2): the fused launch on 2-D tiles for levels taller than 256 rows (0: two
  *                        launches there; 2 = automatic: on for calls of fewer than 512 pairs);

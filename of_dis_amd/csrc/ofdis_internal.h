@@ -118,7 +118,6 @@ struct TvArgs {
   int sor_cring;               // lean SOR: coefficients loaded once by sweep 0, passed on through LDS (S <= 3);
                                // 2: the ring sized to the level's row groups
   int sor_rows2;               // lean SOR with two rows per lane for levels of 321..640 rows (else the pipeline)
-  int sor_half;                // lean SOR of 65..128-row levels on two rows per lane split at ~h / 2 (one row group)
   int smsys;                   // smoothness + system in one launch (k_tv_smsys)
   int prepd;                   // prep + derivatives in one launch (k_tv_prepd, intensity images; 0: three launches)
   int smsys2d;                 // ... and on 2-D tiles for tall levels (k_tv_smsys2d; 0: two launches there, A/B)

@@ -3941,13 +3941,8 @@ __device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
 // the ring), so R = 2 runs levels of up to 640 rows with S <= 3 in 16 waves (E's 544-row level) where R = 1
 // would need 27.  Every per-row ring / coefficient-ring offset is a compile-time multiple of 64 entries.
 // SEL: load form of the lanes outside the frame (see load()).
-// HS < 64 (R = 2, one row group, levels of 65 .. 2 HS rows): lane y < HS runs rows y and y + HS -- every lane's two
-// rows real for h near 2 HS, where the 64-row split left the second group's wave 4 real rows of 64 at B's 68-row level
-// (half the sweep waves idle, 6 waves per frame instead of 3).  Lanes y >= HS run the dump row 2 HS (outside the
-// level) twice; the rings hold 2 HS + 3 entries (row -1, rows 0 .. 2 HS - 1, the dump row and its lower neighbour).
-template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool CZ = false, bool SEL = false, int HS = 64>
+template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool CZ = false, bool SEL = false>
 struct SorLane {
-  static_assert(HS == 64 || R == 2, "half split: two rows per lane");
   static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
   static_assert(CRN == 0 || S <= 3, "coefficient ring depth 6 needs S <= 3");
   static constexpr int PD = NB - 1;                                    // prefetch distance (steps)
@@ -3991,19 +3986,9 @@ struct SorLane {
   int w, h, y, s, lim, rmax, hplane;
   bool border[R], notop[R];
   float omega;
-  int yh1;  // HS < 64: the lane's second row (y + HS, or the dump row 2 HS twice for y >= HS: then y is 2 HS too)
 #ifdef OFDIS_SOR_PROBE
   unsigned *probe = nullptr;  // this wave's [step][4] records (frame 0 only)
 #endif
-  // row r of this lane, and its ring entry offset from the lane's base entry (a compile-time 64 r in the 64 split)
-  __device__ __forceinline__ int yrow(int r) const {
-    if constexpr (HS == 64) return y + 64 * r;
-    else return r == 0 ? y : yh1;
-  }
-  __device__ __forceinline__ int roff(int r) const {
-    if constexpr (HS == 64) return 64 * r;
-    else return r == 0 ? 0 : yh1 - y;
-  }
 
   __device__ __forceinline__ void load(int t, Ld &B) {
     const int d = t - 2 * s;
@@ -4020,8 +4005,8 @@ struct SorLane {
       // launch).  !SEL (launches whose frames all fit the chip -- the latency regime): the lane-constant slot y + 64 r,
       // no per-step vector address arithmetic on the step's critical path (the select cost the single pair's 18 SOR
       // launches 0.50 -> 0.58 ms); its extra lines cost nothing when the chip is not full.
-      const unsigned yr = SEL ? (((unsigned)(d - yrow(r)) < (unsigned)w && yrow(r) < h) ? (unsigned)yrow(r) : 0u)
-                              : (unsigned)yrow(r);
+      const unsigned yr = SEL ? (((unsigned)(d - (y + 64 * r)) < (unsigned)w && y + 64 * r < h) ? (unsigned)(y + 64 * r) : 0u)
+                              : (unsigned)(y + 64 * r);
       if (FIRST || CRN == 0) {
         const float4 *cp = C + (size_t)r0 * CW;
         B.c0[r] = cp[yr * CW];
@@ -4054,15 +4039,15 @@ struct SorLane {
     const int d = t - 2 * s;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int RO = roff(r) * 3;  // ring entries of the lane's row r from its base entry, in f2v / float
-      const int yr = yrow(r);
+      constexpr int RO = 64 * 3;  // ring entries of the row 64 below, in f2v / float
+      const int yr = y + 64 * r;
       const int xp = d - yr;
       const bool hasl = xp > 0, hasr = xp < w - 1;
       f2v o, rgt, bt;
       if (FIRST) {
         o = B.o[r]; rgt = Bn.o[r]; bt = B.b[r];
       } else {  // own value after the previous sweep (step t-2) = the right neighbour read at step t-1
-        o = prv[r]; rgt = ring_p[RO + m1]; bt = ring_p[RO + 3 + m1];
+        o = prv[r]; rgt = ring_p[r * RO + m1]; bt = ring_p[r * RO + 3 + m1];
         prv[r] = rgt;
       }
       // coefficients of this pixel and sv of the one above (entry 0, row -1, stays zero)
@@ -4073,21 +4058,21 @@ struct SorLane {
           c0 = B.c0[r];
           c1 = MODE == 0 ? B.c1[r] : B.c0[r];
           if constexpr (MODE == 0 && CZ) {
-            cr[cs * CRN + roff(r)] = make_float4(c0.x, c0.y, c0.w, c1.z);
-            cr2[cs * CRN + roff(r)] = f2v{c1.x, c1.y};
-            crv[cs * CRN + roff(r)] = c1.w;
+            cr[cs * CRN + 64 * r] = make_float4(c0.x, c0.y, c0.w, c1.z);
+            cr2[cs * CRN + 64 * r] = f2v{c1.x, c1.y};
+            crv[cs * CRN + 64 * r] = c1.w;
           } else {
-            cr[cs * CW * CRN + roff(r)] = c0;
-            if (MODE == 0) cr[(cs * CW + 1) * CRN + roff(r)] = c1;
+            cr[cs * CW * CRN + 64 * r] = c0;
+            if (MODE == 0) cr[(cs * CW + 1) * CRN + 64 * r] = c1;
           }
         } else if constexpr (MODE == 0 && CZ) {
-          const float4 q = cr[cs * CRN + roff(r)];
-          const f2v bq = cr2[cs * CRN + roff(r)];
+          const float4 q = cr[cs * CRN + 64 * r];
+          const f2v bq = cr2[cs * CRN + 64 * r];
           c0 = make_float4(q.x, q.y, q.y, q.z);
-          c1 = make_float4(bq.x, bq.y, q.w, crv[cs * CRN + roff(r)]);
+          c1 = make_float4(bq.x, bq.y, q.w, crv[cs * CRN + 64 * r]);
         } else {
-          c0 = cr[cs * CW * CRN + roff(r)];
-          c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN + roff(r)] : c0;
+          c0 = cr[cs * CW * CRN + 64 * r];
+          c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN + 64 * r] : c0;
         }
       } else {
         c0 = B.c0[r];
@@ -4100,12 +4085,12 @@ struct SorLane {
         tp = f2v{dpp_from_prev_lane(pp[r].x), MODE == 0 ? dpp_from_prev_lane(pp[r].y) : 0.0f};
         tsv = dpp_from_prev_lane(pvv[r]);
         if (top_lds) {
-          tp = ring_s[RO + m1 - 3];
-          tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + roff(r)] : cr[(ct * CW + CW - 1) * CRN - 1 + roff(r)].w) : sv_s[RO + m1 - 3];
+          tp = ring_s[r * RO + m1 - 3];
+          tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + 64 * r] : cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w) : sv_s[r * RO + m1 - 3];
         }
       } else {
-        tp = ring_s[RO + m1 - 3];
-        tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + roff(r)] : cr[(ct * CW + CW - 1) * CRN - 1 + roff(r)].w) : sv_s[RO + m1 - 3];
+        tp = ring_s[r * RO + m1 - 3];
+        tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + 64 * r] : cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w) : sv_s[r * RO + m1 - 3];
       }
       f2v nw;
       float vv;
@@ -4144,8 +4129,8 @@ struct SorLane {
         nw = f2v{(1.0f - omega) * o.x + omega * (Bq / A), 0.0f};
         phr[r] = hr;
       }
-      ring_s[RO + m0] = nw;
-      if (CRN == 0) sv_s[RO + m0] = vv;
+      ring_s[r * RO + m0] = nw;
+      if (CRN == 0) sv_s[r * RO + m0] = vv;
       pvv[r] = vv;
       if (LAST) {
         if ((unsigned)xp < (unsigned)w && yr < h) {
@@ -4193,7 +4178,7 @@ struct SorLane {
     // the previous sweep's value at step ta - 2 (written before the barrier of step ta - 1; zero before t = 0)
     if (!FIRST) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) prv[r] = ta >= 2 ? ring_p[roff(r) * 3 + (ta - 2) % 3] : f2v{0.0f, 0.0f};
+      for (int r = 0; r < R; ++r) prv[r] = ta >= 2 ? ring_p[64 * 3 * r + (ta - 2) % 3] : f2v{0.0f, 0.0f};
     }
     prologue<0>(ta);
     for (int t = ta; t < tb; t += U) block<0>(t);
@@ -4229,23 +4214,19 @@ __host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
 __host__ __device__ __forceinline__ size_t sor_cring_bytes(int crn, int cw, bool cz = false) {
   return (size_t)6 * crn * (cw == 2 ? (cz ? 28 : 32) : 16);
 }
-// (u, v) ring entries of a level: 64 R G + 2, or 2 HS + 3 in the half split (HS < 64)
-__host__ __device__ __forceinline__ int sor_nr(int h, int R, int HS) {
-  return HS < 64 ? 2 * HS + 3 : (h + 64 * R - 1) / (64 * R) * 64 * R + 2;
-}
-__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1, bool cz = false,
-                                                       int HS = 64) {
-  const size_t nr = (size_t)sor_nr(h, R, HS);
+__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1, bool cz = false) {
+  const size_t nr = (size_t)((h + 64 * R - 1) / (64 * R)) * 64 * R + 2;
   const size_t uv = sizeof(float) * 2 * 3 * (size_t)S * nr;
   if (crn == 0) return uv + sizeof(float) * 3 * (size_t)S * nr;
   return (uv + 15) / 16 * 16 + sor_cring_bytes(crn, cw, cz);
 }
 
-// One frame's SOR call, lean form: 64 * G * S threads, R rows per lane (HS < 64: the half split, G = 1).
-template <int S, int MODE, int NB, int CRN, int R, bool CZ = false, bool SEL = false, int HS = 64>
+// One frame's SOR call, lean form: 64 * G * S threads, R rows per lane.
+template <int S, int MODE, int NB, int CRN, int R, bool CZ = false, bool SEL = false>
 __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
   constexpr int CW = MODE == 0 ? 2 : 1;
-  const int NR = sor_nr(a.h, R, HS);
+  const int G = (a.h + 64 * R - 1) / (64 * R);
+  const int NR = G * 64 * R + 2;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = wid / S, s = wid - g * S;
   float *svr = reinterpret_cast<float *>(ring + S * 3 * NR);
@@ -4277,9 +4258,7 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.dv_r = a.dv + fo;
     st.du = a.du + fo;
     st.dv = a.dv + fo;
-    // half split: lane y < HS runs rows y and y + HS; the others the dump row 2 HS (twice)
-    const int y = HS < 64 ? (lane < HS ? lane : 2 * HS) : y0 + lane;
-    st.yh1 = HS < 64 ? (lane < HS ? lane + HS : 2 * HS) : 0;
+    const int y = y0 + lane;
     st.ring_s = ring + (s * NR + y + 1) * 3;
     st.ring_p = ring + ((s > 0 ? s - 1 : 0) * NR + y + 1) * 3;
     st.sv_s = svr + (s * NR + y + 1) * 3;
@@ -4293,7 +4272,7 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.top_lds = lane == 0 && y0 > 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int yr = st.yrow(r);
+      const int yr = y + 64 * r;
       st.notop[r] = yr == 0;
       st.border[r] = yr == 0 || yr >= a.h - 1;
     }
@@ -4305,38 +4284,28 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.run(T, y0, ymax);
   };
   if (s == 0) {
-    SorLane<S, MODE, 0, NB, CRN, R, CZ, SEL, HS> st;
+    SorLane<S, MODE, 0, NB, CRN, R, CZ, SEL> st;
     setup(st);
   } else if (s == 1) {
-    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, CZ, SEL, HS> st;
+    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, CZ, SEL> st;
     setup(st);
   } else if (s == 2) {
-    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, CZ, SEL, HS> st;
+    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, CZ, SEL> st;
     setup(st);
   } else {
-    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, CZ, SEL, HS> st;
+    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, CZ, SEL> st;
     setup(st);
   }
 }
 
 // CG > 0: the coefficient ring holds exactly the CG row groups of the level (+ 2 halos) instead of the most a
 // workgroup of MAXT threads can hold -- less LDS per frame, more frames per CU.
-template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool CZ = false, bool SEL = false,
-          int HS = 64>
+template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool CZ = false, bool SEL = false>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
-  constexpr int crn = !CRING ? 0 : HS < 64 ? 2 * HS + 3 : CG > 0 ? 64 * R * CG + 2 : sor_crn(S, MAXT, R);
+  constexpr int crn = !CRING ? 0 : CG > 0 ? 64 * R * CG + 2 : sor_crn(S, MAXT, R);
   static_assert(CG == 0 || CG * 64 * S <= MAXT, "row groups of the workgroup");
-  static_assert(HS == 64, "the half split runs k_tv_sor_half");
-  sor_lanes_frame<S, MODE, NB, crn, R, CZ, SEL, HS>(a, blockIdx.x, ring_uv);
-}
-// The half split (R = 2, one row group of S waves): registers pinned for eight frames per CU (six waves per SIMD),
-// which its LDS (~20 KB per frame at B's 68-row level) allows.
-// Sweep 0 prefetches one step ahead (NB = 2): two rows' coefficient buffers of three steps did not fit 80 VGPRs.
-template <int S, int MODE, bool CZ, bool SEL, int HS>
-__global__ __launch_bounds__(64 * S) __attribute__((amdgpu_waves_per_eu(6))) void k_tv_sor_half(TvArgs a) {
-  extern __shared__ f2v ring_uv[];
-  sor_lanes_frame<S, MODE, 2, 2 * HS + 3, 2, CZ, SEL, HS>(a, blockIdx.x, ring_uv);
+  sor_lanes_frame<S, MODE, NB, crn, R, CZ, SEL>(a, blockIdx.x, ring_uv);
 }
 
 template <int TH>
@@ -4950,44 +4919,6 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
     else k_tv_sor_lanes<S, 2, 3, MAXT, false, R><<<a.n, th, lds, s>>>(a);
   }
 }
-// The half split (option sor_half): levels of 65 .. 128 rows on S waves of two rows per lane, lane y < HS running
-// rows y and y + HS (HS = ceil(h / 2) rounded up to a multiple of 8), the rings sized to 2 HS + 3 entries.  Same
-// ring protocol, same update, same bits as the 64-row split's two row groups -- half the waves and about half the
-// LDS per frame (B's 68-row level: 3 waves and 20 KB instead of 6 and 31 KB, 8 frames per CU instead of 5).
-template <int S, int HS>
-static void sor_half_hs(const TvArgs &a, hipStream_t s) {
-  const int cw = a.nop == 2 ? 2 : 1;
-  constexpr int crn = 2 * HS + 3;
-  const size_t ld32 = sor_lanes_lds(S, a.h, crn, cw, 2, false, HS), ld28 = sor_lanes_lds(S, a.h, crn, cw, 2, true, HS);
-  const long cus = device_cus(), f32 = sor_frames_per_cu(ld32, S), f28 = sor_frames_per_cu(ld28, S);
-  const bool cz = a.nop == 2 && (a.sor_cring == 3 || (a.sor_cring != 4 && f28 > f32 && (long)a.n > f32 * cus));
-  const bool sel = a.sor_cring >= 3 || (long)a.n > (cz ? f28 : f32) * cus;
-  const size_t lds = cz ? ld28 : ld32;
-  constexpr int th = 64 * S;
-  if (a.nop == 2) {
-    if (cz) {
-      if (sel) k_tv_sor_half<S, 0, true, true, HS><<<a.n, th, lds, s>>>(a);
-      else k_tv_sor_half<S, 0, true, false, HS><<<a.n, th, lds, s>>>(a);
-    } else {
-      if (sel) k_tv_sor_half<S, 0, false, true, HS><<<a.n, th, lds, s>>>(a);
-      else k_tv_sor_half<S, 0, false, false, HS><<<a.n, th, lds, s>>>(a);
-    }
-  } else {
-    if (sel) k_tv_sor_half<S, 2, false, true, HS><<<a.n, th, lds, s>>>(a);
-    else k_tv_sor_half<S, 2, false, false, HS><<<a.n, th, lds, s>>>(a);
-  }
-}
-template <int S>
-static void sor_half(const TvArgs &a, hipStream_t s) {
-  const int hs = ((a.h + 1) / 2 + 7) / 8 * 8;
-  if (hs <= 40) sor_half_hs<S, 40>(a, s);
-  else if (hs <= 48) sor_half_hs<S, 48>(a, s);
-  else if (hs <= 56) sor_half_hs<S, 56>(a, s);
-  else sor_half_hs<S, 64>(a, s);
-}
-bool sor_half_ok(const TvArgs &a) {
-  return a.sor_half && a.sor_cring >= 1 && a.h > 64 && a.h <= 128 && (a.solverit == 2 || a.solverit == 3);
-}
 template <int S>
 static void sor_lanes_s(const TvArgs &a, hipStream_t s) {
   if (64 * S * ((a.h + 63) / 64) <= 512)
@@ -5020,11 +4951,6 @@ void launch_tv_sor(const TvArgs &a, hipStream_t s) {
   }
   const int G = (a.h + 63) / 64, G2 = (a.h + 127) / 128;  // row groups at one / two rows per lane
   const bool lanes_fit = G * a.solverit <= 16 || (a.solverit <= 3 && G2 * a.solverit <= 16 && a.sor_rows2);
-  if (!tiny && !a.sor_generic && a.sor_variant != 1 && sor_half_ok(a)) {
-    if (a.solverit == 2) sor_half<2>(a, s);
-    else sor_half<3>(a, s);
-    return;
-  }
   if (!tiny && !a.sor_generic && a.sor_variant != 1 && a.solverit >= 2 && a.solverit <= 4 && lanes_fit) {
     switch (a.solverit) {
       case 2: sor_lanes_s<2>(a, s); return;

@@ -98,7 +98,6 @@ struct ofdis_context {
                                // select, 1: workgroup limit)
   int opt_prepd = 2;           // prep + derivatives in one launch: 1 intensity images, 2 colour images too (0: three launches)
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
-  int opt_sor_half = 0;        // sweep-per-wave SOR of 65..128-row levels: two rows per lane split at ~h / 2
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
   int opt_sysor = 0;           // levels <= 128 rows (optical flow, intensity images): smoothness + system + SOR of an
@@ -527,7 +526,6 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_variant = c->opt_sor_pipe;
       tv.sor_cring = c->opt_sor_cring;
       tv.sor_rows2 = c->opt_sor_rows2;
-      tv.sor_half = c->opt_sor_half;
       tv.smsys = c->opt_smsys;
       tv.smsys2d = c->opt_smsys2d == 2 ? c->call_frames < 512 : c->opt_smsys2d;
       tv.smsys_march = c->opt_smsys_march;
@@ -1304,7 +1302,6 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   };
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 4},     {"split_cus", &ofdis_context::opt_split_cus, 0, 7},
-      {"sor_half", &ofdis_context::opt_sor_half, 0, 1},
       {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},   {"stagger", &ofdis_context::opt_stagger, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},

@@ -118,7 +118,6 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_cring", 4, 2),       # 32-byte entries with the in-frame load select (the oversubscribed launches' loads)
     ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
-    ("sor_half", 1, 0),        # 65..128-row levels: two rows per lane split at ~h / 2 (one wave per sweep)
     ("smsys_prefetch", 0, 1),  # fused smoothness + system: derivative images loaded in phase 2
     ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)
     ("smsys_deriv", 0, 1),     # fused launch reads all eight derivative planes (prepd writes them)

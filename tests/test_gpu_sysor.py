@@ -101,46 +101,3 @@ def test_sysor_batch(oracle, od, ctx):
         assert_bitexact(out[i], ref, f"frame {i}")
     for f in range(nd, n):
         assert_bitexact(out[f], out[f % nd], f"frame {f}")
-
-
-@pytest.fixture(scope="module")
-def ctx_half(od):
-    c = od.Context(0)
-    c.set_option("sor_half", 1)
-    yield c
-    c.close()
-
-
-@pytest.mark.parametrize("w,h,noc,mode,op,over", SIZES + [(240, 120, 1, 2, 4, {"max_iter": 16, "min_iter": 16,
-                                                                              "sc_l": 0, "sc_f": 1})])
-def test_sor_half_bitexact(oracle, od, ctx_half, w, h, noc, mode, op, over):
-    """The half-split SOR (option sor_half: 65..128-row levels on two rows per lane, lane y running rows y and
-    y + HS) gives the oracle's bits at every size class, optical flow and depth."""
-    a, b = od.synth_pair(w, h, noc, 3, mode)
-    p, q = _params(od, oracle, w, noc, mode, op, over)
-    _run_capture(oracle, ctx_half, a, b, p, q)
-
-
-def test_sor_half_full_1080p_batch(oracle, od, ctx_half):
-    """B's 68-row level in a throughput launch (1200 pairs: more frames than the chip holds, the 28-byte ring and
-    the in-frame load select) and alone: every frame is the oracle's."""
-    import torch
-    w, h, n = 1920, 1080, 1200
-    pa, pb = od.synth_pair(w, h, 1, 9, 1)
-    p, q = _params(od, oracle, w, 1, 1, 2, {})
-    ref = oracle.run_u8(pa, pb, q)
-    assert_bitexact(ctx_half.run_host(pa, pb, p), ref, "single pair")
-    a = torch.from_numpy(pa).cuda().unsqueeze(0).expand(n, -1, -1, -1).contiguous()
-    b = torch.from_numpy(pb).cuda().unsqueeze(0).expand(n, -1, -1, -1).contiguous()
-    ctx_half.set_option("streams", 1)
-    try:
-        out = ctx_half.run(a, b, p)
-        torch.cuda.synchronize()
-    finally:
-        ctx_half.set_option("streams", 0)
-    assert_bitexact(out[0].cpu().numpy(), ref, "frame 0")
-    assert_bitexact(out[n - 1].cpu().numpy(), ref, "last frame")
-    ov = out.view(n, -1).view(torch.int32)
-    assert all(torch.equal(ov[f], ov[0]) for f in range(n))
-    del a, b, out, ov
-    torch.cuda.empty_cache()
