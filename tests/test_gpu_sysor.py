@@ -1,7 +1,7 @@
 """GPU parity of the fused system + SOR launch (option "sysor", k_tv_sysor in ofdis_tvsysor.hip).
 
 One launch per TV inner iteration of a level of at most 128 rows: compute_smoothness, compute_data, sub_laplacian
-and sor_coupled's inverse (FDF1.0.1/opticalflow_aux.c:138-223,408-594, solver.c:122-128) are produced three
+and sor_coupled's inverse (FDF1.0.1/opticalflow_aux.c:138-223,408-594, solver.c:122-128) are produced four
 anti-diagonals ahead of the exact-order SOR wavefront (solver.c:83-433) inside the same workgroup.  Same functions,
 same order: the bar is the oracle's bits, per scale and at full resolution, at every size class the kernel
 distinguishes (one or two row groups, h = 2 .. 128, folded and unfolded skew layouts, 2 and 3 sweeps, the first
