@@ -200,6 +200,9 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        of their loss weights, so the aggregation reads coalesced plane rows (0: loss weights);
  *   "patch_buf" (0/1, default 1): gray p = 12 patch windows by buffer loads with 32-bit offsets where the level's
  *                        image array spans less than 4 GiB (0: 64-bit address arithmetic per load);
+ *   "patch_fdiv" (0/1, default 1): the 2x2 / 1x1 LLT solves of every patch iteration divide by one correctly
+ *                        rounded reciprocal of each pivot per patch plus two FMAs (exact by Markstein's theorem in
+ *                        the range the kernels check; tools/divcheck_l.c), IEEE divisions outside it (0: IEEE always);
  *   "patch_generic" (0/1, default 0): every patch shape on the any-shape kernel (runtime value loops: the
  *                        default for p*p*noc > 448, e.g. RGB p >= 14, gray p >= 22);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;

@@ -76,7 +76,8 @@ struct PatchArgs {
                                               // can (launch_patch returns whether it did)
   int aslots;                                 // A = (p - 1) / steps + 1: slot planes per axis
   int buf32;                                  // the image array of the launch spans < 2^32 bytes (32-bit buffer offsets)
-  int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
+  int fdiv;                                   // 1: the LLT solves divide by FMA-corrected pivot reciprocals (llt_rcp)
+  int stage;                                 // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;
 };

@@ -329,6 +329,57 @@ __device__ __forceinline__ float llt1_solve(float L, float b) {
   return y / L;
 }
 
+// The solves' divisions by the patch's constant pivots, three instructions each instead of the IEEE
+// sequence (two v_div_scale, v_rcp, five FMAs, v_div_fmas, v_div_fixup): with y = RN(1/L) from one IEEE
+// division per patch, q0 = a y, r = fma(-q0, L, a) (exact), q = fma(r, y, q0) is RN(a / L) by Markstein's
+// theorem while nothing under- or overflows -- |L| in [2^-30, 2^30], |a| in [2^-60, 2^60] (every residual then
+// normal).  tools/divcheck_l.c checks it against IEEE a / L on 6.4e9 pairs of that range (0 mismatches; a
+// reciprocal one ulp off gives hundreds).  A lane with any numerator or pivot outside the range (zero, tiny,
+// huge, inf, NaN, a failed factorisation) repeats the whole solve with IEEE divisions in a wave-uniform branch.
+struct LltRcp {
+  float r00, r11;  // RN(1 / L00), RN(1 / L11) (NOP = 1: r00 = RN(1 / L))
+  bool ok;         // pivots in range and the fast form enabled
+};
+__device__ __forceinline__ bool mdiv_in(float a) { return fabsf(a) >= 0x1p-60f && fabsf(a) <= 0x1p60f; }
+__device__ __forceinline__ bool mdiv_pivot(float L) { return fabsf(L) >= 0x1p-30f && fabsf(L) <= 0x1p30f; }
+__device__ __forceinline__ float mdiv(float a, float L, float y) {
+  const float q0 = a * y;
+  const float r = __builtin_fmaf(-q0, L, a);
+  return __builtin_fmaf(r, y, q0);
+}
+template <int NOP>
+__device__ __forceinline__ LltRcp llt_rcp(const Llt2 &f, float L1, bool enable) {
+  LltRcp r;
+  if (NOP == 2) {
+    r.r00 = 1.0f / f.L00;
+    r.r11 = 1.0f / f.L11;
+    r.ok = enable && mdiv_pivot(f.L00) && mdiv_pivot(f.L11);
+  } else {
+    r.r00 = 1.0f / L1;
+    r.r11 = 0.0f;
+    r.ok = enable && mdiv_pivot(L1);
+  }
+  return r;
+}
+__device__ __forceinline__ void llt2_solve_fast(const Llt2 &f, const LltRcp &rc, float b0, float b1, float &x0,
+                                                float &x1) {
+  const float y0 = mdiv(b0, f.L00, rc.r00);
+  const float n1 = b1 - f.L10 * y0;
+  const float y1 = mdiv(n1, f.L11, rc.r11);
+  x1 = mdiv(y1, f.L11, rc.r11);
+  const float n3 = y0 - f.L10 * x1;
+  x0 = mdiv(n3, f.L00, rc.r00);
+  const bool slow = !(rc.ok && mdiv_in(b0) && mdiv_in(n1) && mdiv_in(y1) && mdiv_in(n3));
+  if (__builtin_amdgcn_ballot_w64(slow) != 0 && slow) llt2_solve(f, b0, b1, x0, x1);
+}
+__device__ __forceinline__ float llt1_solve_fast(float L, const LltRcp &rc, float b) {
+  const float y = mdiv(b, L, rc.r00);
+  float x = mdiv(y, L, rc.r00);
+  const bool slow = !(rc.ok && mdiv_in(b) && mdiv_in(y));
+  if (__builtin_amdgcn_ballot_w64(slow) != 0 && slow) x = llt1_solve(L, b);
+  return x;
+}
+
 // The aggregation weight AggregateFlowDense gives patch pixel (lx, ly) -- a pixel of the level (patchgrid.cpp:236-262):
 // 1 / max(2, w) of its loss weight (gray); RGB: the upstream weight pointer advances by 1 for out-of-image pixels and
 // by 3 inside (patchgrid.cpp:243,256-258), so the three weights summed start at ly p + lx + 2 (in-image pixels
@@ -507,6 +558,7 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  const LltRcp lrc = llt_rcp<NOP>(fac, fac1, a.fdiv != 0);
   if (a.stage == 1) {  // timing diagnostic "pconst": construction only; one store keeps the work alive
     if (lane == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[JM - 1];
     return;
@@ -558,11 +610,11 @@ __global__ __launch_bounds__(256) void k_patch(PatchArgs a) {
   while (!converged) {
     ++cnt;
     if (NOP == 2) {
-      llt2_solve(fac, b0, b1, d0, d1);
+      llt2_solve_fast(fac, lrc, b0, b1, d0, d1);
       p0 = p0 - d0;
       p1 = p1 - d1;
     } else {
-      d0 = llt1_solve(fac1, b0);
+      d0 = llt1_solve_fast(fac1, lrc, b0);
       p0 = p0 - d0;
       p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
     }
@@ -686,6 +738,7 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  const LltRcp lrc = llt_rcp<NOP>(fac, fac1, a.fdiv != 0);
   if (a.stage == 1) {  // timing diagnostic "pconst": construction only; one store keeps the work alive
     if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1];
     return;
@@ -776,11 +829,11 @@ __global__ __launch_bounds__(256) void k_patch8(PatchArgs a) {
   while (!converged) {
     ++cnt;
     if (NOP == 2) {
-      llt2_solve(fac, b0, b1, d0, d1);
+      llt2_solve_fast(fac, lrc, b0, b1, d0, d1);
       p0 = p0 - d0;
       p1 = p1 - d1;
     } else {
-      d0 = llt1_solve(fac1, b0);
+      d0 = llt1_solve_fast(fac1, lrc, b0);
       p0 = p0 - d0;
       p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
     }
@@ -909,6 +962,7 @@ __global__ __launch_bounds__(256) void k_patchg(PatchArgs a) {
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  const LltRcp lrc = llt_rcp<NOP>(fac, fac1, a.fdiv != 0);
   const float tlast = A[0] - tmean;  // keeps the template work alive in the diagnostics below
   if (a.stage == 1) {  // timing diagnostic "pconst": construction only
     if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tlast;
@@ -1011,11 +1065,11 @@ __global__ __launch_bounds__(256) void k_patchg(PatchArgs a) {
   while (!converged) {
     ++cnt;
     if (NOP == 2) {
-      llt2_solve(fac, b0, b1, d0, d1);
+      llt2_solve_fast(fac, lrc, b0, b1, d0, d1);
       p0 = p0 - d0;
       p1 = p1 - d1;
     } else {
-      d0 = llt1_solve(fac1, b0);
+      d0 = llt1_solve_fast(fac1, lrc, b0);
       p0 = p0 - d0;
       p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
     }
@@ -1256,6 +1310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  const LltRcp lrc = llt_rcp<NOP>(fac, fac1, a.fdiv != 0);
   if (a.stage == 1) {  // timing diagnostic "pconst": construction only; one store keeps the work alive
     if (live && s8 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[V - 1];
     return;
@@ -1511,11 +1566,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (!first) {
         ++cnt;
         if (NOP == 2) {
-          llt2_solve(fac, b0, b1, d0, d1);
+          llt2_solve_fast(fac, lrc, b0, b1, d0, d1);
           p0 = p0 - d0;
           p1 = p1 - d1;
         } else {
-          d0 = llt1_solve(fac1, b0);
+          d0 = llt1_solve_fast(fac1, lrc, b0);
           p0 = p0 - d0;
           p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
         }
@@ -1675,6 +1730,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  const LltRcp lrc = llt_rcp<NOP>(fac, fac1, a.fdiv != 0);
   if (a.stage == 1) {  // timing diagnostic "pconst"
     if (live && s4 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp2[K - 1].y;
     return;
@@ -1887,11 +1943,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (!first) {
         ++cnt;
         if (NOP == 2) {
-          llt2_solve(fac, b0, b1, d0, d1);
+          llt2_solve_fast(fac, lrc, b0, b1, d0, d1);
           p0 = p0 - d0;
           p1 = p1 - d1;
         } else {
-          d0 = llt1_solve(fac1, b0);
+          d0 = llt1_solve_fast(fac1, lrc, b0);
           p0 = p0 - d0;
           p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
         }
@@ -2072,6 +2128,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
   const Llt2 fac = llt2_factor(H00, H01, H11);
   const float fac1 = llt1_factor(H00);
+  const LltRcp lrc = llt_rcp<NOP>(fac, fac1, a.fdiv != 0);
   if (a.stage == 1) {  // timing diagnostic "pconst"
     if (live && s16 == 0) a.p_iter[gp * NOP] = fac.L00 + fac.L10 + fac.L11 + fac1 + tmp[M - 1];
     return;
@@ -2359,11 +2416,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if (!first) {
         ++cnt;
         if (NOP == 2) {
-          llt2_solve(fac, b0, b1, d0, d1);
+          llt2_solve_fast(fac, lrc, b0, b1, d0, d1);
           p0 = p0 - d0;
           p1 = p1 - d1;
         } else {
-          d0 = llt1_solve(fac1, b0);
+          d0 = llt1_solve_fast(fac1, lrc, b0);
           p0 = p0 - d0;
           p0 = (a.camlr == 0) ? stdminf(p0, 0.0f) : stdmaxf(p0, 0.0f);
         }

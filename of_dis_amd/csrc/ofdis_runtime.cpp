@@ -109,6 +109,7 @@ struct ofdis_context {
   int opt_patch_absw = 1;      // patch kernels that can hand the aggregation its weights directly do (0: loss weights)
   int opt_patch_buf = 1;       // gray p = 12 windows by buffer loads (32-bit offsets) where the image array allows
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
+  int opt_patch_fdiv = 1;      // the LLT solves divide by FMA-corrected pivot reciprocals (0: IEEE divisions)
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
@@ -415,6 +416,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.x16 = c->opt_patch_x16;
     pa.absw = !P.fb && c->opt_patch_absw;  // usefbcon: the complementary grid's loss weights are read raw
     pa.aslots = (p->p_samp_s - 1) / steps + 1;
+    pa.fdiv = c->opt_patch_fdiv;
     pa.buf32 = c->opt_patch_buf && (size_t)n * fsp * sizeof(float) + 4096 <= 0xffffffffu;
     pa.generic = c->opt_patch_generic;
     pa.g = g;
@@ -1315,7 +1317,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
-      {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},
+      {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},  {"patch_fdiv", &ofdis_context::opt_patch_fdiv, 0, 1},
       {"sysor", &ofdis_context::opt_sysor, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };

@@ -131,6 +131,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_x16", 2, 1),       # k_patchx on its exact square-root evaluation (the fallback of the scaled fast one)
     ("patch_absw", 0, 1),      # loss weights to the aggregation instead of the aggregation-weight slot planes
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
+    ("patch_fdiv", 0, 1),      # LLT solves by IEEE divisions instead of the FMA-corrected pivot reciprocals
     ("sysor", 1, 0),           # levels <= 128 rows: system + SOR of an inner iteration in one launch (k_tv_sysor)
 ]
 
@@ -153,6 +154,36 @@ def test_kernel_variants_bitexact(oracle, od, ctx, variant, w, h, noc, mode, op,
         for k, d in zip(keys, defaults):
             ctx.set_option(k, d)
     assert_bitexact(got, ref, f"{keys}={vals}")
+
+
+def _flat_pair(od, w, h, noc, mode):
+    """The synthetic pair with constant blocks (zero gradients: regularised Hessians, zero residuals and
+    right-hand sides) and a saturated stripe: the patch solves' fallback divisions run beside the fast ones."""
+    a, b = od.synth_pair(w, h, noc, 6, mode)
+    a, b = a.copy(), b.copy()
+    for img in (a, b):
+        img[: h // 3, : w // 3] = 0
+        img[h // 2:, w // 2: w // 2 + w // 5] = 128
+        img[h // 4: h // 4 + 6, :] = 255
+    b[: h // 3 + 4, : w // 3 + 4] = 0
+    return a, b
+
+
+@pytest.mark.parametrize("fdiv", [1, 0])
+@pytest.mark.parametrize("w,h,noc,mode,op,over", [(160, 120, 1, 1, 2, {}), (192, 128, 1, 1, 3, {}),
+                                                  (192, 128, 3, 1, 3, {"costfct": 1}), (240, 120, 1, 2, 4, {}),
+                                                  (176, 140, 1, 1, 3, {"patnorm": 0})])
+def test_flat_regions_bitexact(oracle, od, ctx, fdiv, w, h, noc, mode, op, over):
+    """Constant image blocks: the LLT solves' reciprocal-and-FMA divisions hand zero / out-of-range numerators
+    to the IEEE division (patch_fdiv), and every flow value is still the oracle's."""
+    a, b = _flat_pair(od, w, h, noc, mode)
+    p, q = _params(od, oracle, w, noc, mode, op, over)
+    ctx.set_option("patch_fdiv", fdiv)
+    try:
+        got = ctx.run_host(a, b, p)
+    finally:
+        ctx.set_option("patch_fdiv", 1)
+    assert_bitexact(got, oracle.run_u8(a, b, q), f"flat blocks, patch_fdiv={fdiv}")
 
 
 @pytest.mark.parametrize("w,h,noc,op,over", [(160, 120, 1, 2, {}), (173, 97, 1, 2, {}), (192, 128, 3, 3, {}),
