@@ -203,9 +203,14 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "patch_fdiv" (0/1, default 1): the 2x2 / 1x1 LLT solves of every patch iteration divide by one correctly
  *                        rounded reciprocal of each pivot per patch plus two FMAs (exact by Markstein's theorem in
  *                        the range the kernels check; tools/divcheck_l.c), IEEE divisions outside it (0: IEEE always);
+ *   "patch_maxres" (0/1, default 1): with res_thresh = 0 and min_iter >= max_iter (every op-point) the four- and
+ *                        sixteen-lane patch kernels stop on the largest |w| of an evaluation being 0 instead of
+ *                        summing |w| (the same decision; NaN and tiny terms redo the evaluation with the sum);
  *   "patch_generic" (0/1, default 0): every patch shape on the any-shape kernel (runtime value loops: the
  *                        default for p*p*noc > 448, e.g. RGB p >= 14, gray p >= 22);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
+ *   "up_form" (0..2, default 1): optical-flow upsample: 1 / 2 = each staged source row's horizontal taps once per
+ *                        column for blocks of 4 / 8 output rows, 0 = once per output row that reads them (round 4);
  *   "graph" (0/1/2/3, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
  *                        parameters repeat (re-captured when they change); 1 captures single-stream
  *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined; the

@@ -77,7 +77,9 @@ struct PatchArgs {
   int aslots;                                 // A = (p - 1) / steps + 1: slot planes per axis
   int buf32;                                  // the image array of the launch spans < 2^32 bytes (32-bit buffer offsets)
   int fdiv;                                   // 1: the LLT solves divide by FMA-corrected pivot reciprocals (llt_rcp)
-  int stage;                                 // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
+  int maxres;                                 // 1: res_thresh = 0 and min_iter >= max_iter: the four- and sixteen-lane
+                                              // kernels test the largest |w| > 0 instead of mean |w| > res_thresh
+  int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):
                                               // 1 construction only (pconst), 2 + initialisation (pinit)
   LevelGeom g;
 };
@@ -138,6 +140,7 @@ struct UpArgs {
   float *out;         // [n][H0][W0][nop]
   int n, nop, wl, hl, log2s, W0, H0, offx, offy;
   int nt_store;       // non-temporal output stores (A/B option "nt_store")
+  int form;           // nop = 2: 0 k_upsample_rows, 1 k_upsample_h<4>, 2 k_upsample_h<8> (option "up_form")
 };
 
 // Initial flow (run_dense.cpp:356-379): full-resolution [n][H0][W0][nop] -> replicate-padded, x sc,

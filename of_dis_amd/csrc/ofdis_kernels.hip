@@ -1651,6 +1651,10 @@ __device__ __forceinline__ float quad_total(f2p acc) {
   r = r + grp_xor2(r);
   return r + grp_xor1(r);
 }
+__device__ __forceinline__ float quad_max(float m) {
+  m = fmaxf(m, grp_xor2(m));
+  return fmaxf(m, grp_xor1(m));
+}
 
 template <int NOP, int P, int NOC, int MINW, int COST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchq(PatchArgs a) {
@@ -1768,8 +1772,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     if (x >= 0 && y >= 0 && x < g.w && y < g.h) pl[ly * g.w + lx] = 1.0f / stdmaxf(2.0f, wv);
   };
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
-  auto evaluate = [&](float &r0, float *out, auto store_t) {
+  // MAXR (maxres): r0 = the largest |w| instead of the sum -- see the iteration loop
+  auto evaluate = [&](float &r0, float *out, auto store_t, auto maxr_t) {
     constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
+    constexpr bool MAXR = decltype(maxr_t)::value;
     const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
     const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
@@ -1888,16 +1894,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         f2p qy;
         if constexpr (NOP == 2) qy = gy2[k] * e;
         if constexpr (k == 0) {
-          abl = fabsf(wv.x);
-          abh = fabsf(wv.y);
+          if constexpr (MAXR) {
+            abl = fmaxf(fabsf(wv.x), fabsf(wv.y));
+          } else {
+            abl = fabsf(wv.x);
+            abh = fabsf(wv.y);
+          }
           ex = qx;
           if (NOP == 2) ey = qy;
         } else {
-          abl = abl + fabsf(wv.x);
-          abh = abh + fabsf(wv.y);
-          // two scalar adds with |.| source modifiers; left to itself the compiler packs this chain pair
-          // (v_pk_add_f32 after two v_and_b32: three instructions instead of two)
-          asm volatile("" : "+v"(abl), "+v"(abh));
+          if constexpr (MAXR) {
+            abl = fmaxf(abl, fmaxf(fabsf(wv.x), fabsf(wv.y)));  // one v_max3_f32 with |.| modifiers per pair
+          } else {
+            abl = abl + fabsf(wv.x);
+            abh = abh + fabsf(wv.y);
+            // two scalar adds with |.| source modifiers; left to itself the compiler packs this chain pair
+            // (v_pk_add_f32 after two v_and_b32: three instructions instead of two)
+            asm volatile("" : "+v"(abl), "+v"(abh));
+          }
           ex = ex + qx;
           if (NOP == 2) ey = ey + qy;
         }
@@ -1913,7 +1927,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     });
     if constexpr (STORE == 0) {
-      r0 = quad_total(f2p{abl, abh});
+      if constexpr (MAXR)
+        r0 = quad_max(abl);
+      else
+        r0 = quad_total(f2p{abl, abh});
       b0 = quad_total(ex);
       if (NOP == 2) b1 = quad_total(ey);
     }
@@ -1963,23 +1980,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         }
       }
       float r0 = 0.0f;
-      evaluate(r0, nullptr, std::integral_constant<int, 0>());
-      // OptimizeComputeErrImg (patch.cpp:275-295)
+      // OptimizeComputeErrImg (patch.cpp:275-295).  maxres (res_thresh = 0, min_iter >= max_iter: every
+      // op-point): mares only meets the test mares > 0, and the rate tests only iterations that stop anyway; a sum
+      // of |w| >= 0 is positive iff its largest term is, and RN(sum / N) > 0 then too while that term is >= 2^-100.
+      // So the evaluation keeps the largest |w| (one v_max3 per value pair instead of two adds, no division);
+      // a wave with a NaN (b0 / b1 are NaN iff some residual is) or a term in (0, 2^-100) redoes it with the sum.
+      bool summed = true;
+      if (a.maxres) {
+        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type());
+        summed = false;
+        const bool odd = (r0 > 0.0f && r0 < 0x1p-100f) || b0 != b0 || (NOP == 2 && b1 != b1);
+        if (__builtin_amdgcn_ballot_w64(odd) != 0) {
+          evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type());
+          summed = true;
+        }
+      } else {
+        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type());
+      }
       sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
       if (cnt == 1) sq_init = sq;
       mares_old = mares;
-      mares = div_n(r0);
+      mares = summed ? div_n(r0) : r0;
       bool rates = true;
       if (__builtin_amdgcn_ballot_w64(cnt >= a.min_iter) != 0)
         rates = (cnt < a.min_iter) | ((sq / sq_init >= a.dp_thresh_sq) & (mares / mares_old <= a.dr_thresh));
-      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) & rates;
+      const bool keep = (cnt < a.max_iter) & (summed ? mares > a.res_thresh : r0 > 0.0f) & rates;
       if (!keep) converged = true;
     }
     first = false;
   }
   if (live && !start_oob) {
     float r0;
-    evaluate(r0, pwo, std::integral_constant<int, 1>());
+    evaluate(r0, pwo, std::integral_constant<int, 1>(), std::false_type());
   }
   if (live && s4 < NOP) a.p_iter[gp * NOP + s4] = s4 == 0 ? p0 : p1;
 }
@@ -2195,9 +2227,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   // getPatchStaticBil + mean normalisation + LossComputeErrorImage (patch.cpp:221-413) at (pt0, pt1)
   // FAST: the loss square roots by sqrt_nonneg_s64 (exact below 2^64; a sum that comes out non-finite makes the
   // caller redo the evaluation with sqrt_nonneg)
-  auto evaluate = [&](float &r0, float *out, auto store_t, auto fast_t) {
+  // MAXR (maxres, with FAST only): r0 = the largest w instead of the sum -- see the iteration loop
+  auto evaluate = [&](float &r0, float *out, auto store_t, auto fast_t, auto maxr_t) {
     constexpr int STORE = decltype(store_t)::value;  // 0: the sums only; 1: the weights only, to `out`
     constexpr bool FAST = decltype(fast_t)::value;
+    constexpr bool MAXR = decltype(maxr_t)::value;
     const int pos0 = (int)ceilf(pt0 + 0.00001f) + g.pad;
     const int pos1 = (int)ceilf(pt1 + 0.00001f) + g.pad;
     const int pos2 = (int)floorf(pt0), pos3 = (int)floorf(pt1);
@@ -2312,6 +2346,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
     };
     XAcc ab, ex;
+    float abm = 0.0f;           // MAXR: the lane's largest w
     f2p exy = f2p{0.0f, 0.0f};  // optical flow: the x and y chains side by side (own adds packed)
     // pair groups: d of both halves packed; the .x halves (values m) go into the chains at once, the .y halves'
     // d (values m + KP) are kept until their turn, after the group's KP .x values
@@ -2323,13 +2358,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
     };
     auto flush = [&](int m) {  // compile-time m: value m's terms into the chains
-      ab.own(m, pw);  // w >= +0 for every cost (|d| or a square root): |w| == w
+      if constexpr (MAXR)
+        abm = m == 0 ? pw : fmaxf(abm, pw);
+      else
+        ab.own(m, pw);  // w >= +0 for every cost (|d| or a square root): |w| == w
       if constexpr (NOP == 2) {
         exy = m == 0 ? pq : exy + pq;  // the x and y chains' own values (XAcc::own, two chains at once)
       } else {
         ex.own(m, pqx);
       }
-      ab.partner(pw);
+      if constexpr (!MAXR) ab.partner(pw);
       if constexpr (NOP == 2) {  // XAcc::partner per chain
         exy.x = exy.x + dppf(pq.x);
         exy.y = exy.y + dppf(pq.y);
@@ -2384,7 +2422,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     if (STORE == 0) {
       flush(M - 1);
       constexpr float sc = (FAST && COST != 0) ? 0x1p-32f : 1.0f;
-      r0 = ab.total() * sc;
+      if constexpr (MAXR) {
+        float mx = fmaxf(abm, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, abm), 0x128,
+                                                                                0xF, 0xF, true)));
+        mx = fmaxf(mx, grp_xor4(mx));
+        mx = fmaxf(mx, grp_xor2(mx));
+        mx = fmaxf(mx, grp_xor1(mx));
+        // at scale 1; a positive maximum that the rescaling would take below 2^-100 stays positive and small
+        // (the caller's fallback range)
+        r0 = mx > 0.0f ? fmaxf(mx * sc, 0x1p-120f) : mx;
+      } else {
+        r0 = ab.total() * sc;
+      }
       if constexpr (NOP == 2) {
         XAcc tx, ty;
         tx.acc = exy.x;
@@ -2436,23 +2485,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         }
       }
       float r0 = 0.0f;
-      bool exact = COST != 0 && (!xok || a.x16 == 2);
+      // maxres (res_thresh = 0, min_iter >= max_iter: every op-point) -- mares only meets mares > 0 (see
+      // k_patchq): the FAST evaluation keeps the largest w, and a wave with a non-finite b0 / b1 (NaN iff some
+      // residual is) or a term in (0, 2^-100) redoes the iteration's evaluation exactly, with the sum.  Without
+      // maxres every evaluation is the exact one.
+      constexpr float fmx = 3.402823466e38f;
+      bool exact = !a.maxres || (COST != 0 && (!xok || a.x16 == 2));
+      bool summed = true;
       if (!exact) {
-        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type());
-        constexpr float fmx = 3.402823466e38f;
-        exact = COST != 0 && __builtin_amdgcn_ballot_w64(!(r0 <= fmx) || !(fabsf(b0) <= fmx) ||
-                                                         (NOP == 2 && !(fabsf(b1) <= fmx))) != 0;
+        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type(), std::true_type());
+        summed = false;
+        const bool odd = (r0 > 0.0f && r0 < 0x1p-100f) || !(fabsf(b0) <= fmx) || (NOP == 2 && !(fabsf(b1) <= fmx));
+        exact = __builtin_amdgcn_ballot_w64(odd) != 0;
       }
-      if (exact) evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type());
+      if (exact) {
+        evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::false_type(), std::false_type());
+        summed = true;
+      }
       // OptimizeComputeErrImg (patch.cpp:275-295)
       sq = (NOP == 2) ? d0 * d0 + d1 * d1 : d0 * d0;
       if (cnt == 1) sq_init = sq;
       mares_old = mares;
-      mares = div_n(r0);
+      mares = summed ? div_n(r0) : r0;
       bool rates = true;
       if (__builtin_amdgcn_ballot_w64(cnt >= a.min_iter) != 0)
         rates = (cnt < a.min_iter) | ((sq / sq_init >= a.dp_thresh_sq) & (mares / mares_old <= a.dr_thresh));
-      const bool keep = (cnt < a.max_iter) & (mares > a.res_thresh) & rates;
+      const bool keep = (cnt < a.max_iter) & (summed ? mares > a.res_thresh : r0 > 0.0f) & rates;
       if (!keep) converged = true;
     }
     first = false;
@@ -2462,7 +2520,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     // each lane the aggregation weights of pixels s16 + 16 i from there
     if (live && !start_oob) {
       float r0;
-      evaluate(r0, win, std::integral_constant<int, 1>(), std::false_type());
+      evaluate(r0, win, std::integral_constant<int, 1>(), std::false_type(), std::false_type());
     } else {
 #pragma unroll
       for (int m = 0; m < M; ++m) win[s16 + 16 * m] = 0.0f;
@@ -2481,7 +2539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
     }
   } else if (live && !start_oob) {
     float r0;
-    evaluate(r0, pwo, std::integral_constant<int, 1>(), std::false_type());
+    evaluate(r0, pwo, std::integral_constant<int, 1>(), std::false_type(), std::false_type());
   }
   if (live && s16 < NOP) a.p_iter[gp * NOP + s16] = s16 == 0 ? p0 : p1;
 }
@@ -4541,6 +4599,135 @@ __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
   }
 }
 
+// k_upsample_h<R>: the same output (same expressions, same lanes and stores) with each staged source row's
+// horizontal taps computed once per lane and column instead of once per output row that reads them
+// (VResizeLinear blends two HResizeLinear rows; at 2^l = 2 four output rows read four source rows, eight
+// horizontal evaluations before), and the staging copy in 16-byte groups with no per-element division:
+// B's upsample issued ~500 VALU per wave, 43 % of the whole pipeline's VALU (profiles/r05/s9).  R output rows
+// per block (4 or 8).  The staged window starts at the 4-aligned column below the first one the block reads.
+template <int R>
+__global__ __launch_bounds__(256) void k_upsample_h(UpArgs a) {
+  constexpr int NSR = R / 2 + 3;         // source rows a block can touch (2^l >= 2)
+  constexpr int SC = kUpCols / 2 + 8;    // staged columns per row (>= the 514 + 3 a block reads at 2^l = 2)
+  constexpr int S4 = SC / 4;             // 16-byte groups per staged row
+  __shared__ __attribute__((aligned(16))) float src[NSR][2][SC];
+  const int y0 = blockIdx.y * R, f = blockIdx.z;
+  const int dx0 = blockIdx.x * kUpCols + a.offx;
+  const int fct_i = 1 << a.log2s;
+  const float fct = (float)fct_i, half_inv = 1.0f / (float)(2 * fct_i);
+  const long plane = (long)a.wl * a.hl;
+  const float *F = a.flow + (long)f * 2 * plane;
+  auto src_row = [&](int dy, float &fy) {  // resizeGeneric_Invoker rows: sy, fy (weights not clamped)
+    fy = (float)(2 * dy + 1 - fct_i) * half_inv;
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    return sy;
+  };
+  auto clip_row = [&](int r) { return r >= 0 ? (r < a.hl ? r : a.hl - 1) : 0; };
+  const int yl = min(y0 + R, a.H0) - 1;
+  float dummy;
+  const int r_first = clip_row(src_row(y0 + a.offy, dummy));
+  const int r_last = clip_row(src_row(yl + a.offy, dummy) + 1);
+  const int nr = r_last - r_first + 1;
+  const int c_lo = max(0, (int)floorf((float)(2 * dx0 + 1 - fct_i) * half_inv));
+  const int c0 = c_lo & ~3;                                  // staged column 0
+  const int n4 = min(S4, (c_lo - c0 + kUpCols / fct_i + 2 + 3) >> 2);
+  const bool vec = (a.wl & 3) == 0 && ((uintptr_t)a.flow & 15) == 0;
+  for (int e = threadIdx.x; e < nr * 2 * S4; e += 256) {  // (row, comp) = e / S4: a division by a constant
+    const int rc = e / S4, j = e - rc * S4;
+    if (j >= n4) continue;
+    const int r = rc >> 1, comp = rc & 1, c = c0 + 4 * j;
+    const float *row = F + comp * plane + (long)(r_first + r) * a.wl;
+    v4f v;
+    if (vec && c + 3 < a.wl) {
+      v = *reinterpret_cast<const v4f *>(row + c);
+    } else {
+      v = v4f{row[min(c, a.wl - 1)], row[min(c + 1, a.wl - 1)], row[min(c + 2, a.wl - 1)], row[min(c + 3, a.wl - 1)]};
+    }
+    *reinterpret_cast<v4f *>(&src[r][comp][4 * j]) = v * fct;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int xb = blockIdx.x * kUpCols + wv * 256 + 2 * lane;
+  int xs[2] = {xb, xb + 128};
+  int cc[4];
+  float fxs[4], gxs[4];
+  bool lin[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int dx = xs[i >> 1] + (i & 1) + a.offx;
+    float fx = (float)(2 * dx + 1 - fct_i) * half_inv;
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    bool l = true;
+    if (sx + 1 >= a.wl) {
+      l = false;
+      if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
+    }
+    cc[i] = min(max(sx - c0, 0), SC - 2);  // columns past W0 are computed, never stored
+    fxs[i] = fx;
+    gxs[i] = 1.f - fx;
+    lin[i] = l;
+  }
+  auto hrow = [&](int j, float *h) {  // HResizeLinear of staged row j at the lane's 4 columns, both components
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float s0 = src[j][k][cc[q]];
+        h[q * 2 + k] = lin[q] ? s0 * gxs[q] + src[j][k][cc[q] + 1] * fxs[q] : s0;
+      }
+  };
+  float ha[8], hb[8];
+  int ja = -1, jb = -1;  // staged rows held in ha / hb (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int y = y0 + i;
+    if (y >= a.H0) break;
+    float fy;
+    const int sy = src_row(y + a.offy, fy);
+    const int j0 = clip_row(sy) - r_first, j1 = clip_row(sy + 1) - r_first;
+    if (j0 != ja) {
+      if (j0 == jb) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) ha[t] = hb[t];
+      } else {
+        hrow(j0, ha);
+      }
+      ja = j0;
+    }
+    if (j1 != jb) {
+      if (j1 == ja) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) hb[t] = ha[t];
+      } else {
+        hrow(j1, hb);
+      }
+      jb = j1;
+    }
+    const float b0 = 1.f - fy, b1 = fy;
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = ha[t] * b0 + hb[t] * b1;
+    float *orow = a.out + ((long)f * a.H0 + y) * a.W0 * 2;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int x = xs[hh];
+      if (x + 2 <= a.W0) {
+        const v4f val = v4f{v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]};
+        if (a.nt_store)
+          __builtin_nontemporal_store(val, reinterpret_cast<v4f *>(orow + 2 * x));
+        else
+          *reinterpret_cast<v4f *>(orow + 2 * x) = val;
+      } else if (x < a.W0) {
+        orow[2 * x] = v[4 * hh];
+        orow[2 * x + 1] = v[4 * hh + 1];
+      }
+    }
+  }
+}
+
 // The same for depth (nop = 1): lane i of wave wv owns the four output columns xb + 4i .. xb + 4i + 3
 // (xb = block + 256 wv): one 16-byte store per row, 1 KiB contiguous per wave-instruction.
 __global__ __launch_bounds__(256) void k_upsample_rows1(UpArgs a) {
@@ -5066,9 +5253,14 @@ void launch_init_area(const InitArgs &a, hipStream_t s) {
 }
 
 void launch_upsample(const UpArgs &a, hipStream_t s) {
-  if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
-    k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
-  else if (a.nop == 1 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
+  if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0) {
+    if (a.form == 2)
+      k_upsample_h<8><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 8), a.n), 256, 0, s>>>(a);
+    else if (a.form == 1)
+      k_upsample_h<4><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 4), a.n), 256, 0, s>>>(a);
+    else
+      k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
+  } else if (a.nop == 1 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
     k_upsample_rows1<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
   else
     k_upsample<<<dim3(ceil_div(a.W0, 256), a.H0, a.n), 256, 0, s>>>(a);

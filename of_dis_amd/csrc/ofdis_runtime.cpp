@@ -79,6 +79,7 @@ struct ofdis_context {
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
+  int opt_up_form = 1;         // flow upsample: 0 per-output-row horizontal taps, 1 / 2 once per source row (4 / 8 rows)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   // the fused launch on 2-D tiles for tall levels: 1 on, 0 off (two launches there), 2 auto = on for calls of
   // fewer than 512 pairs (one stream).  Measured at config E: alone on the GPU it cuts the system time 10 %
@@ -110,6 +111,7 @@ struct ofdis_context {
   int opt_patch_buf = 1;       // gray p = 12 windows by buffer loads (32-bit offsets) where the image array allows
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
   int opt_patch_fdiv = 1;      // the LLT solves divide by FMA-corrected pivot reciprocals (0: IEEE divisions)
+  int opt_patch_maxres = 1;    // op-point stopping (res_thresh 0, min_iter = max_iter): largest |w| > 0 for mean > 0
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
@@ -417,6 +419,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.absw = !P.fb && c->opt_patch_absw;  // usefbcon: the complementary grid's loss weights are read raw
     pa.aslots = (p->p_samp_s - 1) / steps + 1;
     pa.fdiv = c->opt_patch_fdiv;
+    pa.maxres = c->opt_patch_maxres && pa.res_thresh == 0.0f && pa.min_iter >= pa.max_iter;
     pa.buf32 = c->opt_patch_buf && (size_t)n * fsp * sizeof(float) + 4096 <= 0xffffffffu;
     pa.generic = c->opt_patch_generic;
     pa.g = g;
@@ -769,6 +772,7 @@ int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *
   up.offx = P.padl;
   up.offy = P.padt;
   up.nt_store = c->opt_nt_store;
+  up.form = c->opt_up_form;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
@@ -1313,11 +1317,13 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
-      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 2},
+      {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},  {"patch_fdiv", &ofdis_context::opt_patch_fdiv, 0, 1},
+      {"patch_maxres", &ofdis_context::opt_patch_maxres, 0, 1},
       {"sysor", &ofdis_context::opt_sysor, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
