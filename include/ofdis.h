@@ -175,9 +175,10 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        thread's derivative-image loads before the staging, not after two barriers;
  *   "smsys_small" (0/1, default 1): a fused launch that cannot fill the chip (fewer than 4096 row blocks:
  *                        a few pairs per call) takes ~1 pixel per thread (>= 4 rows per block) instead of 4;
- *   "smsys_deriv" (0/1, default 1): where "prepd" and the fused launch (levels up to 256 rows) or the register
- *                        march (taller levels) run (intensity images), the system kernel filters Ixx, Ixy, Iyy,
- *                        Ixz, Iyz from Ix, Iy, Iz and the prep launch does not write those five planes;
+ *   "smsys_deriv" (0/1, default 1): where "prepd" and the fused launch (levels up to 256 rows, intensity images)
+ *                        or the register march (taller levels, intensity and colour images) run, the system kernel
+ *                        filters Ixx, Ixy, Iyy, Ixz, Iyz from Ix, Iy, Iz and the prep launch does not write those
+ *                        five planes (per channel);
  *   "smsys_march" (0/1, default 1): levels taller than 256 rows run smoothness + system as a register march
  *                        (one wave per 60 columns x 64 rows, no LDS; takes precedence over smsys2d);
  *   "prepd" (0..2, default 2): image warp, temporal images and the derivative filters of a level in one launch

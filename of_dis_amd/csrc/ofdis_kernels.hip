@@ -3252,13 +3252,12 @@ __device__ __forceinline__ float conv5_clamp(const float (&t)[5], int pos, int n
   return kK5[0] * m2 + ((kK5[1] * m1 + kK5[2] * t[2]) + (kK5[3] * p1 + kK5[4] * p2));
 }
 
-// DF (intensity images, option smsys_deriv, round 4): the march keeps rows r - 2 .. r + 2 of Ix, Iy, Iz in registers
-// and filters the five second derivatives of row r itself: a horizontal tap x + k is row r + k of the same lane, a
-// vertical tap y + k row r + k of lane + k (DPP shifts); k_tv_prepd then writes 3 of the 8 derivative planes, and a
-// step reads 5 planes instead of 10.
+// DF (option smsys_deriv; intensity images round 4, colour images round 5): the march keeps rows r - 2 .. r + 2 of
+// Ix, Iy, Iz (of every channel) in registers and filters the five second derivatives of row r itself: a horizontal
+// tap x + k is row r + k of the same lane, a vertical tap y + k row r + k of lane + k (DPP shifts); k_tv_prepd then
+// writes 3 of the 8 derivative planes per channel, and a step reads 5 (colour: 11) planes instead of 10 (26).
 template <int NOP, int NOC, bool DF = false>
 __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
-  static_assert(!DF || NOC == 1, "filtered derivatives: intensity images");
   const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
   const int nstrip = march_strips(h), nseg = march_segments(rows);
   const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (frame, segment, strip), strip fastest
@@ -3321,16 +3320,19 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
     return smooth_from_uu<NOP>(a, uu5, vv5);
   };
   struct Drow {
-    float ix, iy, iz;
+    float ix[NOC], iy[NOC], iz[NOC];
   };
-  auto load_d = [&](int r) {  // DF: Ix, Iy, Iz of row r (0 outside the plane / the level's columns)
-    Drow q{0.f, 0.f, 0.f};
+  auto load_d = [&](int r) {  // DF: Ix, Iy, Iz of row r, every channel (0 outside the plane / the level's columns)
+    Drow q;
     const int pr = prow(r);
-    if (pr >= 0 && ycol) {
-      const unsigned o = f0 + (unsigned)(pr * h + y);
-      q.ix = ldu(a.Ix, o);
-      q.iy = ldu(a.Iy, o);
-      q.iz = ldu(a.Iz, o);
+    const bool in = pr >= 0 && ycol;
+    const unsigned o = (unsigned)((long)f * NOC * a.sp + (in ? pr * h + y : 0));
+#pragma unroll
+    for (int ch = 0; ch < NOC; ++ch) {
+      const unsigned oc = o + (unsigned)(ch * a.sp);
+      q.ix[ch] = in ? ldu(a.Ix, oc) : 0.f;
+      q.iy[ch] = in ? ldu(a.Iy, oc) : 0.f;
+      q.iz[ch] = in ? ldu(a.Iz, oc) : 0.f;
     }
     return q;
   };
@@ -3384,20 +3386,24 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
         t[3] = wave_from_next(p1);
         t[4] = wave_from_next(wave_from_next(p2));
       };
-      float vx[5], vy[5], vz[5];
-      vt(D0.ix, D1.ix, D2.ix, D3.ix, D4.ix, vx);
-      vt(D0.iy, D1.iy, D2.iy, D3.iy, D4.iy, vy);
-      vt(D0.iz, D1.iz, D2.iz, D3.iz, D4.iz, vz);
-      const float hx[5] = {D0.ix, D1.ix, D2.ix, D3.ix, D4.ix}, hz[5] = {D0.iz, D1.iz, D2.iz, D3.iz, D4.iz};
       const int xc = has ? x : 0, yc = ycol ? y : 0;  // (lanes without a pixel: any valid taps)
-      lIx[0] = D2.ix;
-      lIy[0] = D2.iy;
-      lIz[0] = D2.iz;
-      lIxx[0] = conv5_clamp(hx, xc, w);
-      lIxy[0] = conv5_clamp(vx, yc, h);
-      lIyy[0] = conv5_clamp(vy, yc, h);
-      lIxz[0] = conv5_clamp(hz, xc, w);
-      lIyz[0] = conv5_clamp(vz, yc, h);
+#pragma unroll
+      for (int ch = 0; ch < NOC; ++ch) {
+        float vx[5], vy[5], vz[5];
+        vt(D0.ix[ch], D1.ix[ch], D2.ix[ch], D3.ix[ch], D4.ix[ch], vx);
+        vt(D0.iy[ch], D1.iy[ch], D2.iy[ch], D3.iy[ch], D4.iy[ch], vy);
+        vt(D0.iz[ch], D1.iz[ch], D2.iz[ch], D3.iz[ch], D4.iz[ch], vz);
+        const float hx[5] = {D0.ix[ch], D1.ix[ch], D2.ix[ch], D3.ix[ch], D4.ix[ch]};
+        const float hz[5] = {D0.iz[ch], D1.iz[ch], D2.iz[ch], D3.iz[ch], D4.iz[ch]};
+        lIx[ch] = D2.ix[ch];
+        lIy[ch] = D2.iy[ch];
+        lIz[ch] = D2.iz[ch];
+        lIxx[ch] = conv5_clamp(hx, xc, w);
+        lIxy[ch] = conv5_clamp(vx, yc, h);
+        lIyy[ch] = conv5_clamp(vy, yc, h);
+        lIxz[ch] = conv5_clamp(hz, xc, w);
+        lIyz[ch] = conv5_clamp(vz, yc, h);
+      }
       D0 = D1;
       D1 = D2;
       D2 = D3;
@@ -5017,8 +5023,9 @@ bool tv_smsys_ok(const TvArgs &a) {
 // Not where the 40 KB LDS cap of the DF form leaves fewer than 3 rows per block (levels of ~180-256 rows): a
 // block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
-  if (!(a.smsys_deriv && a.noc == 1 && tv_prepd_ok(a) && a.smsys)) return false;
+  if (!(a.smsys_deriv && tv_prepd_ok(a) && a.smsys)) return false;
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) return a.smsys_march != 0;  // the march filters them too
+  if (a.noc != 1) return false;  // colour images: the march only (a row block would stage 9 derivative planes)
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
   while (rb > 1 && smsys_lds_df(a.h, rb, true) > kSmsysDfCap) --rb;
   return rb >= 3;
@@ -5027,9 +5034,14 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {
     const long waves = (long)a.n * march_segments(smsys_rows(a.w, a.h, a.wrap)) * march_strips(a.h);
     const unsigned grid = ceil_div(waves, 4);
-    if (a.noc == 1 && a.smsys_deriv) {  // tv_deriv_fused(): k_tv_prepd wrote Ix, Iy, Iz only
-      if (a.nop == 2) k_tv_smsys_m<2, 1, true><<<grid, 256, 0, s>>>(a);
-      else k_tv_smsys_m<1, 1, true><<<grid, 256, 0, s>>>(a);
+    if (a.smsys_deriv) {  // tv_deriv_fused(): k_tv_prepd wrote Ix, Iy, Iz only
+      if (a.noc == 1) {
+        if (a.nop == 2) k_tv_smsys_m<2, 1, true><<<grid, 256, 0, s>>>(a);
+        else k_tv_smsys_m<1, 1, true><<<grid, 256, 0, s>>>(a);
+      } else {
+        if (a.nop == 2) k_tv_smsys_m<2, 3, true><<<grid, 256, 0, s>>>(a);
+        else k_tv_smsys_m<1, 3, true><<<grid, 256, 0, s>>>(a);
+      }
     } else if (a.nop == 2) {
       if (a.noc == 1) k_tv_smsys_m<2, 1><<<grid, 256, 0, s>>>(a);
       else k_tv_smsys_m<2, 3><<<grid, 256, 0, s>>>(a);

@@ -90,7 +90,7 @@ struct ofdis_context {
   int opt_smsys_march = 1;     // tall levels: smoothness + system as a register march (k_tv_smsys_m)
   int opt_smsys_prefetch = 1;  // fused smoothness + system (gray): derivative images issued before the staging
   int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
-  int opt_smsys_deriv = 1;     // fused smoothness + system (gray): second derivatives filtered from staged Ix, Iy, Iz
+  int opt_smsys_deriv = 1;     // fused smoothness + system (gray; colour: the march): second derivatives filtered from Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
   int opt_sor_cring = 2;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients;
                                // 2: ring sized to the level's row groups (28-byte OF entries in throughput
