@@ -204,8 +204,6 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "patch_fdiv" (0/1, default 1): the 2x2 / 1x1 LLT solves of every patch iteration divide by one correctly
  *                        rounded reciprocal of each pivot per patch plus two FMAs (exact by Markstein's theorem in
  *                        the range the kernels check; tools/divcheck_l.c), IEEE divisions outside it (0: IEEE always);
- *   "patch_qrows" (0/1, default 1): the four-lane gray patch kernel reads each bilinear tap of its window once per
- *                        evaluation, window row by window row (0: the four taps of every value pair);
  *   "patch_maxres" (0/1, default 1): with res_thresh = 0 and min_iter >= max_iter (every op-point) the four- and
  *                        sixteen-lane patch kernels stop on the largest |w| of an evaluation being 0 instead of
  *                        summing |w| (the same decision; NaN and tiny terms redo the evaluation with the sum);

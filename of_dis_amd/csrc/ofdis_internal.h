@@ -77,7 +77,6 @@ struct PatchArgs {
   int aslots;                                 // A = (p - 1) / steps + 1: slot planes per axis
   int buf32;                                  // the image array of the launch spans < 2^32 bytes (32-bit buffer offsets)
   int fdiv;                                   // 1: the LLT solves divide by FMA-corrected pivot reciprocals (llt_rcp)
-  int qrows;                                  // k_patchq: bilinear taps read once per window row (0: four per value pair)
   int maxres;                                 // 1: res_thresh = 0 and min_iter >= max_iter: the four- and sixteen-lane
                                               // kernels test the largest |w| > 0 instead of mean |w| > res_thresh
   int stage;                                  // 0 the whole patch optimisation; timing diagnostics (verbosity 2):

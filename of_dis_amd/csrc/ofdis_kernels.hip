@@ -1656,7 +1656,7 @@ __device__ __forceinline__ float quad_max(float m) {
   return fmaxf(m, grp_xor1(m));
 }
 
-template <int NOP, int P, int NOC, int MINW, int COST, bool ROWS = true>
+template <int NOP, int P, int NOC, int MINW, int COST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void k_patchq(PatchArgs a) {
   const uint3 xb = xcd_block();
   using S = QuadShape<P, NOC>;
@@ -1837,52 +1837,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       }
       wave_lds_sync();
     }
-    f2p pd2[K], macc;
-    if constexpr (ROWS) {
-      // window rows (round 5): T(r, g) = the taps 4g and 4g + NOC of window row r (lane s: + s), one ds_read2_b32;
-      // value (r, g) -- value r ROWV + 4g + s -- takes D, C from T(r, g) and B, A from T(r + 1, g), so every tap of
-      // the lane is read once per evaluation: (P + 1) G reads instead of 4 K (the LDS reads bound this kernel:
-      // 4 K = 72 of them per iteration at p = 12, 4 cycles of the CU's LDS each, against ~2k VALU cycles per SIMD).
-      // The sample is ((w0 A + w1 B) + w2 C) + w3 D as before: (w1 B, w0 A) and (w3 D, w2 C) packed, then the three
-      // additions in that order on the pair halves.  Rows r + 1 and r + 2 are in flight while row r is computed.
-      constexpr int G = S::ROWV / 4;
-      f2p tr[3][G];
-      auto rissue = [&](auto rc) {
-        constexpr int r = decltype(rc)::value;
-        static_for<G>([&](auto gc) {
-          constexpr int g = decltype(gc)::value, o = r * RS + 4 * g;
-          tr[r % 3][g] = lds_read2<o, o + NOC>(wb);
-        });
-      };
-      const f2p wdc = f2p{w3, w2}, wba = f2p{w1, w0};
-      float pv[2 * K];  // the lane's samples in value order: value 4j + s
-      rissue(std::integral_constant<int, 0>{});
-      rissue(std::integral_constant<int, 1>{});
-      static_for<P>([&](auto rc) {
-        constexpr int r = decltype(rc)::value;
-        if constexpr (r + 2 <= P) {
-          rissue(std::integral_constant<int, r + 2>{});
-          lds_wait<G>();
-        } else {
-          lds_wait<0>();
-        }
-        static_for<G>([&](auto gc) {
-          constexpr int g = decltype(gc)::value;
-          reg_fence(tr[r % 3][g]);
-          reg_fence(tr[(r + 1) % 3][g]);
-          const f2p dc = tr[r % 3][g] * wdc, ba = tr[(r + 1) % 3][g] * wba;
-          pv[r * G + g] = ((ba.y + ba.x) + dc.y) + dc.x;
-        });
-      });
-      static_for<K>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        pd2[k] = f2p{pv[2 * k], pv[2 * k + 1]};
-        if constexpr (k == 0) macc = pd2[k];
-        else macc = macc + pd2[k];
-      });
-    } else {
     // taps of pair k: one ds_read2_b32 per tap (D, C, B, A), the next pair's reads in flight
-    f2p q[2][4];
+    f2p pd2[K], q[2][4];
     auto issue = [&](auto kc) {
       constexpr int k = decltype(kc)::value, c0 = S::dtap(k, 0), c1 = S::dtap(k, 4);
       constexpr int mx = (c0 > c1 ? c0 : c1) + RS + NOC;
@@ -1894,6 +1850,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       q[k & 1][3] = lds_read2<c0 - b + RS + NOC, c1 - b + RS + NOC>(ad);  // A
     };
     issue(std::integral_constant<int, 0>{});
+    f2p macc;
     static_for<K>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
       if constexpr (k + 1 < K) {
@@ -1911,7 +1868,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       if constexpr (k == 0) macc = x;
       else macc = macc + x;
     });
-    }
     const float mean = a.patnorm > 0 ? div_n(quad_total(macc)) : 0.0f;
     float abl = 0.0f, abh = 0.0f;
     f2p ex, ey;
@@ -4948,19 +4904,13 @@ static void patchq(const PatchArgs &a, hipStream_t s) {
   const long patches = (long)a.n * a.g.npatch;
   const size_t lds = sizeof(float) * 64 * QuadShape<P, NOC>::WIN;
   const dim3 grid(ceil_div(patches, 64));
-  switch (a.costfct * 4 + (a.nop == 2 ? 2 : 0) + (a.qrows ? 1 : 0)) {
-    case 0: k_patchq<1, P, NOC, MINW1, 0, false><<<grid, 256, lds, s>>>(a); return;
-    case 1: k_patchq<1, P, NOC, MINW1, 0, true><<<grid, 256, lds, s>>>(a); return;
-    case 2: k_patchq<2, P, NOC, MINW2, 0, false><<<grid, 256, lds, s>>>(a); return;
-    case 3: k_patchq<2, P, NOC, MINW2, 0, true><<<grid, 256, lds, s>>>(a); return;
-    case 4: k_patchq<1, P, NOC, MINW1, 1, false><<<grid, 256, lds, s>>>(a); return;
-    case 5: k_patchq<1, P, NOC, MINW1, 1, true><<<grid, 256, lds, s>>>(a); return;
-    case 6: k_patchq<2, P, NOC, MINW2, 1, false><<<grid, 256, lds, s>>>(a); return;
-    case 7: k_patchq<2, P, NOC, MINW2, 1, true><<<grid, 256, lds, s>>>(a); return;
-    case 8: k_patchq<1, P, NOC, MINW1, 2, false><<<grid, 256, lds, s>>>(a); return;
-    case 9: k_patchq<1, P, NOC, MINW1, 2, true><<<grid, 256, lds, s>>>(a); return;
-    case 10: k_patchq<2, P, NOC, MINW2, 2, false><<<grid, 256, lds, s>>>(a); return;
-    default: k_patchq<2, P, NOC, MINW2, 2, true><<<grid, 256, lds, s>>>(a); return;
+  switch (a.costfct * 2 + (a.nop == 2 ? 1 : 0)) {
+    case 0: k_patchq<1, P, NOC, MINW1, 0><<<grid, 256, lds, s>>>(a); return;
+    case 1: k_patchq<2, P, NOC, MINW2, 0><<<grid, 256, lds, s>>>(a); return;
+    case 2: k_patchq<1, P, NOC, MINW1, 1><<<grid, 256, lds, s>>>(a); return;
+    case 3: k_patchq<2, P, NOC, MINW2, 1><<<grid, 256, lds, s>>>(a); return;
+    case 4: k_patchq<1, P, NOC, MINW1, 2><<<grid, 256, lds, s>>>(a); return;
+    default: k_patchq<2, P, NOC, MINW2, 2><<<grid, 256, lds, s>>>(a); return;
   }
 }
 template <int P, int NOC, int MINW>

@@ -111,7 +111,6 @@ struct ofdis_context {
   int opt_patch_buf = 1;       // gray p = 12 windows by buffer loads (32-bit offsets) where the image array allows
   int opt_patch_generic = 0;   // 1: every shape on the any-shape patch kernel k_patchg (parity testing)
   int opt_patch_fdiv = 1;      // the LLT solves divide by FMA-corrected pivot reciprocals (0: IEEE divisions)
-  int opt_patch_qrows = 1;     // four-lane patches read each bilinear tap once per evaluation (0: four reads per pair)
   int opt_patch_maxres = 1;    // op-point stopping (res_thresh 0, min_iter = max_iter): largest |w| > 0 for mean > 0
   // sub-batch pipelining: chunks of `opt_chunk` frames round-robin over `opt_streams` streams, each with
   // its own workspace, so one chunk's latency-bound wavefront overlaps another chunk's streaming kernels.
@@ -423,7 +422,6 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     pa.absw = !P.fb && c->opt_patch_absw;  // usefbcon: the complementary grid's loss weights are read raw
     pa.aslots = (p->p_samp_s - 1) / steps + 1;
     pa.fdiv = c->opt_patch_fdiv;
-    pa.qrows = c->opt_patch_qrows;
     pa.maxres = c->opt_patch_maxres && pa.res_thresh == 0.0f && pa.min_iter >= pa.max_iter;
     pa.buf32 = c->opt_patch_buf && (size_t)n * fsp * sizeof(float) + 4096 <= 0xffffffffu;
     pa.generic = c->opt_patch_generic;
@@ -1340,7 +1338,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},  {"patch_fdiv", &ofdis_context::opt_patch_fdiv, 0, 1},
-      {"patch_maxres", &ofdis_context::opt_patch_maxres, 0, 1}, {"patch_qrows", &ofdis_context::opt_patch_qrows, 0, 1},
+      {"patch_maxres", &ofdis_context::opt_patch_maxres, 0, 1},
       {"sysor", &ofdis_context::opt_sysor, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };

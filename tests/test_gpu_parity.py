@@ -133,7 +133,6 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
     ("patch_fdiv", 0, 1),      # LLT solves by IEEE divisions instead of the FMA-corrected pivot reciprocals
     ("patch_maxres", 0, 1),    # op-point stopping test on the mean |w| instead of the largest |w|
-    ("patch_qrows", 0, 1),     # four-lane patches: four tap reads per value pair instead of once per window row
     ("up_form", 0, 1),         # flow upsample with the horizontal taps once per output row (round 4's kernel)
     ("up_form", 2, 1),         # ... once per source row, 8-row blocks
     ("sysor", 1, 0),           # levels <= 128 rows: system + SOR of an inner iteration in one launch (k_tv_sysor)
