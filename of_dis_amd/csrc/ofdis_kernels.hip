@@ -1905,6 +1905,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
         } else {
           if constexpr (MAXR) {
             abl = fmaxf(abl, fmaxf(fabsf(wv.x), fabsf(wv.y)));  // one v_max3_f32 with |.| modifiers per pair
+            asm volatile("" : "+v"(abl));  // (else the compiler pairs the pairs: v_max + half a v_max3 per pair)
           } else {
             abl = abl + fabsf(wv.x);
             abh = abh + fabsf(wv.y);
