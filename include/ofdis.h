@@ -236,9 +236,7 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        chunk ch - 1's, so chains never share the GPU while each overlaps the other streams' pyramid
  *                        and upsample;
  *   "chain_cus" (0..8, default 0): pipeline: the chain lanes run on the last that many eighths (complementary to
- *                        "split_cus" when the two add up to 8), 0 or 8 = all CUs;
- *   "prio" (0..2, default 0): pipeline, unmasked streams: 1 = the chain lanes at the device's greatest stream priority
- *                        and the streaming stream at its least, 2 = the streaming stream at the least only.
+ *                        "split_cus" when the two add up to 8), 0 or 8 = all CUs.
  * Setting any option drops the captured graph.  Unknown keys and out-of-range values return
  * OFDIS_ERR_INVALID_ARGUMENT.  Apart from "sor_mode", results never depend on these settings. */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);

@@ -120,8 +120,6 @@ struct ofdis_context {
                                      // chain lanes (DIS + TV), chunk ch on chain lane ch % L (0: off)
   int opt_split_cus = 0;             // pipeline: the streaming stream on this many eighths of the CUs (0: all)
   int opt_chain_cus = 0;             // pipeline: the chain lanes on the complementary eighths (0: all CUs)
-  int opt_prio = 0;                  // pipeline: stream priorities -- 1 chain lanes greatest and the streaming stream
-                                     // least, 2 the streaming stream least only (0: default priority everywhere)
   int opt_stagger = 0;               // round robin: chunk ch's chain starts after chunk ch - 1's
   std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
@@ -130,7 +128,6 @@ struct ofdis_context {
     size_t cap = 0;
     hipEvent_t done = nullptr;
     int mask = 0;  // CU mask the stream was created with: 0 none, +k the first k eighths, -k the last k eighths
-    int prio = 0;  // stream priority class it was created with: 0 default, 1 the device's greatest, 2 its least
   };
   std::vector<Lane> lanes;
   hipEvent_t entry = nullptr;
@@ -830,17 +827,15 @@ void cu_mask(int k, std::vector<uint32_t> &m) {
   }
 }
 
-// k lanes (stream, done event, workspace of `bytes`); masks[i] / prios[i] (when given): the CU mask and priority class of
-// lane i's stream, which is re-created when either differs from the one it has.
-int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *masks = nullptr,
-                 const std::vector<int> *prios = nullptr) {
+// k lanes (stream, done event, workspace of `bytes`); masks[i] (when given): the CU mask of lane i's stream, which is
+// re-created when it differs from the one it has.
+int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *masks = nullptr) {
   if ((int)c->lanes.size() < k) c->lanes.resize(k);
   if (!c->entry) HIP_OK(hipEventCreateWithFlags(&c->entry, hipEventDisableTiming));
   for (int i = 0; i < k; ++i) {
     auto &L = c->lanes[i];
     const int want = masks ? (*masks)[i] : L.mask;
-    const int wantp = prios ? (*prios)[i] : L.prio;
-    if (L.s && (L.mask != want || L.prio != wantp)) {  // a different CU mask or priority: a new stream (after all queued work)
+    if (L.s && L.mask != want) {  // a different CU mask: a new stream (after all queued work)
       int rc = drop_graph(c);
       if (rc) return rc;
       HIP_OK(hipDeviceSynchronize());
@@ -848,11 +843,7 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *
       L.s = nullptr;
     }
     if (!L.s) {
-      if (want == 0 && wantp != 0) {
-        int least = 0, greatest = 0;
-        HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_OK(hipStreamCreateWithPriority(&L.s, hipStreamNonBlocking, wantp == 1 ? greatest : least));
-      } else if (want == 0) {
+      if (want == 0) {
         HIP_OK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
       } else {
         std::vector<uint32_t> m;
@@ -860,7 +851,6 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *
         HIP_OK(hipExtStreamCreateWithCUMask(&L.s, (uint32_t)m.size(), m.data()));
       }
       L.mask = want;
-      L.prio = want == 0 ? wantp : 0;
     }
     if (!L.done) HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     if (L.cap < bytes) {
@@ -941,16 +931,12 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
   // the pipeline: chain lanes 0 .. L-1 (CU mask: the last opt_chain_cus eighths), workspaces of lanes 0 .. L (chunk ch
   // in workspace ch mod (L + 1)), the streaming stream = lane L (the first opt_split_cus eighths)
   cp.lanes = cp.kind == CallPlan::kPipeline ? c->opt_pipeline + 1 : std::min(nstreams, cp.nchunks);
-  std::vector<int> masks(cp.lanes, 0), prios(cp.lanes, 0);
+  std::vector<int> masks(cp.lanes, 0);
   if (cp.kind == CallPlan::kPipeline) {
-    for (int i = 0; i < c->opt_pipeline; ++i) {
-      masks[i] = c->opt_chain_cus > 0 && c->opt_chain_cus < 8 ? -c->opt_chain_cus : 0;
-      prios[i] = c->opt_prio == 1 ? 1 : 0;
-    }
+    for (int i = 0; i < c->opt_pipeline; ++i) masks[i] = c->opt_chain_cus > 0 && c->opt_chain_cus < 8 ? -c->opt_chain_cus : 0;
     masks[c->opt_pipeline] = c->opt_split_cus;
-    prios[c->opt_pipeline] = c->opt_prio ? 2 : 0;
-  }  // round robin: unmasked default-priority lanes (a lane a pipeline call changed gets a new stream)
-  int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total, &masks, &prios);
+  }  // round robin: unmasked lanes (a lane a pipeline call masked gets a new stream)
+  int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total, &masks);
   if (rc) return rc;
   if (cp.kind == CallPlan::kPipeline || c->opt_stagger)
     while ((int)c->pipe_ev.size() < 2 * cp.nchunks) {
@@ -1320,8 +1306,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   };
   static const Opt opts[] = {
       {"pipeline", &ofdis_context::opt_pipeline, 0, 4},     {"split_cus", &ofdis_context::opt_split_cus, 0, 7},
-      {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},   {"prio", &ofdis_context::opt_prio, 0, 2},
-        {"stagger", &ofdis_context::opt_stagger, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
+      {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},      {"stagger", &ofdis_context::opt_stagger, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},

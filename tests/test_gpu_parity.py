@@ -244,13 +244,11 @@ def test_batch_equals_singles(od, ctx):
     outs = []
     configs = ((1, 0, 1, 0), (1, 0, 1, 0), (1, 0, 0, 0), (3, 2, 1, 0), (4, 1, 1, 0), (3, 2, 2, 0), (3, 2, 2, 0),
                (1, 2, 1, 1), (1, 2, 1, 1), (1, 2, 0, 1), (1, 1, 1, 1), (1, 3, 0, 1), (1, 2, 2, 1),
-               (1, 1, 0, 2), (1, 2, 0, 3), (2, 1, 0, -1), (3, 2, 2, -1), (1, 2, 0, 11), (1, 1, 0, 22))
+               (1, 1, 0, 2), (1, 2, 0, 3), (2, 1, 0, -1), (3, 2, 2, -1))
     for streams, chunk, graph, pipeline in configs:
-        # pipeline > 1: that many chain lanes; -1: the staggered round robin (option stagger); 11 / 22: pipeline 1 / 2
-        # with stream priorities 1 / 2 (option prio)
+        # pipeline > 1: that many chain lanes; -1: the staggered round robin (option stagger)
         ctx.set_option("stagger", int(pipeline < 0))
-        ctx.set_option("prio", pipeline // 10 if pipeline >= 10 else 0)
-        pipeline = pipeline % 10 if pipeline >= 10 else max(pipeline, 0)
+        pipeline = max(pipeline, 0)
         # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams (also
         # captured with their fork / join); the two-stream pipeline (ragged last chunk; eager -- graph 2 under
         # torch's HIP runtime too, see test_pipeline_capture_native)
@@ -266,7 +264,6 @@ def test_batch_equals_singles(od, ctx):
     ctx.set_option("chunk", 0)
     ctx.set_option("pipeline", 0)
     ctx.set_option("stagger", 0)
-    ctx.set_option("prio", 0)
     for f in range(n):
         single = ctx.run_host(pairs[f][0], pairs[f][1], p)
         for k, out in enumerate(outs):
