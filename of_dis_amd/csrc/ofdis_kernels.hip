@@ -1986,8 +1986,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
       // of |w| >= 0 is positive iff its largest term is, and RN(sum / N) > 0 then too while that term is >= 2^-100.
       // So the evaluation keeps the largest |w| (one v_max3 per value pair instead of two adds, no division);
       // a wave with a NaN (b0 / b1 are NaN iff some residual is) or a term in (0, 2^-100) redoes it with the sum.
+      // (shapes whose value count is a power of two divide by a multiplication: there the two adds per pair it
+      // saves do not pay for the second evaluation copy's registers -- p = 8 spilled 11 VGPRs with it)
       bool summed = true;
-      if (a.maxres) {
+      if (!pow2 && a.maxres) {
         evaluate(r0, nullptr, std::integral_constant<int, 0>(), std::true_type());
         summed = false;
         const bool odd = (r0 > 0.0f && r0 < 0x1p-100f) || b0 != b0 || (NOP == 2 && b1 != b1);
