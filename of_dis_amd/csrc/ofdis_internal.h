@@ -140,6 +140,7 @@ struct UpArgs {
   float *out;         // [n][H0][W0][nop]
   int n, nop, wl, hl, log2s, W0, H0, offx, offy;
   int nt_store;       // non-temporal output stores (A/B option "nt_store")
+  int form;           // nop = 2: 0 k_upsample_rows, 1 k_upsample_h<4>, 2 k_upsample_h<8> (option "up_form")
 };
 
 // Initial flow (run_dense.cpp:356-379): full-resolution [n][H0][W0][nop] -> replicate-padded, x sc,

@@ -4608,6 +4608,135 @@ __global__ __launch_bounds__(256) void k_upsample_rows(UpArgs a) {
   }
 }
 
+// k_upsample_h<R>: the same output (same expressions, same lanes and stores) with each staged source row's
+// horizontal taps computed once per lane and column instead of once per output row that reads them
+// (VResizeLinear blends two HResizeLinear rows; at 2^l = 2 four output rows read four source rows, eight
+// horizontal evaluations before), and the staging copy in 16-byte groups with no per-element division:
+// B's upsample issued ~500 VALU per wave, 43 % of the whole pipeline's VALU (profiles/r05/s9).  R output rows
+// per block (4 or 8).  The staged window starts at the 4-aligned column below the first one the block reads.
+template <int R>
+__global__ __launch_bounds__(256) void k_upsample_h(UpArgs a) {
+  constexpr int NSR = R / 2 + 3;         // source rows a block can touch (2^l >= 2)
+  constexpr int SC = kUpCols / 2 + 8;    // staged columns per row (>= the 514 + 3 a block reads at 2^l = 2)
+  constexpr int S4 = SC / 4;             // 16-byte groups per staged row
+  __shared__ __attribute__((aligned(16))) float src[NSR][2][SC];
+  const int y0 = blockIdx.y * R, f = blockIdx.z;
+  const int dx0 = blockIdx.x * kUpCols + a.offx;
+  const int fct_i = 1 << a.log2s;
+  const float fct = (float)fct_i, half_inv = 1.0f / (float)(2 * fct_i);
+  const long plane = (long)a.wl * a.hl;
+  const float *F = a.flow + (long)f * 2 * plane;
+  auto src_row = [&](int dy, float &fy) {  // resizeGeneric_Invoker rows: sy, fy (weights not clamped)
+    fy = (float)(2 * dy + 1 - fct_i) * half_inv;
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    return sy;
+  };
+  auto clip_row = [&](int r) { return r >= 0 ? (r < a.hl ? r : a.hl - 1) : 0; };
+  const int yl = min(y0 + R, a.H0) - 1;
+  float dummy;
+  const int r_first = clip_row(src_row(y0 + a.offy, dummy));
+  const int r_last = clip_row(src_row(yl + a.offy, dummy) + 1);
+  const int nr = r_last - r_first + 1;
+  const int c_lo = max(0, (int)floorf((float)(2 * dx0 + 1 - fct_i) * half_inv));
+  const int c0 = c_lo & ~3;                                  // staged column 0
+  const int n4 = min(S4, (c_lo - c0 + kUpCols / fct_i + 2 + 3) >> 2);
+  const bool vec = (a.wl & 3) == 0 && ((uintptr_t)a.flow & 15) == 0;
+  for (int e = threadIdx.x; e < nr * 2 * S4; e += 256) {  // (row, comp) = e / S4: a division by a constant
+    const int rc = e / S4, j = e - rc * S4;
+    if (j >= n4) continue;
+    const int r = rc >> 1, comp = rc & 1, c = c0 + 4 * j;
+    const float *row = F + comp * plane + (long)(r_first + r) * a.wl;
+    v4f v;
+    if (vec && c + 3 < a.wl) {
+      v = *reinterpret_cast<const v4f *>(row + c);
+    } else {
+      v = v4f{row[min(c, a.wl - 1)], row[min(c + 1, a.wl - 1)], row[min(c + 2, a.wl - 1)], row[min(c + 3, a.wl - 1)]};
+    }
+    *reinterpret_cast<v4f *>(&src[r][comp][4 * j]) = v * fct;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int xb = blockIdx.x * kUpCols + wv * 256 + 2 * lane;
+  int xs[2] = {xb, xb + 128};
+  int cc[4];
+  float fxs[4], gxs[4];
+  bool lin[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int dx = xs[i >> 1] + (i & 1) + a.offx;
+    float fx = (float)(2 * dx + 1 - fct_i) * half_inv;
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    bool l = true;
+    if (sx + 1 >= a.wl) {
+      l = false;
+      if (sx >= a.wl - 1) { fx = 0; sx = a.wl - 1; }
+    }
+    cc[i] = min(max(sx - c0, 0), SC - 2);  // columns past W0 are computed, never stored
+    fxs[i] = fx;
+    gxs[i] = 1.f - fx;
+    lin[i] = l;
+  }
+  auto hrow = [&](int j, float *h) {  // HResizeLinear of staged row j at the lane's 4 columns, both components
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float s0 = src[j][k][cc[q]];
+        h[q * 2 + k] = lin[q] ? s0 * gxs[q] + src[j][k][cc[q] + 1] * fxs[q] : s0;
+      }
+  };
+  float ha[8], hb[8];
+  int ja = -1, jb = -1;  // staged rows held in ha / hb (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int y = y0 + i;
+    if (y >= a.H0) break;
+    float fy;
+    const int sy = src_row(y + a.offy, fy);
+    const int j0 = clip_row(sy) - r_first, j1 = clip_row(sy + 1) - r_first;
+    if (j0 != ja) {
+      if (j0 == jb) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) ha[t] = hb[t];
+      } else {
+        hrow(j0, ha);
+      }
+      ja = j0;
+    }
+    if (j1 != jb) {
+      if (j1 == ja) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) hb[t] = ha[t];
+      } else {
+        hrow(j1, hb);
+      }
+      jb = j1;
+    }
+    const float b0 = 1.f - fy, b1 = fy;
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = ha[t] * b0 + hb[t] * b1;
+    float *orow = a.out + ((long)f * a.H0 + y) * a.W0 * 2;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int x = xs[hh];
+      if (x + 2 <= a.W0) {
+        const v4f val = v4f{v[4 * hh], v[4 * hh + 1], v[4 * hh + 2], v[4 * hh + 3]};
+        if (a.nt_store)
+          __builtin_nontemporal_store(val, reinterpret_cast<v4f *>(orow + 2 * x));
+        else
+          *reinterpret_cast<v4f *>(orow + 2 * x) = val;
+      } else if (x < a.W0) {
+        orow[2 * x] = v[4 * hh];
+        orow[2 * x + 1] = v[4 * hh + 1];
+      }
+    }
+  }
+}
+
 // The same for depth (nop = 1): lane i of wave wv owns the four output columns xb + 4i .. xb + 4i + 3
 // (xb = block + 256 wv): one 16-byte store per row, 1 KiB contiguous per wave-instruction.
 __global__ __launch_bounds__(256) void k_upsample_rows1(UpArgs a) {
@@ -5140,7 +5269,12 @@ void launch_init_area(const InitArgs &a, hipStream_t s) {
 
 void launch_upsample(const UpArgs &a, hipStream_t s) {
   if (a.nop == 2 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0) {
-    k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
+    if (a.form == 2)
+      k_upsample_h<8><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 8), a.n), 256, 0, s>>>(a);
+    else if (a.form == 1)
+      k_upsample_h<4><<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, 4), a.n), 256, 0, s>>>(a);
+    else
+      k_upsample_rows<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
   } else if (a.nop == 1 && a.log2s >= 1 && a.log2s <= 9 && (a.W0 % 4) == 0 && ((uintptr_t)a.out % 16) == 0)
     k_upsample_rows1<<<dim3(ceil_div(a.W0, kUpCols), ceil_div(a.H0, kUpRows), a.n), 256, 0, s>>>(a);
   else

@@ -79,6 +79,7 @@ struct ofdis_context {
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
+  int opt_up_form = 1;         // flow upsample: 0 per-output-row horizontal taps, 1 / 2 once per source row (4 / 8 rows)
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   // the fused launch on 2-D tiles for tall levels: 1 on, 0 off (two launches there), 2 auto = on for calls of
   // fewer than 512 pairs (one stream).  Measured at config E: alone on the GPU it cuts the system time 10 %
@@ -771,6 +772,7 @@ int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *
   up.offx = P.padl;
   up.offy = P.padt;
   up.nt_store = c->opt_nt_store;
+  up.form = c->opt_up_form;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
@@ -1315,7 +1317,8 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
-      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"graph", &ofdis_context::opt_graph, 0, 3},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 2},
+      {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},

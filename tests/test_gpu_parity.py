@@ -133,6 +133,8 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
     ("patch_fdiv", 0, 1),      # LLT solves by IEEE divisions instead of the FMA-corrected pivot reciprocals
     ("patch_maxres", 0, 1),    # op-point stopping test on the mean |w| instead of the largest |w|
+    ("up_form", 0, 1),         # flow upsample with the horizontal taps once per output row (round 4's kernel)
+    ("up_form", 2, 1),         # ... once per source row, 8-row blocks
     ("sysor", 1, 0),           # levels <= 128 rows: system + SOR of an inner iteration in one launch (k_tv_sysor)
 ]
 
@@ -328,14 +330,20 @@ def test_full_1080p_bitexact(oracle, od, ctx):
     assert_bitexact(got, ref, "1080p op2")
 
 
+@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("w,h,op,over", [(1920, 1080, 2, {}), (1000, 562, 2, {}), (330, 250, 1, {}),
                                          (640, 480, 2, {"sc_l": 2}), (2100, 70, 2, {"sc_l": 1, "sc_f": 2})])
-def test_upsample_sizes_bitexact(oracle, od, ctx, w, h, op, over):
-    """The optical-flow upsample at 2^l = 2 / 4 / 8 / 16, cropped divisibility padding, several 1024-column blocks
-    and a partial last one: the full-resolution flow is the oracle's."""
+def test_upsample_forms_bitexact(oracle, od, ctx, form, w, h, op, over):
+    """Every optical-flow upsample kernel (up_form) at 2^l = 2 / 4 / 8, cropped divisibility padding, several
+    1024-column blocks and a partial last one: the full-resolution flow is the oracle's."""
     a, b = od.synth_pair(w, h, 1, 9, 1)
     p, q = _params(od, oracle, w, 1, 1, op, over)
-    assert_bitexact(ctx.run_host(a, b, p), oracle.run_u8(a, b, q), "upsample")
+    ctx.set_option("up_form", form)
+    try:
+        got = ctx.run_host(a, b, p)
+    finally:
+        ctx.set_option("up_form", 1)
+    assert_bitexact(got, oracle.run_u8(a, b, q), f"up_form={form}")
 
 
 def test_pipeline_capture_native(od, tmp_path):
