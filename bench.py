@@ -471,6 +471,10 @@ def main():
         # measured 2x rocprofv3's kernel durations)
         ctx.set_option("streams", 1)
         ctx.set_option("chunk", chunk_eff)
+        # the upsample kernel the timed region ran (up_form auto follows the call's lanes, which this pass changes)
+        up_user = any(o.split("=")[0] == "up_form" for o in args.option)
+        if not up_user:
+            ctx.set_option("up_form", 1 if min(streams_eff, -(-B // chunk_eff)) >= 2 else 0)
         ctx.enable_kernel_timing(True)
         for _ in range(args.steps):
             step()
@@ -489,6 +493,8 @@ def main():
         ctx.enable_kernel_timing(False)
         ctx.set_option("streams", args.streams)
         ctx.set_option("chunk", args.chunk)
+        if not up_user:
+            ctx.set_option("up_form", 3)
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         roofline = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, dom)
         if dom != "tv_sor" and "tv_sor" in kernels:  # the north-star kernel, reported beside the dominant one

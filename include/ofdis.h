@@ -210,8 +210,10 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "patch_generic" (0/1, default 0): every patch shape on the any-shape kernel (runtime value loops: the
  *                        default for p*p*noc > 448, e.g. RGB p >= 14, gray p >= 22);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
- *   "up_form" (0..2, default 1): optical-flow upsample: 1 / 2 = each staged source row's horizontal taps once per
- *                        column for blocks of 4 / 8 output rows, 0 = once per output row that reads them (round 4);
+ *   "up_form" (0..3, default 3): optical-flow upsample: 1 / 2 = each staged source row's horizontal taps once per
+ *                        column for blocks of 4 / 8 output rows, 0 = once per output row that reads them (round 4),
+ *                        3 = 1 for calls whose chunks run on two or more streams, else 0 (the faster of the two in
+ *                        each regime, measured);
  *   "graph" (0/1/2/3, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
  *                        parameters repeat (re-captured when they change); 1 captures single-stream
  *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined; the

@@ -79,7 +79,10 @@ struct ofdis_context {
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
-  int opt_up_form = 1;         // flow upsample: 0 per-output-row horizontal taps, 1 / 2 once per source row (4 / 8 rows)
+  // flow upsample: 0 per-output-row horizontal taps (k_upsample_rows), 1 / 2 once per staged source row (k_upsample_h,
+  // 4 / 8 rows), 3 auto: 1 when the call runs on two or more lanes, else 0 -- B on one box (profiles/r05/s19): two
+  // streams 310.4k (0) vs 327.7-328.2k (1), one stream 306.8k (0) vs 294.6k (1)
+  int opt_up_form = 3;
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   // the fused launch on 2-D tiles for tall levels: 1 on, 0 off (two launches there), 2 auto = on for calls of
   // fewer than 512 pairs (one stream).  Measured at config E: alone on the GPU it cuts the system time 10 %
@@ -92,6 +95,7 @@ struct ofdis_context {
   int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
   int opt_smsys_deriv = 1;     // fused smoothness + system (gray; colour: the march): second derivatives filtered from Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
+  int call_lanes = 1;          // streams the current call's chunks run on (auto options)
   int opt_sor_cring = 2;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients;
                                // 2: ring sized to the level's row groups (28-byte OF entries in throughput
                                // launches where they fit more frames per CU; the in-frame load select in launches
@@ -772,7 +776,7 @@ int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *
   up.offx = P.padl;
   up.offy = P.padt;
   up.nt_store = c->opt_nt_store;
-  up.form = c->opt_up_form;
+  up.form = c->opt_up_form == 3 ? (c->call_lanes >= 2 ? 1 : 0) : c->opt_up_form;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
@@ -910,6 +914,7 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
             CallPlan &cp) {
   cp.n = n;
   c->call_frames = n;
+  c->call_lanes = 1;
   cp.width = width;
   cp.height = height;
   cp.init = init;
@@ -933,6 +938,7 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
   // the pipeline: chain lanes 0 .. L-1 (CU mask: the last opt_chain_cus eighths), workspaces of lanes 0 .. L (chunk ch
   // in workspace ch mod (L + 1)), the streaming stream = lane L (the first opt_split_cus eighths)
   cp.lanes = cp.kind == CallPlan::kPipeline ? c->opt_pipeline + 1 : std::min(nstreams, cp.nchunks);
+  c->call_lanes = cp.lanes;
   std::vector<int> masks(cp.lanes, 0);
   if (cp.kind == CallPlan::kPipeline) {
     for (int i = 0; i < c->opt_pipeline; ++i) masks[i] = c->opt_chain_cus > 0 && c->opt_chain_cus < 8 ? -c->opt_chain_cus : 0;
@@ -1317,7 +1323,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
-      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 2},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},
       {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},

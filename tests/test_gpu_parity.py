@@ -133,8 +133,9 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("patch_buf", 0, 1),       # gray p = 12 windows by global loads instead of buffer loads
     ("patch_fdiv", 0, 1),      # LLT solves by IEEE divisions instead of the FMA-corrected pivot reciprocals
     ("patch_maxres", 0, 1),    # op-point stopping test on the mean |w| instead of the largest |w|
-    ("up_form", 0, 1),         # flow upsample with the horizontal taps once per output row (round 4's kernel)
-    ("up_form", 2, 1),         # ... once per source row, 8-row blocks
+    ("up_form", 0, 3),         # flow upsample with the horizontal taps once per output row (round 4's kernel)
+    ("up_form", 1, 3),         # ... once per source row, 4-row blocks
+    ("up_form", 2, 3),         # ... once per source row, 8-row blocks
     ("sysor", 1, 0),           # levels <= 128 rows: system + SOR of an inner iteration in one launch (k_tv_sysor)
 ]
 
@@ -342,7 +343,7 @@ def test_upsample_forms_bitexact(oracle, od, ctx, form, w, h, op, over):
     try:
         got = ctx.run_host(a, b, p)
     finally:
-        ctx.set_option("up_form", 1)
+        ctx.set_option("up_form", 3)
     assert_bitexact(got, oracle.run_u8(a, b, q), f"up_form={form}")
 
 
