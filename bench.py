@@ -72,7 +72,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample per leg (1 core, all cores; 0 = skip)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="HIP streams the batch's chunks round-robin over (0 = the library's auto: 2 from 512 pairs)")
+                    help="HIP streams the batch's chunks round-robin over (0 = the library's auto: 2 from 256 pairs)")
     ap.add_argument("--chunk", type=int, default=0, help="frames per chunk (0 = the batch split over the streams)")
     ap.add_argument("--option", action="append", default=[], help="context option key=value (A/B runs)")
     ap.add_argument("--host-io", action="store_true",
@@ -393,8 +393,8 @@ def main():
     ctx = od.Context(dev.index)
     ctx.set_option("streams", args.streams)
     ctx.set_option("chunk", args.chunk)
-    # the library's chunking (ofdis_runtime.cpp stream_count): streams 0 = 2 from 512 pairs, else 1
-    streams_eff = args.streams or (2 if B >= 512 else 1)
+    # the library's chunking (ofdis_runtime.cpp stream_count): streams 0 = 2 from 256 pairs, else 1
+    streams_eff = args.streams or (2 if B >= 256 else 1)
     chunk_eff = min(B, args.chunk or -(-B // streams_eff))
     for kv in args.option:
         k, v = kv.split("=")

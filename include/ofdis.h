@@ -220,7 +220,7 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        two-stream pipeline only under a HIP runtime >= 7.2: the one bundled with
  *                        PyTorch's ROCm 7.0 build crashes capturing its mutually waiting lanes, so there
  *                        it is issued eagerly); 3 captures the pipeline whatever the runtime (diagnostic);
- *   "streams" (0-16, default 0 = automatic: 2 from 512 pairs, else 1): a batch is cut into chunks that run
+ *   "streams" (0-16, default 0 = automatic: 2 from 256 pairs, else 1): a batch is cut into chunks that run
  *                        round-robin on that many HIP streams with separate workspaces, overlapping one
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);

@@ -888,7 +888,8 @@ bool pipeline_capture_ok() {
   return ok;
 }
 
-int stream_count(const ofdis_context *c, int n) { return c->opt_streams > 0 ? c->opt_streams : (n >= 512 ? 2 : 1); }
+// two lanes from 256 pairs (config D, 256 pairs: 223.4-223.7k on one stream, 225.3-226.8k on two; profiles/r05/s22)
+int stream_count(const ofdis_context *c, int n) { return c->opt_streams > 0 ? c->opt_streams : (n >= 256 ? 2 : 1); }
 
 // Frames per launch such that every TV plane group (n * noc * sp floats, addressed with 32-bit byte
 // offsets by the system kernels' ldu) stays below 2^30 floats.

@@ -424,7 +424,7 @@ def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode, over):
 
 
 def test_auto_two_streams_bitexact(oracle, od, ctx):
-    """From 512 pairs the library splits the batch over two streams by default (ofdis_runtime.cpp
+    """From 256 pairs the library splits the batch over two streams by default (ofdis_runtime.cpp
     stream_count): every frame equals the one-stream whole-batch result, and frames of both chunks equal
     the oracle."""
     import torch
@@ -483,7 +483,7 @@ def test_cli_stdout_timers(od, tmp_path):
 
 
 def test_capture_on_large_batch(oracle, od, ctx):
-    """A stage capture on a batch that would be chunked over two streams (>= 512 pairs, and with explicit
+    """A stage capture on a batch that would be chunked over two streams (>= 256 pairs, and with explicit
     stream / chunk options) runs as one launch and captures frame 0 exactly."""
     import torch
     w, h, n = 96, 64, 520
