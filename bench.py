@@ -474,7 +474,7 @@ def main():
         # the upsample kernel the timed region ran (up_form auto follows the call's lanes, which this pass changes)
         up_user = any(o.split("=")[0] == "up_form" for o in args.option)
         if not up_user:
-            ctx.set_option("up_form", 1 if min(streams_eff, -(-B // chunk_eff)) >= 2 else 0)
+            ctx.set_option("up_form", 1 if min(streams_eff, -(-B // chunk_eff)) >= 2 and W >= 1024 else 0)
         ctx.enable_kernel_timing(True)
         for _ in range(args.steps):
             step()
