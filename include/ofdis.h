@@ -274,8 +274,10 @@ int ofdis_read_pnm(const char *path, uint8_t *pixels, int *width, int *height, i
 /* cv::imread(path, want_noc == 1 ? CV_LOAD_IMAGE_GRAYSCALE : CV_LOAD_IMAGE_COLOR) (run_dense.cpp:202-206)
  * for PNG (zlib inflate; gray / RGB / palette / alpha, 1-16 bit, Adam7; libpng's transform chain as
  * OpenCV configures it, incl. png_set_rgb_to_gray(0.299, 0.587)) and Netpbm P1-P6 (colour -> gray with
- * OpenCV's fixed-point BGR2Gray).  Output [h][w][want_noc], BGR for 3.  pixels may be NULL to query the
- * size.  OFDIS_ERR_UNSUPPORTED for other formats (JPEG, BMP, ...), OFDIS_ERR_IO for corrupt files. */
+ * OpenCV's fixed-point BGR2Gray) and BMP (BmpDecoder: 1/4/8-bit palette, 16-bit 555 / 565, 24-bit, 32-bit,
+ * core / info / V4 / V5 headers, bottom-up or top-down; colour -> gray by the same BGR2Gray).  Output
+ * [h][w][want_noc], BGR for 3.  pixels may be NULL to query the size.  OFDIS_ERR_UNSUPPORTED for other formats
+ * (JPEG, TIFF, RLE-compressed BMP, ...), OFDIS_ERR_IO for corrupt files. */
 int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height, int want_noc, size_t capacity);
 
 /* Deterministic synthetic frame pair: band-limited texture + noise, frame b is frame

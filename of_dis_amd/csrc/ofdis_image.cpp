@@ -1,6 +1,6 @@
 // ofdis_image.cpp -- the on-disk image formats on the input side of the path: what run_dense.cpp's
 // cv::imread(path, CV_LOAD_IMAGE_GRAYSCALE / CV_LOAD_IMAGE_COLOR) (run_dense.cpp:202-206) returns, for
-// PNG and the Netpbm family, without OpenCV or libpng (neither is in the image; zlib is).
+// PNG, the Netpbm family and BMP, without OpenCV or libpng (neither is in the image; zlib is).
 //
 // Restated semantics (OpenCV 3.x/4.x grfmt_png.cpp / grfmt_pxm.cpp over libpng 1.6; both absent here, so
 // parity with them is unpinned and pinned instead by tests/test_image_io.py's independent decodes):
@@ -14,6 +14,7 @@
 //   PNM  P1-P6 (ASCII and binary bitmaps / graymaps / pixmaps), maxval <= 255 taken as is, 65535 -> high
 //        byte; colour -> gray by OpenCV's fixed-point icvCvt_BGR2Gray_8u_C3C1R
 //        ((1868 B + 9617 G + 4899 R + 8192) >> 14); colour output is BGR.
+//   BMP  OpenCV's BmpDecoder (grfmt_bmp.cpp): see decode_bmp.
 #include <zlib.h>
 
 #include <cmath>
@@ -358,6 +359,126 @@ int decode_pnm(const std::vector<uint8_t> &f, int want, Image &img) {
   return OFDIS_OK;
 }
 
+// ------------------------------------------------------------------------------------------- BMP
+// OpenCV's BmpDecoder (grfmt_bmp.cpp), restated: BITMAPINFOHEADER and its V4 / V5 extensions (40 / 108 / 124-byte
+// headers) and the OS/2 BITMAPCOREHEADER (12 bytes, 3-byte palette entries); 1 / 4 / 8-bit palette images,
+// 16-bit 5-5-5 (BI_RGB, or BI_BITFIELDS with those masks) and 5-6-5 (BI_BITFIELDS), 24-bit BGR and 32-bit BGRX
+// (BI_RGB or BI_BITFIELDS with the standard masks: alpha dropped); bottom-up rows unless the height is negative,
+// rows padded to 4 bytes.  Colour output is the stored BGR (5-bit fields as (v << 3) & 0xf8 -- no bit
+// replication, icvCvt_BGR5552BGR_8u_C2C3R / icvCvt_BGR5652BGR_8u_C2C3R); gray output is the fixed-point
+// icvCvt_BGR2Gray_8u ((1868 B + 9617 G + 4899 R + 8192) >> 14) of those values -- of the palette entries for
+// palette images (CvtPaletteToGray).  RLE4 / RLE8 and other masks: OFDIS_ERR_UNSUPPORTED.
+inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+inline uint16_t le16(const uint8_t *p) { return (uint16_t)(p[0] | p[1] << 8); }
+
+int decode_bmp(const std::vector<uint8_t> &f, int want, Image &img) {
+  if (f.size() < 26 || f[0] != 'B' || f[1] != 'M') return OFDIS_ERR_IO;
+  const uint32_t off = le32(&f[10]), hsz = le32(&f[14]);
+  int64_t w, h;
+  int bpp;
+  uint32_t comp = 0, nclr = 0;
+  size_t pal_at, pal_entry;
+  if (hsz == 12) {  // BITMAPCOREHEADER
+    w = le16(&f[18]);
+    h = (int16_t)le16(&f[20]);
+    bpp = le16(&f[24]);
+    pal_at = 14 + 12;
+    pal_entry = 3;
+  } else if (hsz == 40 || hsz == 52 || hsz == 56 || hsz == 108 || hsz == 124) {
+    if (f.size() < 14 + 40) return OFDIS_ERR_IO;
+    w = (int32_t)le32(&f[18]);
+    h = (int32_t)le32(&f[22]);
+    bpp = le16(&f[28]);
+    comp = le32(&f[30]);
+    nclr = le32(&f[46]);
+    pal_at = 14 + hsz;
+    pal_entry = 4;
+  } else {
+    return OFDIS_ERR_UNSUPPORTED;
+  }
+  const bool top_down = h < 0;
+  if (top_down) h = -h;
+  if (w <= 0 || h <= 0 || (uint64_t)w * (uint64_t)h > kMaxImagePixels) return OFDIS_ERR_IO;
+  // pixel format
+  enum { kPal, k555, k565, k24, k32 } fmt;
+  if (bpp == 1 || bpp == 4 || bpp == 8) {
+    if (comp != 0) return OFDIS_ERR_UNSUPPORTED;  // RLE8 / RLE4
+    fmt = kPal;
+  } else if (bpp == 16 || bpp == 32) {
+    uint32_t rm = bpp == 16 ? 0x7c00 : 0xff0000, gm = bpp == 16 ? 0x03e0 : 0xff00, bm = bpp == 16 ? 0x001f : 0xff;
+    if (comp == 3) {  // BI_BITFIELDS: masks after the 40-byte header (or inside a V4 / V5 header)
+      if (hsz < 40 || f.size() < 14 + 40 + 12) return OFDIS_ERR_IO;
+      rm = le32(&f[54]);
+      gm = le32(&f[58]);
+      bm = le32(&f[62]);
+      if (hsz == 40) pal_at += 12;
+    } else if (comp != 0) {
+      return OFDIS_ERR_UNSUPPORTED;
+    }
+    if (bpp == 16 && rm == 0x7c00 && gm == 0x03e0 && bm == 0x001f) fmt = k555;
+    else if (bpp == 16 && rm == 0xf800 && gm == 0x07e0 && bm == 0x001f) fmt = k565;
+    else if (bpp == 32 && rm == 0xff0000 && gm == 0xff00 && bm == 0xff) fmt = k32;
+    else return OFDIS_ERR_UNSUPPORTED;
+  } else if (bpp == 24) {
+    if (comp != 0) return OFDIS_ERR_UNSUPPORTED;
+    fmt = k24;
+  } else {
+    return OFDIS_ERR_UNSUPPORTED;
+  }
+  // palette (BGR[X] entries): clrUsed or 2^bpp of them
+  uint8_t pal[256][3] = {};
+  if (fmt == kPal) {
+    const uint32_t n = nclr ? nclr : (1u << bpp);
+    if (n > 256 || pal_at + (size_t)n * pal_entry > f.size()) return OFDIS_ERR_IO;
+    for (uint32_t i = 0; i < n; ++i)
+      for (int k = 0; k < 3; ++k) pal[i][k] = f[pal_at + i * pal_entry + k];
+  }
+  const size_t stride = (((size_t)w * bpp + 31) / 32) * 4;
+  if (off >= f.size() || off + stride * (size_t)h > f.size()) return OFDIS_ERR_IO;
+  img.w = (int)w;
+  img.h = (int)h;
+  img.c = want;
+  img.px.assign((size_t)w * h * want, 0);
+  auto put = [&](size_t i, unsigned b, unsigned g, unsigned r) {
+    if (want == 3) {
+      img.px[3 * i] = (uint8_t)b;
+      img.px[3 * i + 1] = (uint8_t)g;
+      img.px[3 * i + 2] = (uint8_t)r;
+    } else {
+      img.px[i] = (uint8_t)((b * 1868u + g * 9617u + r * 4899u + 8192u) >> 14);
+    }
+  };
+  for (int64_t y = 0; y < h; ++y) {
+    const uint8_t *row = &f[off + stride * (size_t)(top_down ? y : h - 1 - y)];
+    for (int64_t x = 0; x < w; ++x) {
+      const size_t i = (size_t)y * w + x;
+      switch (fmt) {
+        case kPal: {
+          unsigned idx;
+          if (bpp == 8) idx = row[x];
+          else if (bpp == 4) idx = (row[x >> 1] >> ((x & 1) ? 0 : 4)) & 15;
+          else idx = (row[x >> 3] >> (7 - (x & 7))) & 1;
+          put(i, pal[idx][0], pal[idx][1], pal[idx][2]);
+          break;
+        }
+        case k555: {
+          const unsigned t = le16(row + 2 * x);
+          put(i, (t << 3) & 0xf8, (t >> 2) & 0xf8, (t >> 7) & 0xf8);
+          break;
+        }
+        case k565: {
+          const unsigned t = le16(row + 2 * x);
+          put(i, (t << 3) & 0xf8, (t >> 3) & 0xfc, (t >> 8) & 0xf8);
+          break;
+        }
+        case k24: put(i, row[3 * x], row[3 * x + 1], row[3 * x + 2]); break;
+        case k32: put(i, row[4 * x], row[4 * x + 1], row[4 * x + 2]); break;
+      }
+    }
+  }
+  return OFDIS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -373,6 +494,8 @@ int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height,
       rc = decode_png(f, want_noc, img);
     else if (f.size() >= 2 && f[0] == 'P' && f[1] >= '1' && f[1] <= '6')
       rc = decode_pnm(f, want_noc, img);
+    else if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M')
+      rc = decode_bmp(f, want_noc, img);
     else
       rc = OFDIS_ERR_UNSUPPORTED;
     if (rc) return rc;

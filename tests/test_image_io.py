@@ -289,3 +289,94 @@ def test_pnm_red_anchor_and_16bit(tmp_path):
     v = np.array([[0x1234, 0xFFFF, 0x00FF]], ">u2")
     (tmp_path / "w.pgm").write_bytes(b"P5\n3 1\n65535\n" + v.tobytes())
     assert read(tmp_path / "w.pgm", 1)[0, :, 0].tolist() == [0x12, 0xFF, 0x00]
+
+
+# ----------------------------------------------------------------------------- BMP (OpenCV BmpDecoder semantics)
+
+def encode_bmp(kind, bgr, idx=None, palette=None, top_down=False, header=40):
+    """An independent BMP writer: kind in pal1/pal4/pal8 (idx [h][w], palette [n][3] BGR), 555, 565, 24, 32
+    (bgr [h][w][3], low bits ignored by the 16-bit packing); header 40 (INFO), 124 (V5) or 12 (CORE)."""
+    h, w = (idx if idx is not None else bgr).shape[:2]
+    bpp = {"pal1": 1, "pal4": 4, "pal8": 8, "555": 16, "565": 16, "24": 24, "32": 32}[kind]
+    stride = ((w * bpp + 31) // 32) * 4
+    rows = []
+    for y in range(h):
+        if kind.startswith("pal"):
+            vals = idx[y].astype(np.uint8)
+            if bpp == 8:
+                r = vals.tobytes()
+            elif bpp == 4:
+                v = np.concatenate([vals, np.zeros(len(vals) % 2, np.uint8)])
+                r = ((v[0::2] << 4) | v[1::2]).astype(np.uint8).tobytes()
+            else:
+                r = np.packbits(vals.astype(np.uint8)).tobytes()
+        elif kind in ("555", "565"):
+            b, g, rr = (bgr[y, :, k].astype(np.uint16) for k in range(3))
+            t = (b >> 3) | ((g >> 3) << 5) | ((rr >> 3) << 10) if kind == "555" else (b >> 3) | ((g >> 2) << 5) | ((rr >> 3) << 11)
+            r = t.astype("<u2").tobytes()
+        elif kind == "24":
+            r = bgr[y].astype(np.uint8).tobytes()
+        else:
+            r = np.concatenate([bgr[y], np.full((w, 1), 7, np.uint8)], 1).astype(np.uint8).tobytes()
+        rows.append(r + b"\0" * (stride - len(r)))
+    if not top_down:
+        rows = rows[::-1]
+    pix = b"".join(rows)
+    comp = 3 if kind == "565" else 0
+    masks = struct.pack("<III", 0xF800, 0x07E0, 0x001F) if kind == "565" else b""
+    pal = b""
+    if kind.startswith("pal"):
+        ent = 3 if header == 12 else 4
+        pal = b"".join(bytes(list(c)) + (b"" if ent == 3 else b"\0") for c in palette)
+    if header == 12:
+        dib = struct.pack("<IHHHH", 12, w, h, 1, bpp)
+    else:
+        dib = struct.pack("<IiiHHIIiiII", header, w, -h if top_down else h, 1, bpp, comp, len(pix), 2835, 2835,
+                          len(palette) if palette is not None else 0, 0)
+        if header > 40:
+            dib += (masks + b"\0" * (header - 40))[: header - 40]
+            masks = b""
+    off = 14 + len(dib) + len(masks) + len(pal)
+    return b"BM" + struct.pack("<IHHI", off + len(pix), 0, 0, off) + dib + masks + pal + pix
+
+
+@pytest.mark.parametrize("kind", ["pal1", "pal4", "pal8", "555", "565", "24", "32"])
+@pytest.mark.parametrize("top_down,header", [(False, 40), (True, 40), (False, 124), (False, 12)])
+@pytest.mark.parametrize("want", [1, 3])
+def test_bmp(tmp_path, kind, top_down, header, want):
+    if header == 12 and (kind in ("555", "565", "32") or top_down):
+        pytest.skip("OS/2 core headers: palette and 24-bit images, bottom-up")
+    rng = np.random.default_rng(len(kind) + header)
+    h, w = 7, 13
+    idx = palette = None
+    if kind.startswith("pal"):
+        n = {"pal1": 2, "pal4": 16, "pal8": 256}[kind]
+        palette = rng.integers(0, 256, (n, 3))
+        idx = rng.integers(0, n, (h, w))
+        bgr = palette[idx]
+    else:
+        bgr = rng.integers(0, 256, (h, w, 3))
+        if kind == "555":
+            bgr = bgr & 0xF8
+        elif kind == "565":
+            bgr = bgr & np.array([0xF8, 0xFC, 0xF8])
+    path = tmp_path / "i.bmp"
+    path.write_bytes(encode_bmp(kind, bgr, idx, palette, top_down, header))
+    got = read(path, want)
+    b, g, r = (bgr[..., k].astype(np.int64) for k in range(3))
+    ex = np.stack([b, g, r], -1) if want == 3 else ((1868 * b + 9617 * g + 4899 * r + 8192) >> 14)[..., None]
+    assert np.array_equal(got, ex.astype(np.uint8)), (kind, top_down, header, want)
+
+
+def test_bmp_refused_forms(tmp_path):
+    bgr = np.zeros((2, 3, 3), np.uint8)
+    data = bytearray(encode_bmp("24", bgr))
+    data[30:34] = struct.pack("<I", 1)  # BI_RLE8
+    (tmp_path / "rle.bmp").write_bytes(bytes(data))
+    with pytest.raises(_lib.OfdisError) as e:
+        read(tmp_path / "rle.bmp", 3)
+    assert e.value.code == _lib.ERR_UNSUPPORTED
+    (tmp_path / "short.bmp").write_bytes(encode_bmp("24", bgr)[:-5])
+    with pytest.raises(_lib.OfdisError) as e:
+        read(tmp_path / "short.bmp", 3)
+    assert e.value.code == _lib.ERR_IO
