@@ -127,7 +127,6 @@ struct TvArgs {
   int smsys_prefetch;          // k_tv_smsys, intensity images: derivative images loaded before the staging
   int smsys_small;             // k_tv_smsys: ~1 pixel per thread when a launch cannot fill the chip
   int smsys_march;             // tall levels: the register march k_tv_smsys_m (takes precedence over smsys2d)
-  int march_ring;              // k_tv_smsys_m: rows in five-slot rings, loop unrolled five times (0: rotated registers)
   int smsys_deriv;             // row-block k_tv_smsys, intensity images: Ixx .. Iyz computed from staged Ix, Iy, Iz
                                // (k_tv_prepd then writes only Ix, Iy, Iz of the derivative planes); set by the
                                // runtime only where tv_deriv_fused() holds

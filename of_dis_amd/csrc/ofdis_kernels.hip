@@ -3259,7 +3259,7 @@ __device__ __forceinline__ float conv5_clamp(const float (&t)[5], int pos, int n
 // Ix, Iy, Iz (of every channel) in registers and filters the five second derivatives of row r itself: a horizontal
 // tap x + k is row r + k of the same lane, a vertical tap y + k row r + k of lane + k (DPP shifts); k_tv_prepd then
 // writes 3 of the 8 derivative planes per channel, and a step reads 5 (colour: 11) planes instead of 10 (26).
-template <int NOP, int NOC, bool DF = false, bool RING = true>
+template <int NOP, int NOC, bool DF = false>
 __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
   const int w = a.w, h = a.h, rows = smsys_rows(w, h, a.wrap);
   const int nstrip = march_strips(h), nseg = march_segments(rows);
@@ -3339,7 +3339,6 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
     }
     return q;
   };
-  if constexpr (!RING) {
   Drow D0{}, D1{}, D2{}, D3{}, D4{};  // DF: rows r - 2 .. r + 2
   if constexpr (DF) {
     D0 = load_d(R0 - 2);
@@ -3435,111 +3434,6 @@ __global__ __launch_bounds__(256) void k_tv_smsys_m(TvArgs a) {
     U1 = U2;
     Sm = S0;
     S0 = S1;
-  }
-  } else {
-  // Rows live in rings of five slots -- row q in slot (q - R0 + 10) mod 5 -- for the derivative window (rows r - 2 ..
-  // r + 2), the flow rows (r - 1 .. r + 2) and s (r - 1 .. r + 1), and the loop is unrolled five times so every slot
-  // index is a compile-time constant: no register rotation per row (it was ~90 v_mov per row step of the DE march,
-  // ~14 % of its VALU).
-  Drow D[5] = {};
-  Row U[5] = {};
-  float S[5] = {};
-  if constexpr (DF) {
-    D[3] = load_d(R0 - 2);
-    D[4] = load_d(R0 - 1);
-    D[0] = load_d(R0);
-    D[1] = load_d(R0 + 1);
-  }
-  U[4] = load_row(R0 - 1);
-  U[0] = load_row(R0);
-  U[1] = load_row(R0 + 1);
-  S[4] = smooth_row(R0 - 1, load_row(R0 - 2), U[4], U[0]);
-  S[0] = smooth_row(R0, U[4], U[0], U[1]);
-  // one row step at phase J = (r - R0) mod 5: row r in slot J, r + k in slot (J + k) mod 5
-  auto row_step = [&](int r, auto jc) {
-    constexpr int J = decltype(jc)::value;
-    constexpr int M2 = (J + 3) % 5, M1 = (J + 4) % 5, C0 = J, P1 = (J + 1) % 5, P2 = (J + 2) % 5;
-    // the derivative images of row r (issued first: in flight while s of row r + 1 is computed)
-    int x;
-    const bool has = pix(r, x);
-    float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
-    const int pr = prow(r);
-    if constexpr (DF) {
-      D[P2] = load_d(r + 2);
-    } else {
-      const unsigned qd = (unsigned)((long)f * NOC * a.sp + (long)(pr < 0 ? 0 : pr) * h + (ycol ? y : 0));
-#pragma unroll
-      for (int ch = 0; ch < NOC; ++ch) {
-        const unsigned o = qd + (unsigned)(ch * a.sp);
-        if (has) {
-          lIx[ch] = ldu(a.Ix, o); lIy[ch] = ldu(a.Iy, o); lIz[ch] = ldu(a.Iz, o); lIxx[ch] = ldu(a.Ixx, o);
-          lIxy[ch] = ldu(a.Ixy, o); lIyy[ch] = ldu(a.Iyy, o); lIxz[ch] = ldu(a.Ixz, o); lIyz[ch] = ldu(a.Iyz, o);
-        } else {
-          lIx[ch] = lIy[ch] = lIz[ch] = lIxx[ch] = lIxy[ch] = lIyy[ch] = lIxz[ch] = lIyz[ch] = 0.0f;
-        }
-      }
-    }
-    U[P2] = load_row(r + 2);
-    S[P1] = smooth_row(r + 1, U[C0], U[P1], U[P2]);
-    // the system of row r: s, wx, wy of the pixel and its 4-neighbourhood (centre, left, right, up, down)
-    const float Sp = wave_from_prev(S[M1]), Sn = wave_from_next(S[P1]);
-    const float Xp = wave_from_prev(U[M1].wx), Xn = wave_from_next(U[P1].wx);
-    float Yp = 0.f, Yn = 0.f;
-    if (NOP == 2) {
-      Yp = wave_from_prev(U[M1].wy);
-      Yn = wave_from_next(U[P1].wy);
-    }
-    if constexpr (DF) {
-      // vertical taps (x, y + k): row r + k, lane + k (every lane shifts: the DPP moves are wave-wide)
-      auto vt = [&](float m2, float m1, float c, float p1, float p2, float (&t)[5]) {
-        t[0] = wave_from_prev(wave_from_prev(m2));
-        t[1] = wave_from_prev(m1);
-        t[2] = c;
-        t[3] = wave_from_next(p1);
-        t[4] = wave_from_next(wave_from_next(p2));
-      };
-      const int xc = has ? x : 0, yc = ycol ? y : 0;  // (lanes without a pixel: any valid taps)
-#pragma unroll
-      for (int ch = 0; ch < NOC; ++ch) {
-        float vx[5], vy[5], vz[5];
-        vt(D[M2].ix[ch], D[M1].ix[ch], D[C0].ix[ch], D[P1].ix[ch], D[P2].ix[ch], vx);
-        vt(D[M2].iy[ch], D[M1].iy[ch], D[C0].iy[ch], D[P1].iy[ch], D[P2].iy[ch], vy);
-        vt(D[M2].iz[ch], D[M1].iz[ch], D[C0].iz[ch], D[P1].iz[ch], D[P2].iz[ch], vz);
-        const float hx[5] = {D[M2].ix[ch], D[M1].ix[ch], D[C0].ix[ch], D[P1].ix[ch], D[P2].ix[ch]};
-        const float hz[5] = {D[M2].iz[ch], D[M1].iz[ch], D[C0].iz[ch], D[P1].iz[ch], D[P2].iz[ch]};
-        lIx[ch] = D[C0].ix[ch];
-        lIy[ch] = D[C0].iy[ch];
-        lIz[ch] = D[C0].iz[ch];
-        lIxx[ch] = conv5_clamp(hx, xc, w);
-        lIxy[ch] = conv5_clamp(vx, yc, h);
-        lIyy[ch] = conv5_clamp(vy, yc, h);
-        lIxz[ch] = conv5_clamp(hz, xc, w);
-        lIyz[ch] = conv5_clamp(vz, yc, h);
-      }
-    }
-    if (has && out_lane) {
-      const float S5[5] = {S[C0], S[M1], S[P1], Sp, Sn};
-      const float X5[5] = {U[C0].wx, U[M1].wx, U[P1].wx, Xp, Xn};
-      const float Y5[5] = {U[C0].wy, U[M1].wy, U[P1].wy, Yp, Yn};
-      const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
-      float4 c0, c1;
-      sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, U[C0].du, NOP == 2 ? U[C0].dv : 0.0f, lIx, lIy, lIz, lIxx, lIxy,
-                            lIyy, lIxz, lIyz, c0, c1);
-      const long idx = (long)f0 + (long)pr * h + y;
-      if (NOP == 2) {
-        float4 *C = reinterpret_cast<float4 *>(a.coef) + 2 * idx;
-        C[0] = c0;
-        C[1] = c1;
-      } else {
-        reinterpret_cast<float4 *>(a.coef)[idx] = c0;
-      }
-    }
-  };
-  for (int r = R0; r < R1; r += 5) {
-    static_for<5>([&](auto jc) {
-      if (r + decltype(jc)::value < R1) row_step(r + decltype(jc)::value, jc);
-    });
-  }
   }
 }
 
@@ -5143,24 +5037,20 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
   if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {
     const long waves = (long)a.n * march_segments(smsys_rows(a.w, a.h, a.wrap)) * march_strips(a.h);
     const unsigned grid = ceil_div(waves, 4);
-    auto go = [&](auto kern_ring, auto kern_rot) {
-      if (a.march_ring) kern_ring<<<grid, 256, 0, s>>>(a);
-      else kern_rot<<<grid, 256, 0, s>>>(a);
-    };
     if (a.smsys_deriv) {  // tv_deriv_fused(): k_tv_prepd wrote Ix, Iy, Iz only
       if (a.noc == 1) {
-        if (a.nop == 2) go(k_tv_smsys_m<2, 1, true, true>, k_tv_smsys_m<2, 1, true, false>);
-        else go(k_tv_smsys_m<1, 1, true, true>, k_tv_smsys_m<1, 1, true, false>);
+        if (a.nop == 2) k_tv_smsys_m<2, 1, true><<<grid, 256, 0, s>>>(a);
+        else k_tv_smsys_m<1, 1, true><<<grid, 256, 0, s>>>(a);
       } else {
-        if (a.nop == 2) go(k_tv_smsys_m<2, 3, true, true>, k_tv_smsys_m<2, 3, true, false>);
-        else go(k_tv_smsys_m<1, 3, true, true>, k_tv_smsys_m<1, 3, true, false>);
+        if (a.nop == 2) k_tv_smsys_m<2, 3, true><<<grid, 256, 0, s>>>(a);
+        else k_tv_smsys_m<1, 3, true><<<grid, 256, 0, s>>>(a);
       }
     } else if (a.nop == 2) {
-      if (a.noc == 1) go(k_tv_smsys_m<2, 1, false, true>, k_tv_smsys_m<2, 1, false, false>);
-      else go(k_tv_smsys_m<2, 3, false, true>, k_tv_smsys_m<2, 3, false, false>);
+      if (a.noc == 1) k_tv_smsys_m<2, 1><<<grid, 256, 0, s>>>(a);
+      else k_tv_smsys_m<2, 3><<<grid, 256, 0, s>>>(a);
     } else {
-      if (a.noc == 1) go(k_tv_smsys_m<1, 1, false, true>, k_tv_smsys_m<1, 1, false, false>);
-      else go(k_tv_smsys_m<1, 3, false, true>, k_tv_smsys_m<1, 3, false, false>);
+      if (a.noc == 1) k_tv_smsys_m<1, 1><<<grid, 256, 0, s>>>(a);
+      else k_tv_smsys_m<1, 3><<<grid, 256, 0, s>>>(a);
     }
     return;
   }

@@ -94,7 +94,6 @@ struct ofdis_context {
   int opt_smsys_march = 1;     // tall levels: smoothness + system as a register march (k_tv_smsys_m)
   int opt_smsys_prefetch = 1;  // fused smoothness + system (gray): derivative images issued before the staging
   int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
-  int opt_march_ring = 1;      // the register march with five-slot row rings (0: registers rotated every row)
   int opt_smsys_deriv = 1;     // fused smoothness + system (gray; colour: the march): second derivatives filtered from Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
   int call_lanes = 1;          // streams the current call's chunks run on (auto options)
@@ -540,7 +539,6 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.smsys = c->opt_smsys;
       tv.smsys2d = c->opt_smsys2d == 2 ? c->call_frames < 512 : c->opt_smsys2d;
       tv.smsys_march = c->opt_smsys_march;
-      tv.march_ring = c->opt_march_ring;
       tv.smsys_prefetch = c->opt_smsys_prefetch;
       tv.smsys_small = c->opt_smsys_small;
       tv.smsys_deriv = c->opt_smsys_deriv;
@@ -1324,7 +1322,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},
       {"smsys_prefetch", &ofdis_context::opt_smsys_prefetch, 0, 1},
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
-      {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1}, {"march_ring", &ofdis_context::opt_march_ring, 0, 1},
+      {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},

@@ -122,7 +122,6 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)
     ("smsys_deriv", 0, 1),     # fused launch reads all eight derivative planes (prepd writes them)
     ("smsys_march", 0, 1),     # tall levels: the 2-D tiled fused launch (smsys2d auto: on below 512 pairs)
-    ("march_ring", 0, 1),      # tall levels: the register march rotating its rows instead of five-slot rings
     (("smsys_march", "smsys2d"), (0, 0), (1, 2)),  # tall levels: two launches (smoothness, then system)
     ("prepd", 0, 2),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
     ("prepd", 1, 2),           # ... three launches for colour images only
