@@ -423,12 +423,13 @@ def test_cli_png_inputs(oracle, od, tmp_path, exe_name, noc, mode, over):
     assert_bitexact(got, want, f"{exe_name} on PNG inputs")
 
 
-def test_auto_two_streams_bitexact(oracle, od, ctx):
+@pytest.mark.parametrize("n", [300, 520])
+def test_auto_two_streams_bitexact(oracle, od, ctx, n):
     """From 256 pairs the library splits the batch over two streams by default (ofdis_runtime.cpp
     stream_count): every frame equals the one-stream whole-batch result, and frames of both chunks equal
     the oracle."""
     import torch
-    w, h, n, nd = 96, 64, 520, 4
+    w, h, nd = 96, 64, 4
     pairs = [od.synth_pair(w, h, 1, f, 1) for f in range(nd)]
     a = torch.from_numpy(np.stack([pairs[i % nd][0] for i in range(n)])).cuda()
     b = torch.from_numpy(np.stack([pairs[i % nd][1] for i in range(n)])).cuda()
@@ -447,7 +448,8 @@ def test_auto_two_streams_bitexact(oracle, od, ctx):
         ctx.set_option("streams", 0)
     assert_bitexact(auto, one, "two-stream chunks vs one stream")
     q = oracle.oppoint(2, w, 1, 1)
-    for f in (0, 259, 260, 519):  # first / last frame of each 260-pair chunk
+    half = (n + 1) // 2
+    for f in (0, half - 1, half, n - 1):  # first / last frame of each chunk
         ref = oracle.run_u8(pairs[f % nd][0], pairs[f % nd][1], q)
         assert_bitexact(auto[f], ref, f"frame {f}")
 
