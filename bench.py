@@ -474,7 +474,8 @@ def main():
         # the upsample kernel the timed region ran (up_form auto follows the call's lanes, which this pass changes)
         up_user = any(o.split("=")[0] == "up_form" for o in args.option)
         if not up_user:
-            ctx.set_option("up_form", 1 if min(streams_eff, -(-B // chunk_eff)) >= 2 and W >= 1024 else 0)
+            lanes_eff = min(streams_eff, -(-B // chunk_eff))
+            ctx.set_option("up_form", 1 if W >= 1024 and (lanes_eff >= 2 or B < 1024) else 0)
         ctx.enable_kernel_timing(True)
         for _ in range(args.steps):
             step()

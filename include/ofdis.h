@@ -212,8 +212,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
  *   "up_form" (0..3, default 3): optical-flow upsample: 1 / 2 = each staged source row's horizontal taps once per
  *                        column for blocks of 4 / 8 output rows, 0 = once per output row that reads them (round 4),
- *                        3 = 1 for calls whose chunks run on two or more streams on frames at least 1024 wide,
- *                        else 0 (the faster of the two end to end in each measured regime);
+ *                        3 = 1 on frames at least 1024 wide for calls on two or more streams or of fewer than
+ *                        1024 pairs, else 0 (the faster of the two end to end in each measured regime);
  *   "graph" (0/1/2/3, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
  *                        parameters repeat (re-captured when they change); 1 captures single-stream
  *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined; the

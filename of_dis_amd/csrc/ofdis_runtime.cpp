@@ -80,9 +80,10 @@ struct ofdis_context {
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
   // flow upsample: 0 per-output-row horizontal taps (k_upsample_rows), 1 / 2 once per staged source row (k_upsample_h,
-  // 4 / 8 rows), 3 auto: 1 when the call runs on two or more lanes and the frame spans a whole 1024-column block,
-  // else 0 -- measured end to end, alternating on one box each (profiles/r05/s16/NOTE.md): B two lanes 331.4k (1) vs
-  // 322.3k (0), one lane 294.6k vs 306.8k; C 11,260 vs 11,185; D (2 x 128) 226.9k vs 224.1k; A (640 wide) 122.7k vs 124.5k
+  // 4 / 8 rows), 3 auto: 1 when the frame spans a whole 1024-column block and the call runs on two or more lanes or
+  // has fewer than 1024 pairs, else 0 -- measured end to end, alternating on one box each (profiles/r05/s16/NOTE.md):
+  // B two lanes 331.4k (1) vs 322.3k (0), one lane of 2048-pair chunks 294.6k vs 306.8k; C 11,260 vs 11,185; D
+  // (2 x 128) 226.9k vs 224.1k; the 32-pair shard 64.67k vs 64.37k; A (640 wide) 122.7k vs 124.5k
   int opt_up_form = 3;
   int opt_smsys = 1;           // smoothness + system in one launch (0: two launches, A/B)
   // the fused launch on 2-D tiles for tall levels: 1 on, 0 off (two launches there), 2 auto = on for calls of
@@ -777,7 +778,8 @@ int run_upsample(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *
   up.offx = P.padl;
   up.offy = P.padt;
   up.nt_store = c->opt_nt_store;
-  up.form = c->opt_up_form == 3 ? (c->call_lanes >= 2 && P.W0 >= 1024 ? 1 : 0) : c->opt_up_form;
+  up.form = c->opt_up_form == 3 ? (P.W0 >= 1024 && (c->call_lanes >= 2 || c->call_frames < 1024) ? 1 : 0)
+                                 : c->opt_up_form;
   timed(c, 10, s, [&] { launch_upsample(up, s); });
   return hipGetLastError() == hipSuccess ? OFDIS_OK : OFDIS_ERR_DEVICE;
 }
