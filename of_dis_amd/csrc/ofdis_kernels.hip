@@ -122,10 +122,8 @@ __global__ __launch_bounds__(256) void k_pyr_base_gray(PyrBaseArgs a) {
       if (VB == 16) {
 #pragma unroll
         for (int q = 0; q < B / 16; ++q) {
-          typedef unsigned v4u __attribute__((ext_vector_type(4)));
-          const v4u w4 = NT ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(row) + q)
-                            : reinterpret_cast<const v4u *>(row)[q];
-          const uint4 v = make_uint4(w4.x, w4.y, w4.z, w4.w);
+          const uint4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const uint4 *>(row) + q)
+                             : reinterpret_cast<const uint4 *>(row)[q];
           s2 = __builtin_amdgcn_sad_u8(v.x, 0u, s2);
           s2 = __builtin_amdgcn_sad_u8(v.y, 0u, s2);
           s2 = __builtin_amdgcn_sad_u8(v.z, 0u, s2);
