@@ -210,7 +210,6 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "patch_generic" (0/1, default 0): every patch shape on the any-shape kernel (runtime value loops: the
  *                        default for p*p*noc > 448, e.g. RGB p >= 14, gray p >= 22);
  *   "nt_store" (0/1, default 0): write the full-resolution flow with non-temporal stores;
- *   "pyr_nt" (0/1, default 0): the pyramid base reads the u8 frames with non-temporal loads (gray, 2^l >= 16);
  *   "up_form" (0..3, default 3): optical-flow upsample: 1 / 2 = each staged source row's horizontal taps once per
  *                        column for blocks of 4 / 8 output rows, 0 = once per output row that reads them (round 4),
  *                        3 = 1 on frames at least 1024 wide for calls on two or more streams or of fewer than

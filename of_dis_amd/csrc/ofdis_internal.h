@@ -30,7 +30,6 @@ struct PyrBaseArgs {
   int log2s;                     // level of the output (sc_l)
   int w, h;                      // output level size
   float *out;                    // unpadded level [2n][h][w][noc]
-  int nt;                        // non-temporal 16-byte loads of the u8 frames (option "pyr_nt")
 };
 
 // SELECTCHANNEL 2 (run_dense.cpp:139-148): level 0 = Sobel gradient magnitude of the divisibility-padded

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_pyr_base(PyrBaseArgs a) {
 // Intensity images, 2^L = 4..32: one output pixel per thread over the flattened [2n][h][w] range (full
 // waves even for narrow levels), the 2^L rows of the block unrolled so all loads are in flight at once,
 // 4 / 8 / 16-byte loads summed with v_sad_u8.  Blocks that need horizontal clamping take the byte loop.
-template <int L, bool NT = false>
+template <int L>
 __global__ __launch_bounds__(256) void k_pyr_base_gray(PyrBaseArgs a) {
   constexpr int B = 1 << L;
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
@@ -122,8 +122,7 @@ __global__ __launch_bounds__(256) void k_pyr_base_gray(PyrBaseArgs a) {
       if (VB == 16) {
 #pragma unroll
         for (int q = 0; q < B / 16; ++q) {
-          const uint4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const uint4 *>(row) + q)
-                             : reinterpret_cast<const uint4 *>(row)[q];
+          const uint4 v = reinterpret_cast<const uint4 *>(row)[q];
           s2 = __builtin_amdgcn_sad_u8(v.x, 0u, s2);
           s2 = __builtin_amdgcn_sad_u8(v.y, 0u, s2);
           s2 = __builtin_amdgcn_sad_u8(v.z, 0u, s2);
@@ -4852,14 +4851,8 @@ void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s) {
     switch (a.log2s) {
       case 2: k_pyr_base_gray<2><<<blocks, 256, 0, s>>>(a); return;
       case 3: k_pyr_base_gray<3><<<blocks, 256, 0, s>>>(a); return;
-      case 4:
-        if (a.nt) k_pyr_base_gray<4, true><<<blocks, 256, 0, s>>>(a);
-        else k_pyr_base_gray<4><<<blocks, 256, 0, s>>>(a);
-        return;
-      case 5:
-        if (a.nt) k_pyr_base_gray<5, true><<<blocks, 256, 0, s>>>(a);
-        else k_pyr_base_gray<5><<<blocks, 256, 0, s>>>(a);
-        return;
+      case 4: k_pyr_base_gray<4><<<blocks, 256, 0, s>>>(a); return;
+      case 5: k_pyr_base_gray<5><<<blocks, 256, 0, s>>>(a); return;
     }
   }
   k_pyr_base<<<dim3(ceil_div(a.w, 256), a.h, 2 * a.n), 256, 0, s>>>(a);

@@ -79,7 +79,6 @@ struct ofdis_context {
   } gkey;
   hipGraphExec_t gexec = nullptr;
   int opt_nt_store = 0;        // upsample output with non-temporal stores (A/B)
-  int opt_pyr_nt = 0;          // pyramid base: non-temporal 16-byte loads of the u8 frames (A/B)
   // flow upsample: 0 per-output-row horizontal taps (k_upsample_rows), 1 / 2 once per staged source row (k_upsample_h,
   // 4 / 8 rows), 3 auto: 1 when the frame spans a whole 1024-column block and the call runs on two or more lanes or
   // has fewer than 1024 pairs, else 0 -- measured end to end, alternating on one box each (profiles/r05/s16/NOTE.md):
@@ -674,7 +673,6 @@ int run_pyramid(ofdis_context *c, char *ws, const Plan &P, const uint8_t *a, con
     pb.w = P.lv[0].w;
     pb.h = P.lv[0].h;
     pb.out = (float *)(ws + P.off_lvl[0]);
-    pb.nt = c->opt_pyr_nt;
     timed(c, 0, s, [&] { launch_pyr_base(pb, s); });
   }
   for (size_t i = 1; i < P.lv.size(); ++i) {
@@ -1329,7 +1327,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
-      {"nt_store", &ofdis_context::opt_nt_store, 0, 1}, {"pyr_nt", &ofdis_context::opt_pyr_nt, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},
+      {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},
       {"graph", &ofdis_context::opt_graph, 0, 3},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
