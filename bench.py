@@ -149,16 +149,12 @@ def kernel_roofline(od, p, W, H, B, per_launch, cfg, steps, kernels, name):
                        "frac_counters: PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/traffic.json) / launch "
                        "time; model_equiv_frac: the SURVEY 8(d) per-sweep unit x sweeps, a streaming-equivalent "
                        "rate of the sweep-fused kernel (may exceed 1, not a roofline fraction)")
-    if name == "tv_sysor":
-        # the fused system + SOR launch (option sysor): the byte model is already once per inner iteration (wx, wy,
-        # du, dv and the eight derivative planes in, du, dv out: 56 B per pixel for intensity optical flow), i.e. the
-        # compulsory bytes of the iteration; counters as for tv_sor
-        out["frac_compulsory"] = out["frac"]
-        out["frac_counters"] = (None if traffic is None else
-                                round(traffic / (k["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4))
-        out["counters_vs_compulsory"] = None if traffic is None else round(traffic / bytes_launch, 3)
-        out["note"] = ("one TV inner iteration (smoothness, system, exact-order SOR) per launch; frac = 56 B/px "
-                       "(optical flow, intensity) once per launch / launch time / 8 TB/s")
+    if name == "tv_level":
+        # the fused red-black level launch of the latency mode (sor_mode = 1): every inner iteration of a level in one
+        # workgroup per frame; bytes = wx, wy and the eight derivative planes in, the flow out, once per level.  Not an
+        # HBM-bound kernel: 1 + 2 * solverit workgroup barriers per inner iteration on one CU per frame
+        out["limiter"] = ("barrier / VALU latency of one workgroup per frame (latency mode; the later inner "
+                          "iterations read the derivative planes from L2)")
     if name == "patch":  # not an HBM-bound kernel: say what bounds it
         out["limiter"] = ("VALU issue: SQ_ACTIVE_INST_VALU x waves/SIMD ~ 0.9-1.2 of SIMD cycles at configs C and E "
                           "(profiles/r02/pmc, profiles/r03/pmc); bytes = compulsory per patch (template, gradients, "
@@ -464,7 +460,6 @@ def main():
     kernels = {}
     roofline = None
     roofline_sor = None
-    roofline_sysor = None
     if not args.no_kernel_timing:
         # the same launches (chunk_eff pairs each), serialised on one stream: each kernel timed alone
         # (HIP events bracketing launches of two concurrent streams do not measure the kernels: they
@@ -500,8 +495,6 @@ def main():
         roofline = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, dom)
         if dom != "tv_sor" and "tv_sor" in kernels:  # the north-star kernel, reported beside the dominant one
             roofline_sor = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, "tv_sor")
-        if dom != "tv_sysor" and "tv_sysor" in kernels:  # the fused system + SOR launch (levels <= 128 rows)
-            roofline_sysor = kernel_roofline(od, p, W, H, B, chunk_eff, cfg, args.steps, kernels, "tv_sysor")
 
     # ---- single-pair latency (the drop-in CLI's case: one pair per call), device-resident and host buffers
     latency = None
@@ -594,7 +587,7 @@ def main():
                        "options": args.option,
                        "parallelism": f"frame-sharded x{world}" + (" (rehearsal: ranks share the GPU)"
                                                                    if rehearsal else "")},
-            "roofline": roofline, "roofline_tv_sor": roofline_sor, "roofline_tv_sysor": roofline_sysor, "cpu_baseline": cpu, "parity": parity,
+            "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,
             "latency": latency, "host_io": host_io, "shard_of_8": shard8, "kernels": kernels,
         }
         if cpu:

@@ -184,9 +184,13 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "prepd" (0..2, default 2): image warp, temporal images and the derivative filters of a level in one launch
  *                        (1: intensity images only, colour images in three launches; 0: three launches);
  *   "sor_mode" (0/1, default 0): 0 = sor_coupled's exact lexicographic order (the reference's bits);
- *                        1 = red-black order (SURVEY §7 4(ii) throughput mode: every half-sweep fully
- *                        parallel; a different iteration -- NOT the reference's bits, end-point error
- *                        gated against the exact path; the one option that changes results);
+ *                        1 = the latency mode, red-black order (every half-sweep fully parallel):
+ *                        levels of at most 8192 pixels run their whole inner loop -- smoothness, system, 2 x solverit
+ *                        half-sweeps per inner iteration -- and the flow update in one launch of one workgroup per
+ *                        frame (k_tv_level_rb), larger levels the system launches and one launch per half-sweep.
+ *                        A different iteration -- NOT the reference's bits: bit-exact against the oracle's
+ *                        red-black restatement, end-point error gated against the exact path; the one option
+ *                        that changes results.  For calls that cannot fill the chip (one pair, a few dozen);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (patches of at most
  *                        448 values; larger ones always run the any-shape kernel);
  *   "patch_window" (0/1, default 1): p = 8 / 12 patches read their bilinear taps from an LDS copy of the
@@ -214,33 +218,14 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        column for blocks of 4 / 8 output rows, 0 = once per output row that reads them (round 4),
  *                        3 = 1 on frames at least 1024 wide for calls on two or more streams or of fewer than
  *                        1024 pairs, else 0 (the faster of the two end to end in each measured regime);
- *   "graph" (0/1/2/3, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
+ *   "graph" (0/1/2, default 1): replay a batch as one captured HIP graph while its pointers, sizes and
  *                        parameters repeat (re-captured when they change); 1 captures single-stream
- *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined; the
- *                        two-stream pipeline only under a HIP runtime >= 7.2: the one bundled with
- *                        PyTorch's ROCm 7.0 build crashes capturing its mutually waiting lanes, so there
- *                        it is issued eagerly); 3 captures the pipeline whatever the runtime (diagnostic);
+ *                        batches, 2 also the multi-stream ones (chunks forked over lanes and joined);
  *   "streams" (0-16, default 0 = automatic: 2 from 256 pairs, else 1): a batch is cut into chunks that run
  *                        round-robin on that many HIP streams with separate workspaces, overlapping one
  *                        chunk's latency-bound wavefront with another's streaming kernels (1 stream and
  *                        several chunks: the chunks run one after the other);
  *   "chunk" (frames per chunk, 0 to 2^30, default 0 = the batch split evenly over the streams);
- *   "sysor" (0/1, default 0): optical flow on intensity images, levels of up to 128 rows, 2 or 3 sweeps: each TV
- *                        inner iteration as ONE launch -- smoothness, system and the 2x2 inverse produced three
- *                        anti-diagonals ahead of the exact-order SOR wavefront by producer waves of the same
- *                        workgroup, the coefficients handed over in LDS, one barrier per step (0: the system and
- *                        the SOR as two launches, the coefficients through memory);
- *   "pipeline" (0..4, default 0): with several chunks, a software pipeline instead of the round robin: one stream
- *                        runs the HBM-streaming stages (u8 -> pyramid, full-resolution upsample) of every chunk while
- *                        L = "pipeline" chain lanes run the chunks' DIS + TV chains (chunk ch on lane ch mod L, event
- *                        hand-overs, L + 1 workspaces);
- *   "split_cus" (0..7, default 0): pipeline: the streaming stream runs on that many eighths of the CUs (a CU-masked
- *                        stream; the eighths spread evenly over the XCDs), 0 = all CUs;
- *   "stagger" (0/1, default 0): round robin over several streams: chunk ch's DIS + TV chain starts only after
- *                        chunk ch - 1's, so chains never share the GPU while each overlaps the other streams' pyramid
- *                        and upsample;
- *   "chain_cus" (0..8, default 0): pipeline: the chain lanes run on the last that many eighths (complementary to
- *                        "split_cus" when the two add up to 8), 0 or 8 = all CUs.
  * Setting any option drops the captured graph.  Unknown keys and out-of-range values return
  * OFDIS_ERR_INVALID_ARGUMENT.  Apart from "sor_mode", results never depend on these settings. */
 int ofdis_context_set_option(ofdis_context *ctx, const char *key, int value);

@@ -131,8 +131,9 @@ struct TvArgs {
                                // (k_tv_prepd then writes only Ix, Iy, Iz of the derivative planes); set by the
                                // runtime only where tv_deriv_fused() holds
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)
-  int sysor;                   // levels <= 128 rows (optical flow, intensity images): smoothness + system + SOR of an
-                               // inner iteration in one launch (k_tv_sysor) where tv_sysor_ok() holds
+  int lat;                     // sor_mode = 1 latency form (tv_level_rb_ok): k_tv_prepd writes the flow copies and
+                               // the eight derivative planes in the colour-split entry layout (lat_idx) that
+                               // k_tv_level_rb reads
 };
 
 struct UpArgs {
@@ -153,6 +154,8 @@ struct InitArgs {
 };
 
 void launch_init_area(const InitArgs &a, hipStream_t s);
+void warm_kernels_module(hipStream_t s);  // one empty launch per kernel translation unit: loads its code object
+void warm_tvrb_module(hipStream_t s);
 void launch_pyr_base(const PyrBaseArgs &a, hipStream_t s);
 void launch_pyr_gradmag(const PyrGradmagArgs &a, hipStream_t s);
 void launch_pyr_down(const PyrDownArgs &a, hipStream_t s);
@@ -170,8 +173,8 @@ bool tv_smsys_ok(const TvArgs &a);
 bool tv_deriv_fused(const TvArgs &a);  // the level's derivative filters can move into k_tv_smsys (smsys_deriv)
 void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
-bool tv_sysor_ok(const TvArgs &a);  // ofdis_tvsysor.hip
-void launch_tv_sysor(const TvArgs &a, hipStream_t s);
+bool tv_level_rb_ok(const TvArgs &a);  // ofdis_tvrb.hip
+void launch_tv_level_rb(const TvArgs &a, int n_inner, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);
 

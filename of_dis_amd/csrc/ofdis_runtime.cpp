@@ -26,7 +26,7 @@ using namespace ofdis;
 namespace {
 
 const char *const kKernelNames[] = {"pyr_base", "pyr_down", "pyr_pad_grad", "patch",    "aggregate", "tv_prep",
-                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_sysor"};
+                                    "tv_deriv", "tv_system", "tv_sor",       "tv_final", "upsample",  "tv_level"};
 
 struct Plan {
   int n = 0, W0 = 0, H0 = 0, Wp = 0, Hp = 0, padl = 0, padt = 0, padw = 0, padh = 0;
@@ -107,8 +107,6 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
-  int opt_sysor = 0;           // levels <= 128 rows (optical flow, intensity images): smoothness + system + SOR of an
-                               // inner iteration in one launch (k_tv_sysor)
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw;
@@ -123,18 +121,11 @@ struct ofdis_context {
   // streams 0 = auto: 2 for batches of >= 512 pairs (measured +7-9 % at 1024 1080p pairs: two 512-pair
   // chains on two streams), else 1; chunk 0 = the batch split evenly over the streams.
   int opt_streams = 0, opt_chunk = 0;
-  int opt_pipeline = 0;              // software pipeline: the streaming stages on one stream beside `opt_pipeline`
-                                     // chain lanes (DIS + TV), chunk ch on chain lane ch % L (0: off)
-  int opt_split_cus = 0;             // pipeline: the streaming stream on this many eighths of the CUs (0: all)
-  int opt_chain_cus = 0;             // pipeline: the chain lanes on the complementary eighths (0: all CUs)
-  int opt_stagger = 0;               // round robin: chunk ch's chain starts after chunk ch - 1's
-  std::vector<hipEvent_t> pipe_ev;   // per-chunk hand-over events of the pipeline
   struct Lane {
     hipStream_t s = nullptr;
     char *ws = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;
-    int mask = 0;  // CU mask the stream was created with: 0 none, +k the first k eighths, -k the last k eighths
   };
   std::vector<Lane> lanes;
   hipEvent_t entry = nullptr;
@@ -546,9 +537,10 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
-      tv.sysor = c->opt_sysor;
-      const bool sysor = tv_sysor_ok(tv);  // the fused launch reads the eight derivative planes: prepd writes them all
-      tv.smsys_deriv = !sysor && tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
+      // latency form of sor_mode = 1: the whole inner loop and the flow update in one launch per level, prep writing
+      // the colour-split layout that launch reads (all eight derivative planes)
+      tv.lat = tv_level_rb_ok(tv);
+      tv.smsys_deriv = !tv.lat && tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
       } else {
@@ -558,12 +550,12 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
           launch_tv_deriv2(tv, s);
         });
       }
+      if (tv.lat) {
+        timed(c, 11, s, [&] { launch_tv_level_rb(tv, n_inner, s); });
+        continue;
+      }
       for (int it = 0; it < n_inner; ++it) {
         tv.first_iter = it == 0;
-        if (sysor) {  // smoothness + system + SOR of the iteration in one launch, the coefficients in LDS
-          timed(c, 11, s, [&] { launch_tv_sysor(tv, s); });
-          continue;
-        }
         timed(c, 7, s, [&] {
           if (tv_smsys_ok(tv)) {
             launch_tv_smsys(tv, s);
@@ -730,6 +722,14 @@ int ofdis_context_create(int device, ofdis_context **out) {
     delete c;
     return OFDIS_ERR_DEVICE;
   }
+  // load the kernels' code objects now, not inside the first call's timers (the drop-in CLI's one pair)
+  warm_kernels_module(c->stream);
+  warm_tvrb_module(c->stream);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return OFDIS_ERR_DEVICE;
+  }
   *out = c;
   return OFDIS_OK;
 }
@@ -756,7 +756,6 @@ void ofdis_context_destroy(ofdis_context *c) {
   if (c->entry) hipEventDestroy(c->entry);
   if (c->ev_null) hipEventDestroy(c->ev_null);
   if (c->ev_ws) hipEventDestroy(c->ev_ws);
-  for (auto e : c->pipe_ev) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -806,61 +805,23 @@ int run_init(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, c
 }
 
 // One chunk of frames through the whole pipeline on stream s with workspace ws.
-// chain_wait / chain_done (optional): an event the chain (run_levels) waits for first / is recorded after it.
 int run_chunk(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p, const uint8_t *img_a,
-              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s,
-              hipEvent_t chain_wait = nullptr, hipEvent_t chain_done = nullptr) {
+              const uint8_t *img_b, const float *init, float *flow_out, hipStream_t s) {
   int rc = run_pyramid(c, ws, P, img_a, img_b, s);
   if (rc) return rc;
   if (init && (rc = run_init(c, ws, P, p, init, s))) return rc;
-  if (chain_wait) HIP_OK(hipStreamWaitEvent(s, chain_wait, 0));
   rc = run_levels(c, ws, P, p, s, init ? (const float *)(ws + P.off_init) : nullptr, nullptr);
-  if (chain_done) HIP_OK(hipEventRecord(chain_done, s));
   if (rc) return rc;
   return run_upsample(c, ws, P, p, flow_out, s);
 }
 
-// CU mask of k eighths of the device's CUs (k > 0: classes 0 .. k-1, k < 0: classes 8+k .. 7), CU i of class
-// ((i mod 8) + i / 8) mod 8.  Every class holds an equal share of each aligned group of 32 CUs and of each residue
-// mod 8, so the subset spreads evenly over the eight XCDs whether the mask's bits enumerate the CUs XCD by XCD or
-// interleave them.
-void cu_mask(int k, std::vector<uint32_t> &m) {
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-    ncu = 256;
-  m.assign((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i) {
-    const int cls = ((i % 8) + i / 8) % 8;
-    if (k > 0 ? cls < k : cls >= 8 + k) m[i / 32] |= 1u << (i % 32);
-  }
-}
-
-// k lanes (stream, done event, workspace of `bytes`); masks[i] (when given): the CU mask of lane i's stream, which is
-// re-created when it differs from the one it has.
-int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *masks = nullptr) {
+// k lanes (stream, done event, workspace of `bytes`).
+int ensure_lanes(ofdis_context *c, int k, size_t bytes) {
   if ((int)c->lanes.size() < k) c->lanes.resize(k);
   if (!c->entry) HIP_OK(hipEventCreateWithFlags(&c->entry, hipEventDisableTiming));
   for (int i = 0; i < k; ++i) {
     auto &L = c->lanes[i];
-    const int want = masks ? (*masks)[i] : L.mask;
-    if (L.s && L.mask != want) {  // a different CU mask: a new stream (after all queued work)
-      int rc = drop_graph(c);
-      if (rc) return rc;
-      HIP_OK(hipDeviceSynchronize());
-      HIP_OK(hipStreamDestroy(L.s));
-      L.s = nullptr;
-    }
-    if (!L.s) {
-      if (want == 0) {
-        HIP_OK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
-      } else {
-        std::vector<uint32_t> m;
-        cu_mask(want, m);
-        HIP_OK(hipExtStreamCreateWithCUMask(&L.s, (uint32_t)m.size(), m.data()));
-      }
-      L.mask = want;
-    }
+    if (!L.s) HIP_OK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
     if (!L.done) HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     if (L.cap < bytes) {
       if (L.ws) {
@@ -878,19 +839,6 @@ int ensure_lanes(ofdis_context *c, int k, size_t bytes, const std::vector<int> *
   return OFDIS_OK;
 }
 
-// The two-stream pipeline's lanes wait on each other in both directions inside one capture.  The HIP
-// runtime bundled with PyTorch 2.10 (ROCm 7.0, 70051831) segfaults in hipStreamEndCapture on that event
-// pattern -- a 40-line program of empty kernels does too (tools/capture_repro.hip, profiles/r02/capture/) --
-// while ROCm 7.2's runtime (70226015) captures and replays it exactly (tests/cpp/pipe_capture.cpp).  In a
-// Python process that imported torch, torch's runtime is the one that serves this library.
-bool pipeline_capture_ok() {
-  static const bool ok = [] {
-    int v = 0;
-    return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
-  }();
-  return ok;
-}
-
 // two lanes from 256 pairs (config D, 256 pairs: 223.4-223.7k on one stream, 225.3-226.8k on two; profiles/r05/s22)
 int stream_count(const ofdis_context *c, int n) { return c->opt_streams > 0 ? c->opt_streams : (n >= 256 ? 2 : 1); }
 
@@ -903,15 +851,16 @@ int tv_frame_cap(const ofdis_params *p, int width, int height) {
   return (int)std::min((long)(1 << 30), ((1L << 30) - 1) / per);  // 0: one frame alone is too large
 }
 
-// How one call is issued: the whole batch on one stream and workspace (single), chunks round-robin over
-// lanes (round robin), or the two-stream software pipeline.  Everything the issue needs -- workspaces,
-// lane streams, events -- is allocated by prepare(), before any capture begins.
+// How one call is issued: the whole batch on one stream and workspace (single), or chunks round-robin over
+// lanes (round robin).  Everything the issue needs -- workspaces, lane streams, events -- is allocated by
+// prepare(), before any capture begins.  (Round 5's software pipeline over a streaming stream and chain lanes,
+// with CU-masked streams and a staggered round robin, measured slower in every form and was removed in round 6.)
 struct CallPlan {
-  enum Kind { kSingle, kRoundRobin, kPipeline } kind = kSingle;
+  enum Kind { kSingle, kRoundRobin } kind = kSingle;
   int n = 0, width = 0, height = 0, chunk = 0, nchunks = 1, lanes = 0;
   bool init = false;
   Plan whole;               // kSingle
-  std::vector<Plan> parts;  // kRoundRobin / kPipeline: one plan per chunk
+  std::vector<Plan> parts;  // kRoundRobin: one plan per chunk
 };
 
 int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int height, bool init, bool capturing,
@@ -936,27 +885,12 @@ int prepare(ofdis_context *c, const ofdis_params *p, int n, int width, int heigh
     cp.whole = batch_plan(p, n, width, height, init);
     return ensure_ws(c, cp.whole.total);
   }
-  cp.kind = c->opt_pipeline && !c->timing ? CallPlan::kPipeline : CallPlan::kRoundRobin;
+  cp.kind = CallPlan::kRoundRobin;
   for (int ch = 0; ch < cp.nchunks; ++ch)
     cp.parts.push_back(batch_plan(p, std::min(chunk, n - ch * chunk), width, height, init));
-  // the pipeline: chain lanes 0 .. L-1 (CU mask: the last opt_chain_cus eighths), workspaces of lanes 0 .. L (chunk ch
-  // in workspace ch mod (L + 1)), the streaming stream = lane L (the first opt_split_cus eighths)
-  cp.lanes = cp.kind == CallPlan::kPipeline ? c->opt_pipeline + 1 : std::min(nstreams, cp.nchunks);
+  cp.lanes = std::min(nstreams, cp.nchunks);
   c->call_lanes = cp.lanes;
-  std::vector<int> masks(cp.lanes, 0);
-  if (cp.kind == CallPlan::kPipeline) {
-    for (int i = 0; i < c->opt_pipeline; ++i) masks[i] = c->opt_chain_cus > 0 && c->opt_chain_cus < 8 ? -c->opt_chain_cus : 0;
-    masks[c->opt_pipeline] = c->opt_split_cus;
-  }  // round robin: unmasked lanes (a lane a pipeline call masked gets a new stream)
-  int rc = ensure_lanes(c, cp.lanes, cp.parts[0].total, &masks);
-  if (rc) return rc;
-  if (cp.kind == CallPlan::kPipeline || c->opt_stagger)
-    while ((int)c->pipe_ev.size() < 2 * cp.nchunks) {
-      hipEvent_t e = nullptr;
-      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->pipe_ev.push_back(e);
-    }
-  return OFDIS_OK;
+  return ensure_lanes(c, cp.lanes, cp.parts[0].total);
 }
 
 // Chunks round-robin over the lanes, each chunk's whole pipeline on one lane (fork from s, join into s).
@@ -967,15 +901,11 @@ int issue_round_robin(ofdis_context *c, const CallPlan &cp, hipStream_t s, const
   for (int i = 0; i < k; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
   const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
   const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
-  // stagger: chunk ch's chain (DIS + TV levels) starts only after chunk ch - 1's, so the chains never share the
-  // GPU while each overlaps the other lanes' streaming stages (pyramid, upsample)
-  hipEvent_t *ev_chain = c->opt_stagger && k > 1 ? c->pipe_ev.data() : nullptr;
   for (int ch = 0; ch < cp.nchunks; ++ch) {
     const size_t f0 = (size_t)ch * cp.chunk;
     auto &L = c->lanes[ch % k];
     int rc = run_chunk(c, L.ws, cp.parts[ch], p, img_a + f0 * in_frame, img_b + f0 * in_frame,
-                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s,
-                       ev_chain && ch > 0 ? ev_chain[ch - 1] : nullptr, ev_chain ? ev_chain[ch] : nullptr);
+                       init ? init + f0 * out_frame : nullptr, flow_out + f0 * out_frame, L.s);
     if (rc) return rc;
   }
   for (int i = 0; i < k; ++i) {
@@ -985,71 +915,10 @@ int issue_round_robin(ofdis_context *c, const CallPlan &cp, hipStream_t s, const
   return OFDIS_OK;
 }
 
-// Software pipeline over chunks ("pipeline" option = L chain lanes).  One stream (lane L) runs the HBM-streaming
-// stages -- the pyramid from the u8 frames and the full-resolution upsample -- and L chain lanes the latency-bound
-// DIS + TV chain (run_levels) of chunk ch on lane ch mod L, so chains overlap the streaming of other chunks.  W = L + 1
-// workspaces: chunk ch uses workspace ch mod W.  Issue order on the streaming stream: pyr 0 .. W-1, then up c and
-// pyr c + W for c = 0, 1, ...: pyr c + W reuses the workspace of chunk c only after up c (same stream, issued before
-// it), which waits for levels c.  With "split_cus" / "chain_cus" the streaming stream and the chain lanes run on
-// disjoint CU subsets (hipExtStreamCreateWithCUMask), so the streaming kernels' workgroups never queue behind the
-// chains' (VERDICT r04 next 4).  Every hand-over is an event recorded before it is waited on (in host issue order)
-// within this call (and so within a capture), and all lanes join s at the end.
-int issue_pipeline(ofdis_context *c, const CallPlan &cp, hipStream_t s, const ofdis_params *p,
-                   const uint8_t *img_a, const uint8_t *img_b, const float *init, float *flow_out) {
-  const size_t in_frame = (size_t)cp.width * cp.height * p->noc;
-  const size_t out_frame = (size_t)cp.width * cp.height * cp.parts[0].nop;
-  const int L = cp.lanes - 1, W = cp.lanes;
-  hipStream_t S = c->lanes[L].s;
-  hipEvent_t *ev_pyr = c->pipe_ev.data(), *ev_lev = c->pipe_ev.data() + cp.nchunks;
-  // OFDIS_PIPE_SKIP (debugging the capture of this issue, tools/graph_probe.py): bit 0 leaves out the pyramid
-  // launches, bit 1 the levels, bit 2 the upsample (the output is then wrong; the event pattern is kept)
-  static const int skip = std::getenv("OFDIS_PIPE_SKIP") ? std::atoi(std::getenv("OFDIS_PIPE_SKIP")) : 0;
-  HIP_OK(hipEventRecord(c->entry, s));
-  for (int i = 0; i <= L; ++i) HIP_OK(hipStreamWaitEvent(c->lanes[i].s, c->entry, 0));
-  auto pyr = [&](int ch) -> int {
-    const size_t f0 = (size_t)ch * cp.chunk;
-    char *ws = c->lanes[ch % W].ws;
-    int r = (skip & 1) ? 0 : run_pyramid(c, ws, cp.parts[ch], img_a + f0 * in_frame, img_b + f0 * in_frame, S);
-    if (r) return r;
-    if (init && (r = run_init(c, ws, cp.parts[ch], p, init + f0 * out_frame, S))) return r;
-    HIP_OK(hipEventRecord(ev_pyr[ch], S));
-    return OFDIS_OK;
-  };
-  int rc = OFDIS_OK;
-  for (int ch = 0; ch < std::min(W, cp.nchunks); ++ch)
-    if ((rc = pyr(ch))) return rc;
-  for (int ch = 0; ch < cp.nchunks; ++ch) {
-    char *ws = c->lanes[ch % W].ws;
-    const Plan &P = cp.parts[ch];
-    hipStream_t Lc = c->lanes[ch % L].s;
-    HIP_OK(hipStreamWaitEvent(Lc, ev_pyr[ch], 0));
-    if (!(skip & 2) && (rc = run_levels(c, ws, P, p, Lc, init ? (const float *)(ws + P.off_init) : nullptr, nullptr)))
-      return rc;
-    HIP_OK(hipEventRecord(ev_lev[ch], Lc));
-    HIP_OK(hipStreamWaitEvent(S, ev_lev[ch], 0));
-    if (!(skip & 4) && (rc = run_upsample(c, ws, P, p, flow_out + (size_t)ch * cp.chunk * out_frame, S))) return rc;
-    if (ch + W < cp.nchunks && (rc = pyr(ch + W))) return rc;
-  }
-  for (int i = 0; i <= L; ++i) {
-    HIP_OK(hipEventRecord(c->lanes[i].done, c->lanes[i].s));
-    HIP_OK(hipStreamWaitEvent(s, c->lanes[i].done, 0));
-  }
-  if (trace_on()) {
-    for (int i = 0; i <= L; ++i) {
-      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-      unsigned long long id = 0;
-      const hipError_t e = hipStreamGetCaptureInfo(c->lanes[i].s, &st, &id);
-      OFDIS_TRACE("pipeline: lane %d (%p) capture status %d id %llu (err %d)", i, (void *)c->lanes[i].s, (int)st, id, (int)e);
-    }
-  }
-  return OFDIS_OK;
-}
-
 int issue(ofdis_context *c, const CallPlan &cp, hipStream_t s, const ofdis_params *p, const uint8_t *img_a,
           const uint8_t *img_b, const float *init, float *flow_out) {
   switch (cp.kind) {
     case CallPlan::kRoundRobin: return issue_round_robin(c, cp, s, p, img_a, img_b, init, flow_out);
-    case CallPlan::kPipeline: return issue_pipeline(c, cp, s, p, img_a, img_b, init, flow_out);
     default: return run_chunk(c, c->ws, cp.whole, p, img_a, img_b, init, flow_out, s);
   }
 }
@@ -1095,12 +964,8 @@ int run_batch(ofdis_context *c, hipStream_t s, const uint8_t *img_a, const uint8
   int rc = prepare(c, p, n, width, height, init != nullptr, capturing, cp);
   if (rc) return rc;
   OFDIS_TRACE("run_batch: kind %d, %d chunks of %d, %d lanes", (int)cp.kind, cp.nchunks, cp.chunk, cp.lanes);
-  // graph 1: capture single-stream batches; graph 2: also the multi-lane (fork / join) issues, the two-stream
-  // pipeline only where the HIP runtime captures it correctly (pipeline_capture_ok); graph 3: capture it
-  // regardless (the probe of that runtime bug, tools/graph_probe.py)
-  const bool graph = c->opt_graph == 3 ||
-                     (c->opt_graph == 2 && (cp.kind != CallPlan::kPipeline || pipeline_capture_ok())) ||
-                     (c->opt_graph == 1 && cp.kind == CallPlan::kSingle);
+  // graph 1: capture single-stream batches; graph 2: also the multi-lane (fork / join) issues
+  const bool graph = c->opt_graph == 2 || (c->opt_graph == 1 && cp.kind == CallPlan::kSingle);
   if (!graph || capturing || c->timing) return issue(c, cp, s, p, img_a, img_b, init, flow_out);
   // ~80 dependent launches per chunk: record them once as a HIP graph (on the context's own stream -- the
   // caller's may be the legacy NULL stream, which cannot capture) and replay it on the caller's stream while
@@ -1317,8 +1182,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
     int lo, hi;
   };
   static const Opt opts[] = {
-      {"pipeline", &ofdis_context::opt_pipeline, 0, 4},     {"split_cus", &ofdis_context::opt_split_cus, 0, 7},
-      {"chain_cus", &ofdis_context::opt_chain_cus, 0, 8},      {"stagger", &ofdis_context::opt_stagger, 0, 1},     {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
+      {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
       {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},
@@ -1328,13 +1192,12 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},
-      {"graph", &ofdis_context::opt_graph, 0, 3},
+      {"graph", &ofdis_context::opt_graph, 0, 2},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},  {"patch_fdiv", &ofdis_context::opt_patch_fdiv, 0, 1},
       {"patch_maxres", &ofdis_context::opt_patch_maxres, 0, 1},
-      {"sysor", &ofdis_context::opt_sysor, 0, 1},
       {"streams", &ofdis_context::opt_streams, 0, 16},      {"chunk", &ofdis_context::opt_chunk, 0, 1 << 30},
   };
   for (const Opt &o : opts) {
@@ -1393,8 +1256,9 @@ int ofdis_algorithmic_bytes(const ofdis_params *p, int width, int height, const 
     const double px = (double)g.w * g.h;
     const int n_inner = p->usetvref ? p->tv_innerit * (g.level + 1) : 0;
     if (k == "tv_sor") b += n_inner * p->tv_solverit * px * (nop == 2 ? 44.0 : 24.0);
-    // fused system + SOR: wx, wy, du, dv and the eight derivative planes in, du, dv out -- once per inner iteration
-    if (k == "tv_sysor") b += n_inner * px * 4.0 * (2 * nop + 8 * noc + nop);
+    // fused red-black level (latency form): wx, wy and the eight derivative planes in, the flow out -- once per level
+    // (the later inner iterations re-read the derivative planes from the frame's L2-resident copy)
+    if (k == "tv_level" && n_inner > 0) b += px * 4.0 * (2 * nop + 8 * noc);
     if (k == "tv_system") b += n_inner * px * (4.0 * (8 * noc + 1 + 2 * nop) + 4.0 * (nop == 2 ? 7 : 4));
     // patch: per patch the template + gradients, ONE (p+1)^2 target window, the outputs (the compulsory bytes;
     // re-reads of the window over the iterations are cache-resident, and the kernel is VALU-issue bound)

@@ -9,6 +9,8 @@
 // the reference's CMakeLists.txt:36-61.  Images: PNG and Netpbm, decoded with cv::imread's semantics
 // (ofdis_read_image; OpenCV is not in this image).  Unlike the reference, argv is validated (the
 // reference reads past argv for 6 <= argc < 24, run_dense.cpp:270-295).
+// OFDIS_CLI_TIMING=1 adds a per-process breakdown on stderr (HIP runtime init + context creation with the code-object
+// load, the call, the file write; tools/cli_wall.py): the reference's stdout timers stay as they are.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -35,14 +37,21 @@ static std::vector<uint8_t> load(const char *path, int &w, int &h) {
     rc = ofdis_read_image(path, px.data(), &w, &h, NOCHANNELS, px.size());
   }
   if (rc != OFDIS_OK) {
-    std::fprintf(stderr, "cannot read %s (PNG or Netpbm expected): %s\n", path, ofdis_status_string(rc));
+    std::fprintf(stderr, "cannot read %s (PNG, Netpbm or BMP expected): %s\n", path, ofdis_status_string(rc));
     std::exit(1);
   }
   return px;
 }
 
+static double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
 int main(int argc, char **argv) {
   auto t0 = std::chrono::steady_clock::now();
+  const auto tproc = t0;
+  const char *tenv = std::getenv("OFDIS_CLI_TIMING");
+  const bool cli_timing = tenv && std::atoi(tenv) != 0;
   // argv[24] / argv[25]: "hasinfile" and the initial-flow file, the reference's commented-out plumbing
   // (run_dense.cpp:293-294): a .flo (OF) / float depth .flo (DE) of the input size
   const bool hasinfile = argc == 26 && std::atoi(argv[24]) != 0;
@@ -75,8 +84,11 @@ int main(int argc, char **argv) {
   if (p.verbosity > 1)
     std::printf("TIME (Image loading     ) (ms): %3g\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  const double load_ms = ms_since(t0);
   ofdis_context *ctx = nullptr;
+  auto tc = std::chrono::steady_clock::now();
   rc = ofdis_context_create(0, &ctx);
+  const double ctx_ms = ms_since(tc);
   if (rc != OFDIS_OK) {
     std::fprintf(stderr, "no usable gfx950 device: %s\n", ofdis_status_string(rc));
     return 1;
@@ -93,9 +105,13 @@ int main(int argc, char **argv) {
       return 1;
     }
   }
+  auto tr = std::chrono::steady_clock::now();
   rc = ofdis_run_batch_u8_init_host(ctx, a.data(), b.data(), hasinfile ? init.data() : nullptr, 1, w, h, &p,
                                     flow.data());
+  const double run_ms = ms_since(tr);
+  tr = std::chrono::steady_clock::now();
   ofdis_context_destroy(ctx);
+  const double destroy_ms = ms_since(tr);
   if (rc != OFDIS_OK) {
     std::fprintf(stderr, "flow computation failed: %s\n", ofdis_status_string(rc));
     return 1;
@@ -106,8 +122,11 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "cannot write %s\n", argv[3]);
     return 1;
   }
-  if (p.verbosity > 1)
-    std::printf("TIME (Saving flow file  ) (ms): %3g\n",
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  const double write_ms = ms_since(t0);
+  if (p.verbosity > 1) std::printf("TIME (Saving flow file  ) (ms): %3g\n", write_ms);
+  if (cli_timing)
+    std::fprintf(stderr,
+                 "cli_ms load %.3f context_create %.3f call %.3f context_destroy %.3f write %.3f main_total %.3f\n",
+                 load_ms, ctx_ms, run_ms, destroy_ms, write_ms, ms_since(tproc));
   return 0;
 }

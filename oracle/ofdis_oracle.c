@@ -1034,7 +1034,80 @@ void ofo_sor_point_de(float *du, const float *a11, const float *b1, const float 
       }
 }
 
-/* ------------------------------------------------------------------ VarRefClass (refine_variational.cpp) */
+/* Red-black order of the same per-pixel SOR updates -- NOT a reference function: the checker of the GPU's opt-in
+ * sor_mode = 1 (k_tv_level_rb / k_tv_sor_rb), whose iteration differs from solver.c's lexicographic
+ * one.  Same operands and the same rounding order per update as sor_coupled (solver.c:83-433: the in-place 2x2 inverse
+ * of :122-128 with the border forms :131-190, the right-hand-side trees :241-300) and the DE point form (solver.c:
+ * 439-471); only the order changes: every pixel with x + y even, then every odd one, `iterations` times.  Within a
+ * colour the updates are independent (every neighbour has the other colour), so the loop order inside it is free. */
+static int g_sor_order = 0; /* 0 lexicographic (the reference), 1 red-black */
+void ofo_set_sor_order(int order) { g_sor_order = order; }
+int ofo_get_sor_order(void) { return g_sor_order; }
+
+void ofo_sor_rb_of(float *du, float *dv, float *a11, float *a12, float *a22, const float *b1, const float *b2,
+                   const float *hh, const float *vv, int w, int hgt, int iterations, float omega) {
+  if (w < 2 || hgt < 2 || iterations < 1) {
+    ofo_sor_point_of(du, dv, a11, a12, a22, b1, b2, hh, vv, w, hgt, iterations, omega);
+    return;
+  }
+  for (int y = 0; y < hgt; ++y) /* the inverse of sor_coupled's first sweep, for every pixel up front */
+    for (int x = 0; x < w; ++x) {
+      size_t o = (size_t)y * w + x;
+      const float hl = x > 0 ? hh[o - 1] : 0.0f, hr = hh[o];
+      float dpsis;
+      if (y == 0) dpsis = hl + (hr + vv[o]);
+      else if (y < hgt - 1) dpsis = (hl + hr) + (vv[o - w] + vv[o]);
+      else dpsis = hl + (hr + vv[o - w]);
+      float A11 = a22[o] + dpsis, A22 = a11[o] + dpsis, m12 = a12[o];
+      float det = A11 * A22 - m12 * m12;
+      a11[o] = A11 / det;
+      a22[o] = A22 / det;
+      a12[o] = m12 / (0.0f - det);
+    }
+  for (int it = 0; it < iterations; ++it)
+    for (int colour = 0; colour < 2; ++colour)
+      for (int y = 0; y < hgt; ++y)
+        for (int x = (y + colour) & 1; x < w; x += 2) {
+          size_t o = (size_t)y * w + x;
+          const float hl = x > 0 ? hh[o - 1] : 0.0f, hr = hh[o];
+          const float ur = x < w - 1 ? du[o + 1] : 0.0f, vr = x < w - 1 ? dv[o + 1] : 0.0f;
+          float s1, s2;
+          if (y == 0) {
+            s1 = (b1[o] + hr * ur) + vv[o] * du[o + w];
+            s2 = (b2[o] + hr * vr) + vv[o] * dv[o + w];
+          } else if (y < hgt - 1) {
+            const float vt = vv[o - w];
+            s1 = ((hr * ur) + vt * du[o - w]) + (b1[o] + vv[o] * du[o + w]);
+            s2 = ((hr * vr) + vt * dv[o - w]) + (b2[o] + vv[o] * dv[o + w]);
+          } else {
+            const float vt = vv[o - w];
+            s1 = (b1[o] + hr * ur) + vt * du[o - w];
+            s2 = (b2[o] + hr * vr) + vt * dv[o - w];
+          }
+          const float B1 = x == 0 ? s1 : hl * du[o - 1] + s1;
+          const float B2 = x == 0 ? s2 : hl * dv[o - 1] + s2;
+          const float u0 = du[o], v0 = dv[o];
+          du[o] = u0 + omega * (a11[o] * B1 + a12[o] * B2 - u0);
+          dv[o] = v0 + omega * (a12[o] * B1 + a22[o] * B2 - v0);
+        }
+}
+
+void ofo_sor_rb_de(float *du, const float *a11, const float *b1, const float *hh, const float *vv, int w, int hgt,
+                   int iterations, float omega) {
+  for (int it = 0; it < iterations; ++it)
+    for (int colour = 0; colour < 2; ++colour)
+      for (int j = 0; j < hgt; ++j)
+        for (int i = (j + colour) & 1; i < w; i += 2) {
+          float su = 0.0f, sd = 0.0f;
+          size_t o = (size_t)j * w + i;
+          if (j > 0) { su -= vv[o - w] * du[o - w]; sd += vv[o - w]; }
+          if (i > 0) { su -= hh[o - 1] * du[o - 1]; sd += hh[o - 1]; }
+          if (j < hgt - 1) { su -= vv[o] * du[o + w]; sd += vv[o]; }
+          if (i < w - 1) { su -= hh[o] * du[o + 1]; sd += hh[o]; }
+          float A11 = a11[o] + sd, B1 = b1[o] - su;
+          du[o] = (1.0f - omega) * du[o] + omega * (B1 / A11);
+        }
+}
 
 /* ------------------------------------------------------------------ VarRefClass (refine_variational.cpp) */
 
@@ -1082,6 +1155,8 @@ static int var_refine(const cam_t *c, const opt_t *o, const ofdis_params *p, con
       ofo_sub_laplacian(b2, wy, sh, sv, w, h);
       if (p->omp_build) /* refine_variational.cpp:202-203 (#ifdef _OPENMP) */
         ofo_sor_point_of(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
+      else if (g_sor_order == 1)
+        ofo_sor_rb_of(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
       else
         ofo_sor_coupled(du, dv, a11, a12, a22, b1, b2, sh, sv, w, h, p->tv_solverit, omega);
       for (size_t i = 0; i < n; ++i) {
@@ -1091,7 +1166,10 @@ static int var_refine(const cam_t *c, const opt_t *o, const ofdis_params *p, con
     } else {
       ofo_compute_data_de(a11, b1, mask, du, Ix, Iy, Iz, Ixx, Ixy, Iyy, Ixz, Iyz, w, h, noc, hdo3, hgo3);
       ofo_sub_laplacian(b1, wx, sh, sv, w, h);
-      ofo_sor_point_de(du, a11, b1, sh, sv, w, h, p->tv_solverit, omega);
+      if (g_sor_order == 1)
+        ofo_sor_rb_de(du, a11, b1, sh, sv, w, h, p->tv_solverit, omega);
+      else
+        ofo_sor_point_de(du, a11, b1, sh, sv, w, h, p->tv_solverit, omega);
       for (size_t i = 0; i < n; ++i)
         uu[i] = (c->camlr == 0) ? ssemin(wx[i] + du[i], 0.0f) : ssemax(wx[i] + du[i], 0.0f);
     }

@@ -101,6 +101,14 @@ void ofo_sor_point_of(float *du, float *dv, const float *a11, const float *a12, 
 /* sor_coupled_slow_but_readable_DE (solver.c:439-471) */
 void ofo_sor_point_de(float *du, const float *a11, const float *b1, const float *h, const float *v, int w,
                       int hgt, int iterations, float omega);
+/* Red-black order of the same updates (NOT a reference function: the checker of the GPU's opt-in sor_mode = 1).
+ * ofo_set_sor_order(1) makes every later refinement (ofo_run_u8*, ofo_refine_level) use it; 0 restores solver.c's. */
+void ofo_set_sor_order(int order);
+int ofo_get_sor_order(void);
+void ofo_sor_rb_of(float *du, float *dv, float *a11, float *a12, float *a22, const float *b1, const float *b2,
+                   const float *h, const float *v, int w, int hgt, int iterations, float omega);
+void ofo_sor_rb_de(float *du, const float *a11, const float *b1, const float *h, const float *v, int w, int hgt,
+                   int iterations, float omega);
 
 #ifdef __cplusplus
 }

@@ -83,11 +83,32 @@ def lib():
         L.ofo_sor_coupled.argtypes = [_f32p] * 9 + [C.c_int, C.c_int, C.c_int, C.c_float]
         L.ofo_sor_point_de.argtypes = [_f32p] * 5 + [C.c_int, C.c_int, C.c_int, C.c_float]
         L.ofo_sor_point_of.argtypes = [_f32p] * 9 + [C.c_int, C.c_int, C.c_int, C.c_float]
+        L.ofo_sor_rb_of.argtypes = [_f32p] * 9 + [C.c_int, C.c_int, C.c_int, C.c_float]
+        L.ofo_sor_rb_de.argtypes = [_f32p] * 5 + [C.c_int, C.c_int, C.c_int, C.c_float]
+        L.ofo_set_sor_order.argtypes = [C.c_int]
+        L.ofo_get_sor_order.restype = C.c_int
         for f in ("ofo_params_oppoint", "ofo_build_pyramid", "ofo_build_pyramid_ex", "ofo_oflow", "ofo_upsample_crop", "ofo_run_u8",
                   "ofo_run_u8_init", "ofo_refine_level"):
             getattr(L, f).restype = C.c_int
         _lib = L
     return _lib
+
+
+class sor_order:
+    """Context manager: the oracle's refinements use red-black SOR order (1; the GPU's opt-in sor_mode = 1) or
+    solver.c's lexicographic order (0, the default) inside the block."""
+
+    def __init__(self, order: int):
+        self.order = order
+
+    def __enter__(self):
+        self.prev = lib().ofo_get_sor_order()
+        lib().ofo_set_sor_order(self.order)
+        return self
+
+    def __exit__(self, *exc):
+        lib().ofo_set_sor_order(self.prev)
+        return False
 
 
 def oppoint(op: int, width: int, mode: int = 1, noc: int = 1) -> Params:

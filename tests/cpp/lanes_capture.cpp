@@ -1,7 +1,7 @@
-// Graph capture of the two-stream pipeline issue through the C ABI, in a process of its own (its HIP calls
-// go to the ROCm runtime libofdis.so links, not to a runtime another library brought along).  An eager run,
-// then runs with option graph=GMODE (2: capture every issue the runtime supports capturing; 3: also force
-// it), each compared bitwise with the eager output.  Usage: pipe_capture [GMODE]   (prints "same 1" per run)
+// Graph capture of the multi-lane round robin (chunks forked over two streams and joined) through the C ABI, in a
+// process of its own (its HIP calls go to the ROCm runtime libofdis.so links, not to a runtime another library
+// brought along).  An eager run, then runs with option graph=GMODE (2: capture the multi-lane issues too), each
+// compared bitwise with the eager output.  Usage: lanes_capture [GMODE]   (prints "same 1" per run)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -29,9 +29,8 @@ int main(int argc, char **argv) {
   CK(ofdis_params_oppoint(&p, 2, w, 1, 1));
   ofdis_context *c = nullptr;
   CK(ofdis_context_create(0, &c));
-  CK(ofdis_context_set_option(c, "streams", 1));
+  CK(ofdis_context_set_option(c, "streams", 2));
   CK(ofdis_context_set_option(c, "chunk", 2));
-  CK(ofdis_context_set_option(c, "pipeline", 1));
   CK(ofdis_context_set_option(c, "graph", 0));
   CK(ofdis_run_batch_u8_host(c, ha.data(), hb.data(), n, w, h, &p, o1.data()));
   CK(ofdis_context_set_option(c, "graph", gmode));

@@ -136,7 +136,6 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("up_form", 0, 3),         # flow upsample with the horizontal taps once per output row (round 4's kernel)
     ("up_form", 1, 3),         # ... once per source row, 4-row blocks
     ("up_form", 2, 3),         # ... once per source row, 8-row blocks
-    ("sysor", 1, 0),           # levels <= 128 rows: system + SOR of an inner iteration in one launch (k_tv_sysor)
 ]
 
 
@@ -245,28 +244,20 @@ def test_batch_equals_singles(od, ctx):
     b = torch.from_numpy(np.stack([x[1] for x in pairs])).cuda()
     p = od.oppoint(2, w, 1, 1)
     outs = []
-    configs = ((1, 0, 1, 0), (1, 0, 1, 0), (1, 0, 0, 0), (3, 2, 1, 0), (4, 1, 1, 0), (3, 2, 2, 0), (3, 2, 2, 0),
-               (1, 2, 1, 1), (1, 2, 1, 1), (1, 2, 0, 1), (1, 1, 1, 1), (1, 3, 0, 1), (1, 2, 2, 1),
-               (1, 1, 0, 2), (1, 2, 0, 3), (2, 1, 0, -1), (3, 2, 2, -1))
-    for streams, chunk, graph, pipeline in configs:
-        # pipeline > 1: that many chain lanes; -1: the staggered round robin (option stagger)
-        ctx.set_option("stagger", int(pipeline < 0))
-        pipeline = max(pipeline, 0)
-        # whole batch on one stream (graph captured, then replayed; eager launches); chunks over streams (also
-        # captured with their fork / join); the two-stream pipeline (ragged last chunk; eager -- graph 2 under
-        # torch's HIP runtime too, see test_pipeline_capture_native)
+    configs = ((1, 0, 1), (1, 0, 1), (1, 0, 0), (3, 2, 1), (4, 1, 1), (3, 2, 2), (3, 2, 2), (2, 1, 0), (2, 3, 2),
+               (1, 2, 1), (1, 2, 0))
+    for streams, chunk, graph in configs:
+        # whole batch on one stream (graph captured, then replayed; eager launches); chunks round-robin over
+        # streams (also captured with their fork / join: graph 2); chunks one after another on one stream
         ctx.set_option("streams", streams)
         ctx.set_option("chunk", chunk)
         ctx.set_option("graph", graph)
-        ctx.set_option("pipeline", pipeline)
         o = ctx.run(a, b, p)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
     ctx.set_option("graph", 1)
     ctx.set_option("streams", 0)
     ctx.set_option("chunk", 0)
-    ctx.set_option("pipeline", 0)
-    ctx.set_option("stagger", 0)
     for f in range(n):
         single = ctx.run_host(pairs[f][0], pairs[f][1], p)
         for k, out in enumerate(outs):
@@ -347,23 +338,21 @@ def test_upsample_forms_bitexact(oracle, od, ctx, form, w, h, op, over):
     assert_bitexact(got, oracle.run_u8(a, b, q), f"up_form={form}")
 
 
-def test_pipeline_capture_native(od, tmp_path):
-    """The two-stream pipeline captured as a HIP graph (option graph=2) in a process of its own, i.e. under the
-    ROCm runtime libofdis.so links (>= 7.2): captured, replayed, bit-identical to its eager issue.  (Under the
-    runtime bundled with PyTorch the pipeline is issued eagerly: that runtime crashes in hipStreamEndCapture
-    on the lanes' mutual waits, tools/capture_repro.hip.)"""
+def test_lanes_capture_native(od, tmp_path):
+    """The multi-lane round robin captured as a HIP graph (option graph=2) in a process of its own, i.e. under the
+    ROCm runtime libofdis.so links: captured, replayed, bit-identical to its eager issue."""
     import subprocess
     from test_host_abi import ROOT
     libdir = os.path.dirname(od._lib.LIB_PATH)
-    exe = str(tmp_path / "pipe_capture")
+    exe = str(tmp_path / "lanes_capture")
     subprocess.run(["g++", "-std=c++14", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "pipe_capture.cpp"), "-L", libdir, "-lofdis",
+                    os.path.join(ROOT, "tests", "cpp", "lanes_capture.cpp"), "-L", libdir, "-lofdis",
                     f"-Wl,-rpath,{libdir}", "-o", exe], check=True, capture_output=True, timeout=300)
     r = subprocess.run([exe, "2"], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, OFDIS_TRACE="1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("same 1") == 2, r.stdout
-    assert "graph: capture (kind 2" in r.stderr and "graph: captured rc 0 end 0" in r.stderr, r.stderr[-2000:]
+    assert "graph: capture (kind 1" in r.stderr and "graph: captured rc 0 end 0" in r.stderr, r.stderr[-2000:]
 
 
 def test_oflow_hpp_dropin_program(oracle, od, tmp_path):

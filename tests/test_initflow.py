@@ -116,7 +116,7 @@ def test_gpu_init_bitexact(O, w, h, noc, mode, op, over):
 
 @pytest.mark.gpu
 def test_gpu_init_batch_paths(O):
-    """Batch with per-frame initial flows: one stream (graph), eager, round-robin chunks, pipeline."""
+    """Batch with per-frame initial flows: one stream (graph), eager, round-robin chunks (eager and captured)."""
     import torch
     import of_dis_amd as od
     w, h, n = 176, 96, 5
@@ -129,16 +129,15 @@ def test_gpu_init_batch_paths(O):
     ini = torch.from_numpy(np.stack(inits)).cuda()
     p = od.oppoint(2, w, 1, 1)
     ctx = od.Context(0)
-    for streams, chunk, graph, pipeline in ((1, 0, 1, 0), (1, 0, 1, 0), (1, 0, 0, 0), (2, 2, 1, 0), (1, 2, 1, 1)):
+    for streams, chunk, graph in ((1, 0, 1), (1, 0, 1), (1, 0, 0), (2, 2, 1), (2, 2, 2), (1, 2, 1)):
         ctx.set_option("streams", streams)
         ctx.set_option("chunk", chunk)
         ctx.set_option("graph", graph)
-        ctx.set_option("pipeline", pipeline)
         out = ctx.run(a, b, p, init=ini)
         torch.cuda.synchronize()
         o = out.cpu().numpy()
         for f in range(n):
-            assert np.array_equal(o[f].view(np.uint32), want[f].view(np.uint32)), (streams, chunk, graph, pipeline, f)
+            assert np.array_equal(o[f].view(np.uint32), want[f].view(np.uint32)), (streams, chunk, graph, f)
     ctx.close()
 
 
