@@ -523,6 +523,35 @@ def main():
         ctx.set_option("streams", args.streams)
         ctx.set_option("chunk", args.chunk)
 
+    # ---- the latency mode beside the exact default (sor_mode = 1: red-black SOR, each TV level's inner loop in one
+    # launch per frame): one pair per call, and a config-D shard (32 pairs per call, the pairs
+    # each of 8 GPUs gets of BASELINE's 256) -- its end-point difference against the exact path is in "parity" below
+    latency_mode = None
+    rb_out = None
+    if rank == 0 and world == 1 and not args.no_latency and not any(o.startswith("sor_mode") for o in args.option):
+        ctx.set_option("sor_mode", 1)
+        lat_rb = pair_latency(od, ctx, p, pairs[0], dev, torch)
+        n32 = min(32, B)
+        ctx.set_option("streams", 0)
+        ctx.set_option("chunk", 0)
+        for _ in range(max(1, args.warmup)):
+            ctx.run_ptr(a.data_ptr(), b.data_ptr(), n32, W, H, p, out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        t0s = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.run_ptr(a.data_ptr(), b.data_ptr(), n32, W, H, p, out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        t32 = time.perf_counter() - t0s
+        rb_out = out[:min(nd, n32)].cpu().numpy()
+        ctx.set_option("sor_mode", 0)
+        ctx.set_option("streams", args.streams)
+        ctx.set_option("chunk", args.chunk)
+        r32 = W * H * n32 * args.steps / t32 / 1e6
+        latency_mode = {"option": "sor_mode=1", "single_pair": lat_rb,
+                        "shard_32": {"pairs_per_call": n32, "mpix_s_per_gpu": round(r32, 2),
+                                     "ms_per_call": round(t32 / args.steps * 1e3, 3)},
+                        "exact_single_pair_device_ms_median": latency["device_ms_median"] if latency else None}
+
     # ---- host-buffer entry point (PCIe-inclusive; never the headline value)
     host_io = None
     if args.host_io and rank == 0:
@@ -558,6 +587,11 @@ def main():
             exact = np.array_equal(g.view(np.uint32), ref.view(np.uint32))
             sums[3] += int(exact)
             sums[4] += (1 + tiles_equal[k]) if exact else 0
+            if rb_out is not None and k < len(rb_out):  # the latency mode's output of the same pair vs the exact path
+                e = np.sqrt(((rb_out[k].astype(np.float64) - ref) ** 2).sum(-1))
+                latency_mode.setdefault("epe_vs_exact_cpu_ref", []).append(
+                    {"pair": k, "avg": round(float(e.mean()), 5), "p99": round(float(np.percentile(e, 99)), 4),
+                     "max": round(float(e.max()), 4)})
         if rank == 0 and world == 1:
             cpu = cpu_baseline(O, q, pairs, W, H, args.cpu_seconds, binary, args.config)
     if world > 1:
@@ -588,7 +622,8 @@ def main():
                        "parallelism": f"frame-sharded x{world}" + (" (rehearsal: ranks share the GPU)"
                                                                    if rehearsal else "")},
             "roofline": roofline, "roofline_tv_sor": roofline_sor, "cpu_baseline": cpu, "parity": parity,
-            "latency": latency, "host_io": host_io, "shard_of_8": shard8, "kernels": kernels,
+            "latency": latency, "latency_mode": latency_mode, "host_io": host_io, "shard_of_8": shard8,
+            "kernels": kernels,
         }
         if cpu:
             line["speedup_vs_cpu_1core"] = round(mpix / cpu["value"], 1)

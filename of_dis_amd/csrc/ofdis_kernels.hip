@@ -4025,6 +4025,7 @@ struct SorLane {
   f2v *cr2;
   float *crv;
   int w, h, y, s, lim, rmax, hplane;
+  unsigned yc[R];  // !SEL load slot: row y + 64 r clamped into the frame (lanes past h read row h - 1: in the plane)
   bool border[R], notop[R];
   float omega;
 #ifdef OFDIS_SOR_PROBE
@@ -4037,17 +4038,20 @@ struct SorLane {
     const unsigned r1 = FIRST ? (unsigned)sor_row2(d + 1, lim, rmax) * (unsigned)hplane : 0u;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      // SEL (launches with more frames than the chip holds at once): only the lanes whose pixel (d - yr, yr) is
-      // inside the frame fetch their own slot -- a plane row holds h slots, of which the folded layout gives the
-      // others to diagonal d -+ w, so every slot was fetched (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels
-      // (the PMC fetch excess); the other lanes read the row's first slot (one line they share;
-      // every use of their values is discarded by a select).  A select, not an exec-masked load: loads under a
-      // branch cost the prefetch (the wait-count pass then waits for them at the join: tv_sor 135 -> 166 us per
-      // launch).  !SEL (launches whose frames all fit the chip -- the latency regime): the lane-constant slot y + 64 r,
-      // no per-step vector address arithmetic on the step's critical path (the select cost the single pair's 18 SOR
-      // launches 0.50 -> 0.58 ms); its extra lines cost nothing when the chip is not full.
-      const unsigned yr = SEL ? (((unsigned)(d - (y + 64 * r)) < (unsigned)w && y + 64 * r < h) ? (unsigned)(y + 64 * r) : 0u)
-                              : (unsigned)(y + 64 * r);
+      // SEL (launches with more frames than the chip holds at once): a plane row holds h slots, of which the folded
+      // layout gives the ones outside the wave's in-frame run to diagonal d -+ w, so lane-constant slots fetch every
+      // slot (w + h + 2S - 3) / w ~ 1.6 times per call at B's levels (the PMC fetch excess).  Here
+      // the lane's row is clamped into the run [max(d - w + 1, 0), min(d, h - 1)] (bounds in SALU, one v_med3 per
+      // lane): a lane outside the frame reads a slot an in-frame lane of its wave reads, so the wave fetches the lines
+      // of its run only; every use of such a lane's values is discarded by a select.  (Round 4's form selected the
+      // row's first slot: compare, compare, select per load.  An exec-masked load costs the prefetch: the wait-count
+      // pass waits for it at the join, tv_sor 135 -> 166 us per launch.)  !SEL (launches whose frames all fit the
+      // chip -- the latency regime): the lane-constant slot, no per-step vector address arithmetic at all.
+      unsigned yr = yc[r];
+      if (SEL) {
+        const int lo = min(max(d - w + 1, 0), h - 1), hi = max(min(d, h - 1), 0);
+        yr = (unsigned)min(max(y + 64 * r, lo), hi);
+      }
       if (FIRST || CRN == 0) {
         const float4 *cp = C + (size_t)r0 * CW;
         B.c0[r] = cp[yr * CW];
@@ -4314,6 +4318,7 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int yr = y + 64 * r;
+      st.yc[r] = (unsigned)min(yr, a.h - 1);
       st.notop[r] = yr == 0;
       st.border[r] = yr == 0 || yr >= a.h - 1;
     }
@@ -5095,12 +5100,21 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
       }
     }
   }
+  // every other form: the same oversubscription rule for the in-frame load select
+  const bool sel = a.sor_cring >= 3 || (long)a.n > sor_frames_per_cu(lds, G * S) * device_cus();
+  auto go2 = [&](auto cr, auto sl) {
+    constexpr bool CR = decltype(cr)::value, SL = decltype(sl)::value;
+    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, CR, R, 0, false, SL><<<a.n, th, lds, s>>>(a);
+    else k_tv_sor_lanes<S, 2, 3, MAXT, CR, R, 0, false, SL><<<a.n, th, lds, s>>>(a);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
   if (cring) {
-    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, true, R><<<a.n, th, lds, s>>>(a);
-    else k_tv_sor_lanes<S, 2, 3, MAXT, true, R><<<a.n, th, lds, s>>>(a);
+    if (sel) go2(T_{}, T_{});
+    else go2(T_{}, F_{});
   } else {
-    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, false, R><<<a.n, th, lds, s>>>(a);
-    else k_tv_sor_lanes<S, 2, 3, MAXT, false, R><<<a.n, th, lds, s>>>(a);
+    if (sel) go2(F_{}, T_{});
+    else go2(F_{}, F_{});
   }
 }
 template <int S>

@@ -85,13 +85,64 @@ __device__ __forceinline__ LvNb lv_nb(int x, int y, int c, int w, int h, int E) 
   return n;
 }
 
+// The same where a missing neighbour may be any entry (the system's and the update's uses of it are selected away):
+// (p -+ 1) >> 1 and (p -+ w) >> 1 need no border test, right = left + 1 and down = up + w whatever the row, and only
+// the two indices that can leave the arrays are clamped -- a colour-1 pixel's upper neighbour in row 0 (below entry
+// 0), a colour-0 pixel's lower one in the last row (past 2 E: the s array ends there).  c is a compile-time colour.
+__device__ __forceinline__ LvNb lv_nb_any(int x, int y, int c, int w, int E) {
+  const int p = y * w + x, ob = (1 - c) * E;
+  LvNb n;
+  n.i[0] = c * E + (p >> 1);
+  n.i[1] = ob + ((p - 1) >> 1);
+  n.i[2] = n.i[1] + 1;
+  const int u = ob + ((p - w) >> 1);
+  n.i[3] = c ? max(u, 0) : u;
+  n.i[4] = c ? u + w : min(u + w, 2 * E - 1);
+  return n;
+}
+
+// rb_update's optical-flow update on (u, v) pairs: v_pk_mul_f32 / v_pk_add_f32 round each half like the scalar
+// instruction and the operations are rb_update's, in its order (sor_rhs's operand selects per component), so the
+// same bits in about half the VALU issue.
+__device__ __forceinline__ f2v rb_update_of_pk(const RbPix &d, bool hasl, bool hasr, bool border, bool notop,
+                                               float omega, f2v l, f2v r, f2v t, f2v b, f2v o) {
+  const f2v R = hasr ? r : f2v{0.0f, 0.0f};
+  const f2v X = f2v{d.hr, d.hr} * R, Y = f2v{d.vt, d.vt} * t, Z = f2v{d.vb, d.vb} * b;
+  const f2v Bv = f2v{d.b1, d.b2};
+  const f2v lft = X + (border ? Bv : Y);
+  const f2v rgt = (border ? f2v{-0.0f, -0.0f} : Bv) + (border ? (notop ? Z : Y) : Z);
+  const f2v s = lft + rgt;
+  const f2v B = hasl ? f2v{d.hl, d.hl} * l + s : s;
+  const f2v m = f2v{d.i11, d.i12} * f2v{B.x, B.x} + f2v{d.i12, d.i22} * f2v{B.y, B.y};
+  return o + f2v{omega, omega} * (m - o);
+}
+__device__ __forceinline__ f2v lv_f2(float2 v) { return f2v{v.x, v.y}; }
+
+// The eight derivative values of one owned pixel (per channel), read from the colour-split planes
+template <int NOC>
+struct LvDeriv {
+  float Ix[NOC], Iy[NOC], Iz[NOC], Ixx[NOC], Ixy[NOC], Iyy[NOC], Ixz[NOC], Iyz[NOC];
+};
+template <int NOC>
+__device__ __forceinline__ void lv_load_deriv(const TvArgs &a, int f, unsigned idx, LvDeriv<NOC> &D) {
+#pragma unroll
+  for (int ch = 0; ch < NOC; ++ch) {  // wave-uniform plane base + 32-bit offset (ldu)
+    const long pb = ((long)f * NOC + ch) * a.sp;
+    D.Ix[ch] = ldu(a.Ix + pb, idx); D.Iy[ch] = ldu(a.Iy + pb, idx); D.Iz[ch] = ldu(a.Iz + pb, idx);
+    D.Ixx[ch] = ldu(a.Ixx + pb, idx); D.Ixy[ch] = ldu(a.Ixy + pb, idx); D.Iyy[ch] = ldu(a.Iyy + pb, idx);
+    D.Ixz[ch] = ldu(a.Ixz + pb, idx); D.Iyz[ch] = ldu(a.Iyz + pb, idx);
+  }
+}
+
 template <int NOP, int NOC, int CPT>
 __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, int n_inner) {
   using V = typename LvV<NOP>::T;
   constexpr int MODE = NOP == 2 ? 0 : 2;
-  // CPT 4 (2,049..8,192 pixels): hl / vt of each update are re-derived from s in LDS (still the iteration's s during
-  // the half-sweeps) instead of being held for all eight pixels -- the registers the 1024-thread budget lacks
-  constexpr bool SLDS = CPT >= 4;
+  // CPT 4 (2,049..8,192 pixels): the four diffusivities of each update (hl, hr, vt, vb) are re-derived from s in LDS
+  // (still the iteration's s during the half-sweeps) instead of being held for all eight pixels -- the registers the
+  // 1024-thread budget lacks; the same sums as sys_finish's
+  constexpr bool SLDS = CPT >= 4 || (NOC == 3 && CPT >= 2);
+  constexpr bool PF = NOC == 1;  // colour images: 24 derivative values per pixel, no register room for a second buffer
   extern __shared__ float4 lv_raw[];
   const int w = a.w, h = a.h, wh = w * h, E = lat_entries(w, h), T = blockDim.x, f = blockIdx.x;
   V *UV = reinterpret_cast<V *>(lv_raw);               // [2 E] (du, dv)
@@ -122,9 +173,18 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, int n_inner) {
     }
   __syncthreads();
 
+  // the derivative planes of an owned pixel are read one pixel ahead of its system (two buffers, compile-time
+  // indexed; the first pixel's during the smoothness phase): the L2 round trip overlaps the previous system
+  // instead of opening each one.  Pixel j = c CPT + k is entry c E + threadIdx.x + T k (a missing one reads entry 0).
+  auto deriv_idx = [&](int j) -> unsigned {
+    const int c = j / CPT, k = j % CPT, e = threadIdx.x + T * k;
+    return (unsigned)lv_fresh(xy[c][k] < 0 ? 0 : c * E + e);
+  };
+  LvDeriv<NOC> dbuf[2];
 #pragma unroll 1
   for (int it = 0; it < n_inner; ++it) {
     const bool first = it == 0;
+    if (PF) lv_load_deriv<NOC>(a, f, deriv_idx(0), dbuf[0]);
     // ---- compute_smoothness (opticalflow_aux.c:138-160) on uu = wx + du over the clamped neighbourhood
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -152,19 +212,15 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, int n_inner) {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
+        const int j = c * CPT + k;
+        // the next pixel's derivatives are requested whether or not this thread owns pixel j
+        if (PF && j + 1 < 2 * CPT) lv_load_deriv<NOC>(a, f, deriv_idx(j + 1), dbuf[(j + 1) & 1]);
         if (xy[c][k] < 0) continue;
         const int q = lv_fresh(xy[c][k]), x = q & 0xffff, y = q >> 16;
-        const LvNb nb = lv_nb(x, y, c, w, h, E);
+        const LvNb nb = lv_nb_any(x, y, c, w, E);
         const int idx = nb.i[0];
-        float lIx[NOC], lIy[NOC], lIz[NOC], lIxx[NOC], lIxy[NOC], lIyy[NOC], lIxz[NOC], lIyz[NOC];
-#pragma unroll
-        for (int ch = 0; ch < NOC; ++ch) {  // wave-uniform plane base + 32-bit offset (ldu)
-          const long pb = ((long)f * NOC + ch) * a.sp;
-          const unsigned o = (unsigned)idx;
-          lIx[ch] = ldu(a.Ix + pb, o); lIy[ch] = ldu(a.Iy + pb, o); lIz[ch] = ldu(a.Iz + pb, o);
-          lIxx[ch] = ldu(a.Ixx + pb, o); lIxy[ch] = ldu(a.Ixy + pb, o); lIyy[ch] = ldu(a.Iyy + pb, o);
-          lIxz[ch] = ldu(a.Ixz + pb, o); lIyz[ch] = ldu(a.Iyz + pb, o);
-        }
+        if (!PF) lv_load_deriv<NOC>(a, f, deriv_idx(j), dbuf[0]);
+        const LvDeriv<NOC> &D = dbuf[PF ? j & 1 : 0];
         float S5[5], X5[5], Y5[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -176,13 +232,15 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, int n_inner) {
         const V uv = UV[idx];
         const float m = warp_mask(x, y, X5[0], Y5[0], w, h);
         float4 c0, c1;
-        sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, lv_x(uv), lv_y(uv), lIx, lIy, lIz, lIxx, lIxy, lIyy, lIxz,
-                              lIyz, c0, c1);
+        sys_compute<NOP, NOC>(a, x, y, S5, X5, Y5, m, lv_x(uv), lv_y(uv), D.Ix, D.Iy, D.Iz, D.Ixx, D.Ixy, D.Iyy,
+                              D.Ixz, D.Iyz, c0, c1);
         RbPix &r = d[c][k];
         if (NOP == 2) {
-          r.i11 = c0.x; r.i12 = c0.y; r.i22 = c0.w; r.b1 = c1.x; r.b2 = c1.y; r.hr = c1.z; r.vb = c1.w;
+          r.i11 = c0.x; r.i12 = c0.y; r.i22 = c0.w; r.b1 = c1.x; r.b2 = c1.y;
+          if (!SLDS) { r.hr = c1.z; r.vb = c1.w; }
         } else {
-          r.i11 = c0.x; r.i12 = 0.0f; r.i22 = 0.0f; r.b1 = c0.y; r.b2 = 0.0f; r.hr = c0.z; r.vb = c0.w;
+          r.i11 = c0.x; r.i12 = 0.0f; r.i22 = 0.0f; r.b1 = c0.y; r.b2 = 0.0f;
+          if (!SLDS) { r.hr = c0.z; r.vb = c0.w; }
         }
         // sh of the left pixel (s[x-1] + s[x]) and sv of the upper one (s[y-1] + s[y]): rb_load's hl / vt
         if (!SLDS) {
@@ -201,18 +259,24 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, int n_inner) {
         for (int k = 0; k < CPT; ++k) {
           if (xy[c][k] < 0) continue;
           const int q = lv_fresh(xy[c][k]), x = q & 0xffff, y = q >> 16;
-          const LvNb nb = lv_nb(x, y, c, w, h, E);
+          const LvNb nb = lv_nb_any(x, y, c, w, E);
           const V o = UV[nb.i[0]], l = UV[nb.i[1]], r = UV[nb.i[2]], t = UV[nb.i[3]], b = UV[nb.i[4]];
-          float u = lv_x(o), v = lv_y(o);
-          if (SLDS) {  // the same two sums as the system phase's
-            const float sc = S[nb.i[0]], sl = S[nb.i[1]], su = S[nb.i[3]];
+          if (SLDS) {
+            const float sc = S[nb.i[0]], sl = S[nb.i[1]], sr = S[nb.i[2]], su = S[nb.i[3]], sd = S[nb.i[4]];
             d[c][k].hl = x > 0 ? sl + sc : 0.0f;
             d[c][k].vt = y > 0 ? su + sc : 0.0f;
+            d[c][k].hr = x < w - 1 ? sc + sr : 0.0f;
+            d[c][k].vb = y < h - 1 ? sc + sd : 0.0f;
           }
-          rb_update<MODE>(d[c][k], x, y, w, h, a.omega, lv_x(l), lv_x(r), lv_x(t), lv_x(b), lv_y(l), lv_y(r),
-                          lv_y(t), lv_y(b), u, v);
-          if constexpr (NOP == 2) UV[nb.i[0]] = make_float2(u, v);
-          else UV[nb.i[0]] = u;
+          if constexpr (NOP == 2) {
+            const f2v n = rb_update_of_pk(d[c][k], x > 0, x < w - 1, y == 0 || y >= h - 1, y == 0, a.omega, lv_f2(l),
+                                          lv_f2(r), lv_f2(t), lv_f2(b), lv_f2(o));
+            UV[nb.i[0]] = make_float2(n.x, n.y);
+          } else {
+            float u = o, v = 0.0f;
+            rb_update<MODE>(d[c][k], x, y, w, h, a.omega, l, r, t, b, 0.0f, 0.0f, 0.0f, 0.0f, u, v);
+            UV[nb.i[0]] = u;
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();

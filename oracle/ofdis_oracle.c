@@ -143,42 +143,64 @@ static inline int reflect101(int i, int n) {
   return i;
 }
 
-static void sobel_level(const float *L, int w, int h, int noc, float *dx, float *dy) {
-  for (int y = 0; y < h; ++y)
-    for (int x = 0; x < w; ++x) {
-      int xm = reflect101(x - 1, w), xp = reflect101(x + 1, w);
-      int ym = reflect101(y - 1, h), yp = reflect101(y + 1, h);
-      for (int c = 0; c < noc; ++c) {
+/* One output value of the Sobel pair at (x, y), any position (reflect-101 border). */
+static inline void sobel_px(const float *L, int w, int h, int noc, int x, int y, float *dx, float *dy) {
+  int xm = reflect101(x - 1, w), xp = reflect101(x + 1, w);
+  int ym = reflect101(y - 1, h), yp = reflect101(y + 1, h);
+  for (int c = 0; c < noc; ++c) {
 #define PX(xx, yy) L[((yy) * w + (xx)) * noc + c]
-        float tm = PX(xp, ym) - PX(xm, ym);
-        float t0 = PX(xp, y) - PX(xm, y);
-        float tp = PX(xp, yp) - PX(xm, yp);
-        dx[(y * w + x) * noc + c] = (tm + tp) * 0.125f + t0 * 0.25f;
-        float sm = (PX(xm, ym) + PX(xp, ym)) * 0.125f + PX(x, ym) * 0.25f;
-        float sp = (PX(xm, yp) + PX(xp, yp)) * 0.125f + PX(x, yp) * 0.25f;
-        dy[(y * w + x) * noc + c] = sp - sm;
+    float tm = PX(xp, ym) - PX(xm, ym);
+    float t0 = PX(xp, y) - PX(xm, y);
+    float tp = PX(xp, yp) - PX(xm, yp);
+    dx[(y * w + x) * noc + c] = (tm + tp) * 0.125f + t0 * 0.25f;
+    float sm = (PX(xm, ym) + PX(xp, ym)) * 0.125f + PX(x, ym) * 0.25f;
+    float sp = (PX(xm, yp) + PX(xp, yp)) * 0.125f + PX(x, yp) * 0.25f;
+    dy[(y * w + x) * noc + c] = sp - sm;
 #undef PX
-      }
-    }
+  }
 }
 
-static void pad_level(const float *L, int w, int h, int noc, int pad, int replicate, float *out) {
-  int W = w + 2 * pad, H = h + 2 * pad;
-  for (int y = 0; y < H; ++y)
-    for (int x = 0; x < W; ++x) {
-      int sx = x - pad, sy = y - pad;
-      int inside = sx >= 0 && sx < w && sy >= 0 && sy < h;
-      for (int c = 0; c < noc; ++c) {
-        float v;
-        if (inside)
-          v = L[(sy * w + sx) * noc + c];
-        else if (replicate)
-          v = L[(clampi(sy, 0, h - 1) * w + clampi(sx, 0, w - 1)) * noc + c];
-        else
-          v = 0.0f;
-        out[(y * W + x) * noc + c] = v;
-      }
+/* The interior rows run as one contiguous loop over the row's values (the neighbours are fixed offsets: the
+ * compiler vectorises it, as OpenCV's SIMD Sobel is), the border pixels through sobel_px: same expressions. */
+static void sobel_level(const float *L, int w, int h, int noc, float *dx, float *dy) {
+  const int rs = w * noc;
+  for (int y = 0; y < h; ++y) {
+    if (y == 0 || y == h - 1 || w < 3) {
+      for (int x = 0; x < w; ++x) sobel_px(L, w, h, noc, x, y, dx, dy);
+      continue;
     }
+    sobel_px(L, w, h, noc, 0, y, dx, dy);
+    const float *restrict up = L + (size_t)(y - 1) * rs, *restrict mid = up + rs, *restrict dn = mid + rs;
+    float *restrict ox = dx + (size_t)y * rs, *restrict oy = dy + (size_t)y * rs;
+    for (int i = noc; i < rs - noc; ++i) {
+      const float tm = up[i + noc] - up[i - noc], t0 = mid[i + noc] - mid[i - noc], tp = dn[i + noc] - dn[i - noc];
+      ox[i] = (tm + tp) * 0.125f + t0 * 0.25f;
+      const float sm = (up[i - noc] + up[i + noc]) * 0.125f + up[i] * 0.25f;
+      const float sp = (dn[i - noc] + dn[i + noc]) * 0.125f + dn[i] * 0.25f;
+      oy[i] = sp - sm;
+    }
+    sobel_px(L, w, h, noc, w - 1, y, dx, dy);
+  }
+}
+
+/* copyMakeBorder: the level's rows copied whole, the border columns / rows replicated or zero. */
+static void pad_level(const float *L, int w, int h, int noc, int pad, int replicate, float *out) {
+  const int W = w + 2 * pad, H = h + 2 * pad;
+  for (int y = 0; y < H; ++y) {
+    const int sy = clampi(y - pad, 0, h - 1);
+    float *o = out + (size_t)y * W * noc;
+    const float *src = L + (size_t)sy * w * noc;
+    if (!replicate && (y < pad || y >= pad + h)) {
+      memset(o, 0, sizeof(float) * (size_t)W * noc);
+      continue;
+    }
+    memcpy(o + (size_t)pad * noc, src, sizeof(float) * (size_t)w * noc);
+    for (int x = 0; x < pad; ++x)
+      for (int c = 0; c < noc; ++c) {
+        o[x * noc + c] = replicate ? src[c] : 0.0f;
+        o[(pad + w + x) * noc + c] = replicate ? src[(w - 1) * noc + c] : 0.0f;
+      }
+  }
 }
 
 int ofo_build_pyramid(const uint8_t *img, int width, int height, int noc, int sc_f, int sc_l, int imgpadding,
@@ -201,8 +223,10 @@ int ofo_build_pyramid_ex(const uint8_t *img, int width, int height, int noc, int
       const uint8_t *r0 = img + (size_t)(2 * y) * w * noc, *r1 = r0 + (size_t)w * noc;
       float *o = cur + (size_t)y * rn;
       if (noc == 1) {
+        /* the sums of u8 samples are exact integers (< 2^11): summed as integers, converted once -- the same value
+         * as the float sums, in a form the compiler vectorises like OpenCV's resize does */
         for (int x = 0; x < nw; ++x)
-          o[x] = (((float)r0[2 * x] + (float)r0[2 * x + 1]) + ((float)r1[2 * x] + (float)r1[2 * x + 1])) * 0.25f;
+          o[x] = (float)(((int)r0[2 * x] + (int)r0[2 * x + 1]) + ((int)r1[2 * x] + (int)r1[2 * x + 1])) * 0.25f;
       } else {
         for (int x = 0; x < nw; ++x)
           for (int c = 0; c < noc; ++c) {
@@ -235,6 +259,10 @@ int ofo_build_pyramid_ex(const uint8_t *img, int width, int height, int noc, int
       for (int y = 0; y < nh; ++y) {
         const float *r0 = cur + (size_t)(2 * y) * w * noc, *r1 = r0 + (size_t)w * noc;
         float *o = nx + (size_t)y * nw * noc;
+        if (noc == 1) { /* compile-time channel stride: the loop vectorises */
+          for (int x = 0; x < nw; ++x) o[x] = ((r0[2 * x] + r0[2 * x + 1]) + (r1[2 * x] + r1[2 * x + 1])) * 0.25f;
+          continue;
+        }
         for (int x = 0; x < nw; ++x)
           for (int c = 0; c < noc; ++c) {
             const int i = 2 * x * noc + c;

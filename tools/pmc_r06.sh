@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 HBM traffic per kernel for every bench config: two rocprofv3 --pmc passes each (FETCH_SIZE, WRITE_SIZE: they
+# Round-6 HBM traffic per kernel for every bench config: two rocprofv3 --pmc passes each (FETCH_SIZE, WRITE_SIZE: they
 # do not fit one pass on gfx950), counters only, each pass its own run under its own time limit, at the pairs per
 # launch the bench config runs (bench.py config_tag).  Reduced by tools/pmc_traffic.py into gpurun_out/<out>/traffic.json
 # (copied to profiles/traffic.json afterwards, every entry carrying its source).
@@ -25,6 +25,6 @@ for spec in "$@"; do
     if [ $rc -ne 0 ]; then exit $rc; fi
   done
   python tools/pmc_traffic.py "$OUT/${CFG}_FETCH_SIZE" "$OUT/${CFG}_WRITE_SIZE" "$TAG" "$OUT/traffic.json" \
-    "profiles/r05/pmc (round 5: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, $CFG at $PL pairs per launch)"
+    "profiles/r06/pmc (round 6: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, $CFG at $PL pairs per launch)"
 done
 echo "== done $(date +%T)"

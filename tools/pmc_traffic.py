@@ -21,7 +21,7 @@ from collections import defaultdict
 LOGICAL = [
     (r"k_pyr_base", "pyr_base"), (r"k_pyr_down", "pyr_down"), (r"k_pyr_pad_grad", "pyr_pad_grad"),
     (r"k_patch", "patch"), (r"k_aggregate", "aggregate"), (r"k_tv_prep", "tv_prep"),
-    (r"k_tv_deriv", "tv_deriv"), (r"k_tv_smooth|k_tv_system|k_tv_smsys", "tv_system"), (r"k_tv_sysor", "tv_sysor"),
+    (r"k_tv_deriv", "tv_deriv"), (r"k_tv_smooth|k_tv_system|k_tv_smsys", "tv_system"), (r"k_tv_level", "tv_level"),
     (r"k_tv_sor", "tv_sor"),
     (r"k_tv_final", "tv_final"), (r"k_upsample", "upsample"),
 ]
