@@ -191,6 +191,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        A different iteration -- NOT the reference's bits: bit-exact against the oracle's
  *                        red-black restatement, end-point error gated against the exact path; the one option
  *                        that changes results.  For calls that cannot fill the chip (one pair, a few dozen);
+ *   "lat_fuse" (0/1, default 1): latency mode without a stage capture or usefbcon: each level's aggregation and
+ *                        prep run inside its refinement launch (0: their own launches; the same bits);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (patches of at most
  *                        448 values; larger ones always run the any-shape kernel);
  *   "patch_window" (0/1, default 1): p = 8 / 12 patches read their bilinear taps from an LDS copy of the
@@ -261,7 +263,8 @@ int ofdis_read_pnm(const char *path, uint8_t *pixels, int *width, int *height, i
  * OpenCV configures it, incl. png_set_rgb_to_gray(0.299, 0.587)) and Netpbm P1-P6 (colour -> gray with
  * OpenCV's fixed-point BGR2Gray) and BMP (BmpDecoder: 1/4/8-bit palette, 16-bit 555 / 565, 24-bit, 32-bit,
  * core / info / V4 / V5 headers, bottom-up or top-down; colour -> gray by the same BGR2Gray).  Output
- * [h][w][want_noc], BGR for 3.  pixels may be NULL to query the size.  OFDIS_ERR_UNSUPPORTED for other formats
+ * [h][w][want_noc], BGR for 3.  pixels may be NULL to query the size (PNG: from the checked chunk structure and
+ * header, nothing inflated; a corrupt stream then fails the pixel call).  OFDIS_ERR_UNSUPPORTED for other formats
  * (JPEG, TIFF, RLE-compressed BMP, ...), OFDIS_ERR_IO for corrupt files. */
 int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height, int want_noc, size_t capacity);
 

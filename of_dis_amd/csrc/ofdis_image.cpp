@@ -69,23 +69,31 @@ bool unfilter(uint8_t *data, int rows, size_t rb, int bpp) {
   std::vector<uint8_t> prev(rb, 0);
   uint8_t *out = data;  // rows are compacted in place: out lags the input by one byte per row
   const uint8_t *in = data;
+  const size_t bp = (size_t)bpp < rb ? (size_t)bpp : rb;
   for (int y = 0; y < rows; ++y) {
     const int ft = *in++;
     uint8_t *cur = out;
     std::memmove(cur, in, rb);
     in += rb;
-    for (size_t i = 0; i < rb; ++i) {
-      const int a = i >= (size_t)bpp ? cur[i - bpp] : 0, b = prev[i], c = i >= (size_t)bpp ? prev[i - bpp] : 0;
-      int v = cur[i];
-      switch (ft) {
-        case 0: break;
-        case 1: v += a; break;
-        case 2: v += b; break;
-        case 3: v += (a + b) >> 1; break;
-        case 4: v += paeth(a, b, c); break;
-        default: return false;
-      }
-      cur[i] = (uint8_t)v;
+    const uint8_t *pv = prev.data();
+    // one loop per filter type (the first bpp bytes have no left neighbour: a = c = 0)
+    switch (ft) {
+      case 0: break;
+      case 1:
+        for (size_t i = bp; i < rb; ++i) cur[i] = (uint8_t)(cur[i] + cur[i - bpp]);
+        break;
+      case 2:
+        for (size_t i = 0; i < rb; ++i) cur[i] = (uint8_t)(cur[i] + pv[i]);
+        break;
+      case 3:
+        for (size_t i = 0; i < bp; ++i) cur[i] = (uint8_t)(cur[i] + (pv[i] >> 1));
+        for (size_t i = bp; i < rb; ++i) cur[i] = (uint8_t)(cur[i] + ((cur[i - bpp] + pv[i]) >> 1));
+        break;
+      case 4:
+        for (size_t i = 0; i < bp; ++i) cur[i] = (uint8_t)(cur[i] + paeth(0, pv[i], 0));
+        for (size_t i = bp; i < rb; ++i) cur[i] = (uint8_t)(cur[i] + paeth(cur[i - bpp], pv[i], pv[i - bpp]));
+        break;
+      default: return false;
     }
     std::memcpy(prev.data(), cur, rb);
     out += rb;
@@ -107,7 +115,7 @@ inline unsigned sample(const uint8_t *row, size_t s, int depth) {
 
 constexpr uint64_t kMaxImagePixels = 1ull << 30;
 
-int decode_png(const std::vector<uint8_t> &f, int want, Image &img) {
+int decode_png(const std::vector<uint8_t> &f, int want, Image &img, bool header_only = false) {
   static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
   if (f.size() < 8 || std::memcmp(f.data(), sig, 8) != 0) return OFDIS_ERR_IO;
   uint32_t W = 0, H = 0;
@@ -158,6 +166,12 @@ int decode_png(const std::vector<uint8_t> &f, int want, Image &img) {
     case 6: nch = 4; if (depth != 8 && depth != 16) return OFDIS_ERR_IO; break;
     default: return OFDIS_ERR_IO;
   }
+  if (header_only) {  // a size query (pixels == NULL): the chunk structure, CRCs and header checked, nothing inflated
+    img.w = (int)W;
+    img.h = (int)H;
+    img.c = want;
+    return OFDIS_OK;
+  }
   if (ctype == 3 && (plte.empty() || plte.size() % 3)) return OFDIS_ERR_IO;
   const int bpp = std::max(1, nch * depth / 8);
   auto row_bytes = [&](uint32_t w) { return ((size_t)w * nch * depth + 7) / 8; };
@@ -195,6 +209,10 @@ int decode_png(const std::vector<uint8_t> &f, int want, Image &img) {
     for (uint32_t y = 0; y < ph; ++y) {
       const uint8_t *r = sub + y * rb;
       uint16_t *dst = &smp[((size_t)(y0 + y * dy) * W) * nch];
+      if (depth == 8 && dx == 1 && x0 == 0) {  // the common case: one byte per sample, a whole row
+        for (size_t i = 0; i < (size_t)pw * nch; ++i) dst[i] = r[i];
+        continue;
+      }
       for (uint32_t x = 0; x < pw; ++x)
         for (int k = 0; k < nch; ++k) dst[(size_t)(x0 + x * dx) * nch + k] = (uint16_t)sample(r, (size_t)x * nch + k, depth);
     }
@@ -491,7 +509,7 @@ int ofdis_read_image(const char *path, uint8_t *pixels, int *width, int *height,
     Image img;
     int rc;
     if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G')
-      rc = decode_png(f, want_noc, img);
+      rc = decode_png(f, want_noc, img, pixels == nullptr);
     else if (f.size() >= 2 && f[0] == 'P' && f[1] >= '1' && f[1] <= '6')
       rc = decode_pnm(f, want_noc, img);
     else if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M')

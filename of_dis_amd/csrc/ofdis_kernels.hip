@@ -37,6 +37,7 @@ typedef float float4_v __attribute__((ext_vector_type(4)));
 namespace {
 
 #include "ofdis_tv_dev.inc"  // clampi, ssemin/max, skewed indexing, data term, smoothness, system
+#include "ofdis_agg_dev.inc"  // aggregation weights, slot planes, the own-grid gather
 
 inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
@@ -378,36 +379,6 @@ __device__ __forceinline__ float llt1_solve_fast(float L, const LltRcp &rc, floa
   const bool slow = !(rc.ok && mdiv_in(b) && mdiv_in(y));
   if (__builtin_amdgcn_ballot_w64(slow) != 0 && slow) x = llt1_solve(L, b);
   return x;
-}
-
-// The aggregation weight AggregateFlowDense gives patch pixel (lx, ly) -- a pixel of the level (patchgrid.cpp:236-262):
-// 1 / max(2, w) of its loss weight (gray); RGB: the upstream weight pointer advances by 1 for out-of-image pixels and
-// by 3 inside (patchgrid.cpp:243,256-258), so the three weights summed start at ly p + lx + 2 (in-image pixels
-// before it).  (ptx, pty): the patch's reference position.  Used by the aggregation on loss weights and by the patch
-// kernels that hand it the aggregation weights directly (PatchArgs::absw).
-__device__ __forceinline__ float agg_weight(const float *pw, int noc, int p, int w, int h, int ptx, int pty, int lx,
-                                            int ly) {
-  const int hp = p / 2;
-  if (noc == 1) return 1.0f / stdmaxf(2.0f, pw[ly * p + lx]);
-  const int lx0 = max(0, hp - ptx), lx1 = min(p, w - ptx + hp);
-  const int ly0 = max(0, hp - pty), ly1 = min(p, h - pty + hp);
-  const int nin = lx1 - lx0;
-  int before_in = max(0, min(ly, ly1) - ly0) * nin;
-  if (ly >= ly0 && ly < ly1) before_in += max(0, min(lx, lx1) - lx0);
-  const int off = ly * p + lx + 2 * before_in;
-  float absw = stdmaxf(2.0f, pw[off]);
-  absw = absw + stdmaxf(2.0f, pw[off + 1]);
-  absw = absw + stdmaxf(2.0f, pw[off + 2]);
-  return 1.0f / absw;
-}
-
-// Aggregation-weight slot planes (PatchArgs::absw / AggArgs::absw): per frame A * A planes of the level's w x h,
-// A = (p - 1) / steps + 1 -- the most patches of one grid column (row) that cover a pixel, consecutive in px (py),
-// so (px mod A, py mod A) tells apart every patch covering a pixel.  Patch (px, py) writes agg_weight of its pixel
-// (x, y) at plane (px mod A) A + py mod A, pixel (x, y): each plane pixel is written by at most one patch, and the
-// aggregation reads a pixel's weights as whole coalesced plane rows.
-__device__ __forceinline__ long agg_plane_off(int f, int A, int px, int py, int w, int h, int x, int y) {
-  return (((long)f * A * A + (px % A) * A + (py % A)) * h + y) * w + x;
 }
 
 template <int JM>
@@ -2549,37 +2520,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
 
 // ------------------------------------------------------------------------------------------------ aggregation
 
-__device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
-
-// Own-grid part of AggregateFlowDense (patchgrid.cpp:213-275) for pixel (x, y): the sums of weights and
-// weighted displacements, in the serial order (ascending patch id).
-__device__ __forceinline__ void aggregate_own(const AggArgs &a, int x, int y, int f, float &we, float &f0,
-                                              float &f1) {
-  const LevelGeom &g = a.g;
-  const int hp = a.p / 2;
-  // patches whose footprint [pt - p/2, pt + p/2 - 1] covers x, visited in ascending patch id
-  const int pxlo = max(0, -floordiv(-(x - hp + 1 - g.offw), a.steps));
-  const int pxhi = min(g.nopw - 1, floordiv(x + hp - g.offw, a.steps));
-  const int pylo = max(0, -floordiv(-(y - hp + 1 - g.offh), a.steps));
-  const int pyhi = min(g.noph - 1, floordiv(y + hp - g.offh, a.steps));
-  const float *PI = a.p_iter + (long)f * g.npatch * a.nop;
-  const float *PW = a.pweight + (long)f * g.npatch * a.novals;
-  for (int px = pxlo; px <= pxhi; ++px) {
-    const int ptx = px * a.steps + g.offw;
-    const int lx = x - ptx + hp;
-    for (int py = pylo; py <= pyhi; ++py) {
-      const int pty = py * a.steps + g.offh;
-      const int ly = y - pty + hp;
-      const int ip = px * g.noph + py;
-      const float absw = a.absw ? a.pweight[agg_plane_off(f, a.aslots, px, py, g.w, g.h, x, y)]
-                                : agg_weight(PW + (long)ip * a.novals, a.noc, a.p, g.w, g.h, ptx, pty, lx, ly);
-      we = we + absw;
-      f0 = f0 + PI[ip * a.nop] * absw;
-      if (a.nop == 2) f1 = f1 + PI[ip * a.nop + 1] * absw;
-    }
-  }
-}
-
 // Forward-backward merging (usefbcon, patchgrid.cpp:277-375): the complementary grid's patch q, at its
 // optimised position pos, splats -displacement * bilinear weight over its footprint; pixel (x, y) receives
 // the taps cc, fc, cf, ff of the loop positions (x, y), (x+1, y), (x, y+1), (x+1, y+1) in that order (the
@@ -2724,28 +2664,6 @@ __device__ __forceinline__ void tv_prep_values(const TvArgs &a, int x, int y, in
     v[3 + a.noc + ch] = w2 - i1;
   }
 #undef SB
-}
-// The same for channel ch alone: t, It of that channel, the flow (tv_prep_values' expressions: same bits).
-__device__ __forceinline__ void tv_prep_values_ch(const TvArgs &a, int x, int y, int f, int ch, float &t, float &it,
-                                                  float &wx, float &wy) {
-  const long plane = (long)a.w * a.h;
-  const long o = (long)y * a.w + x;
-  wx = a.flow[(long)f * a.nop * plane + o];
-  wy = a.nop == 2 ? a.flow[(long)f * a.nop * plane + plane + o] : 0.0f;
-  const float xx = (float)x + wx, yy = (float)y + wy;
-  const int xi = (int)floorf(xx), yi = (int)floorf(yy);
-  const float dx = xx - (float)xi, dy = yy - (float)yi;
-  const int x1 = clampi(xi, 0, a.w - 1), x2 = clampi(xi + 1, 0, a.w - 1);
-  const int y1 = clampi(yi, 0, a.h - 1), y2 = clampi(yi + 1, 0, a.h - 1);
-  const long fs = (long)a.W * (a.h + 2 * a.pad) * a.noc;
-  const float *B = a.img_b + f * fs, *A = a.img_a + f * fs;
-#define SB(xq, yq) B[((long)((yq) + a.pad) * a.W + (xq) + a.pad) * a.noc + ch]
-  const float w2 = SB(x1, y1) * (1.0f - dx) * (1.0f - dy) + SB(x2, y1) * dx * (1.0f - dy) +
-                   SB(x1, y2) * (1.0f - dx) * dy + SB(x2, y2) * dx * dy;
-#undef SB
-  const float i1 = A[((long)(y + a.pad) * a.W + x + a.pad) * a.noc + ch];
-  t = 0.5f * (w2 + i1);
-  it = w2 - i1;
 }
 // The values of pixel (x, y) into the skewed planes (du = dv = 0: the increment starts at zero).  The mask
 // is not stored: it is a function of (x, y, wx, wy), which the system kernels recompute (warp_mask) from the
@@ -5073,8 +4991,11 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
       const long cus = device_cus(), f32 = sor_frames_per_cu(ld32, G * S), f28 = sor_frames_per_cu(ld28, G * S);
       const bool cz = a.nop == 2 && (a.sor_cring == 3 || (a.sor_cring != 4 && f28 > f32 && (long)a.n > f32 * cus));
       const size_t ldsg = cz ? ld28 : ld32;
-      // the in-frame load select only where the launch oversubscribes the chip (sor_cring 3 / 4: everywhere, parity)
-      const bool sel = a.sor_cring >= 3 || (long)a.n > (cz ? f28 : f32) * cus;
+      // the clamped in-frame load form in throughput launches -- more frames than CUs -- and the lane-constant slots in
+      // latency launches, where the per-step v_med3 would sit on the wavefront's critical path (sor_cring 3 / 4:
+      // everywhere, parity).  Measured (profiles/r06/s5): B's tv_sor 111-113 us per 2048-pair launch either way, its
+      // counted bytes 1.36x -> 1.27x the compulsory ones; the single pair 0.84 -> 0.91 ms with it everywhere.
+      const bool sel = a.sor_cring >= 3 || (long)a.n > cus;
       auto go = [&](auto gc) {
         constexpr int CG = decltype(gc)::value;
         if (a.nop == 2) {
@@ -5100,8 +5021,8 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
       }
     }
   }
-  // every other form: the same oversubscription rule for the in-frame load select
-  const bool sel = a.sor_cring >= 3 || (long)a.n > sor_frames_per_cu(lds, G * S) * device_cus();
+  // every other form: the same rule for the clamped load form
+  const bool sel = a.sor_cring >= 3 || (long)a.n > device_cus();
   auto go2 = [&](auto cr, auto sl) {
     constexpr bool CR = decltype(cr)::value, SL = decltype(sl)::value;
     if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, CR, R, 0, false, SL><<<a.n, th, lds, s>>>(a);

@@ -107,6 +107,7 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
+  int opt_lat_fuse = 1;        // latency mode: the level's aggregation and prep inside its refinement launch
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw;
@@ -462,26 +463,11 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     ag.g = g;
     ag.cg_p_iter = P.fb ? pb.p_iter : nullptr;
     ag.cg_pweight = P.fb ? pb.pweight : nullptr;
-    if (times) HIP_OK(hipEventRecord(ev[3], s));
-    timed(c, 4, s, [&] { launch_aggregate(ag, s); });
     float *flow_bw = (float *)(ws + P.off_flow_bw[i]);
-    const bool bw_level = P.fb && sl > p->sc_l;  // the backward flow is not needed after the last scale
-    if (bw_level) {                               // patchgrid.cpp:213-397 with the roles swapped
-      AggArgs ab = ag;
-      ab.p_iter = pb.p_iter;
-      ab.pweight = pb.pweight;
-      ab.cg_p_iter = pa.p_iter;
-      ab.cg_pweight = pa.pweight;
-      ab.flow = flow_bw;
-      timed(c, 4, s, [&] { launch_aggregate(ab, s); });
-    }
-    if (times) HIP_OK(hipEventRecord(ev[4], s));
-    int rc = capture(c, s, c->cap_dis, sl, P, flow);
-    if (rc) return rc;
-
     const int n_inner = p->tv_innerit * (sl + 1);  // refine_variational.cpp:36
-    for (int dir = 0; dir < (bw_level ? 2 : 1) && p->usetvref && n_inner > 0; ++dir) {
-      // dir 1: VarRefClass on the backward flow with the images swapped (oflow.cpp:312-316)
+    // the refinement's arguments for direction dir (dir 1: VarRefClass on the backward flow with the images swapped,
+    // oflow.cpp:312-316)
+    auto make_tv = [&](int dir) {
       const long sp = skew_plane(g.w, g.h);
       const size_t pl = (size_t)n * sp;
       float *t0 = (float *)(ws + P.off_tv);
@@ -537,10 +523,38 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
+      return tv;
+    };
+    // latency mode without a stage capture or usefbcon: the level's aggregation and prep run inside its one
+    // refinement launch (k_tv_level_rb<..., FUSE>: the same expressions as k_aggregate / k_tv_prepd)
+    const bool fuse = c->opt_lat_fuse && p->usetvref && n_inner > 0 && !P.fb && c->cap_dis.empty() && c->cap_tv.empty() &&
+                      tv_level_rb_ok(make_tv(0));
+    if (times) HIP_OK(hipEventRecord(ev[3], s));
+    if (!fuse) timed(c, 4, s, [&] { launch_aggregate(ag, s); });
+    const bool bw_level = P.fb && sl > p->sc_l;  // the backward flow is not needed after the last scale
+    if (bw_level) {                               // patchgrid.cpp:213-397 with the roles swapped
+      AggArgs ab = ag;
+      ab.p_iter = pb.p_iter;
+      ab.pweight = pb.pweight;
+      ab.cg_p_iter = pa.p_iter;
+      ab.cg_pweight = pa.pweight;
+      ab.flow = flow_bw;
+      timed(c, 4, s, [&] { launch_aggregate(ab, s); });
+    }
+    if (times) HIP_OK(hipEventRecord(ev[4], s));
+    int rc = capture(c, s, c->cap_dis, sl, P, flow);
+    if (rc) return rc;
+
+    for (int dir = 0; dir < (bw_level ? 2 : 1) && p->usetvref && n_inner > 0; ++dir) {
+      TvArgs tv = make_tv(dir);
       // latency form of sor_mode = 1: the whole inner loop and the flow update in one launch per level, prep writing
       // the colour-split layout that launch reads (all eight derivative planes)
       tv.lat = tv_level_rb_ok(tv);
       tv.smsys_deriv = !tv.lat && tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
+      if (fuse) {
+        timed(c, 11, s, [&] { launch_tv_level_rb_fused(tv, ag, n_inner, s); });
+        continue;
+      }
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
       } else {
@@ -1195,6 +1209,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"graph", &ofdis_context::opt_graph, 0, 2},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
+      {"lat_fuse", &ofdis_context::opt_lat_fuse, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},  {"patch_fdiv", &ofdis_context::opt_patch_fdiv, 0, 1},
       {"patch_maxres", &ofdis_context::opt_patch_maxres, 0, 1},

@@ -100,6 +100,17 @@ def test_redblack_bitexact_vs_oracle_rb(oracle, od, rbctx, w, h, noc, mode, op, 
     _assert_bitexact(got, ref, "full-resolution flow")
 
 
+@pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in RB_CASES if not c[5].get("usefbcon")])
+def test_redblack_fused_level_bitexact(oracle, od, rbctx, w, h, noc, mode, op, over):
+    """Without a stage capture (and without usefbcon) the latency mode runs each level's aggregation and prep inside its
+    refinement launch (k_tv_level_rb<..., FUSE>): the full-resolution flow is still the oracle's red-black bits."""
+    a, b = od.synth_pair(w, h, noc, 2, mode)
+    p, q = _params(od, oracle, w, noc, mode, op, over)
+    with oracle.sor_order(1):
+        ref = oracle.run_u8(a, b, q)
+    _assert_bitexact(rbctx.run_host(a, b, p), ref, "full-resolution flow (fused levels)")
+
+
 # (W, H, noc, mode, op, frame, gate): the 0.05 px gate of SURVEY §8(c) at the op-point-2 configs (A, B / D);
 # the finer op-points 3 / 4 (more levels, finest scale 1 or 2) are reported against a looser 0.1 px ceiling
 # (measured round 2: 640x480 RGB op3 0.054 px average).
