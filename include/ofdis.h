@@ -191,8 +191,6 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        A different iteration -- NOT the reference's bits: bit-exact against the oracle's
  *                        red-black restatement, end-point error gated against the exact path; the one option
  *                        that changes results.  For calls that cannot fill the chip (one pair, a few dozen);
- *   "lat_fuse" (0/1, default 1): latency mode without a stage capture or usefbcon: each level's aggregation and
- *                        prep run inside its refinement launch (0: their own launches; the same bits);
  *   "wave_per_patch" (0/1): one wave64 per patch instead of eight lanes per patch (patches of at most
  *                        448 values; larger ones always run the any-shape kernel);
  *   "patch_window" (0/1, default 1): p = 8 / 12 patches read their bilinear taps from an LDS copy of the

@@ -175,7 +175,6 @@ void launch_tv_smsys(const TvArgs &a, hipStream_t s);
 void launch_tv_sor(const TvArgs &a, hipStream_t s);
 bool tv_level_rb_ok(const TvArgs &a);  // ofdis_tvrb.hip
 void launch_tv_level_rb(const TvArgs &a, int n_inner, hipStream_t s);
-void launch_tv_level_rb_fused(const TvArgs &a, const AggArgs &ag, int n_inner, hipStream_t s);
 void launch_tv_final(const TvArgs &a, hipStream_t s);
 void launch_upsample(const UpArgs &a, hipStream_t s);
 

@@ -107,7 +107,6 @@ struct ofdis_context {
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
   int opt_sor_mode = 0;        // 0 exact lexicographic order (the reference's bits); 1 red-black (opt-in)
-  int opt_lat_fuse = 1;        // latency mode: the level's aggregation and prep inside its refinement launch
   int opt_patch_window = 1;    // eight-lane patches read their bilinear taps from an LDS window (0: L1 gathers)
   int opt_patch_quad = 1;      // windowed gray patches on four lanes per patch (k_patchq; 0: eight, k_patchw)
   int opt_patch_x16 = 1;       // windowed RGB p = 12 patches on sixteen lanes per patch (k_patchx; 0: eight, k_patchw;
@@ -525,12 +524,8 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.prepd = c->opt_prepd;
       return tv;
     };
-    // latency mode without a stage capture or usefbcon: the level's aggregation and prep run inside its one
-    // refinement launch (k_tv_level_rb<..., FUSE>: the same expressions as k_aggregate / k_tv_prepd)
-    const bool fuse = c->opt_lat_fuse && p->usetvref && n_inner > 0 && !P.fb && c->cap_dis.empty() && c->cap_tv.empty() &&
-                      tv_level_rb_ok(make_tv(0));
     if (times) HIP_OK(hipEventRecord(ev[3], s));
-    if (!fuse) timed(c, 4, s, [&] { launch_aggregate(ag, s); });
+    timed(c, 4, s, [&] { launch_aggregate(ag, s); });
     const bool bw_level = P.fb && sl > p->sc_l;  // the backward flow is not needed after the last scale
     if (bw_level) {                               // patchgrid.cpp:213-397 with the roles swapped
       AggArgs ab = ag;
@@ -551,10 +546,6 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       // the colour-split layout that launch reads (all eight derivative planes)
       tv.lat = tv_level_rb_ok(tv);
       tv.smsys_deriv = !tv.lat && tv_deriv_fused(tv);  // before the prep launch: it decides which planes prepd writes
-      if (fuse) {
-        timed(c, 11, s, [&] { launch_tv_level_rb_fused(tv, ag, n_inner, s); });
-        continue;
-      }
       if (tv_prepd_ok(tv)) {
         timed(c, 5, s, [&] { launch_tv_prepd(tv, s); });
       } else {
@@ -1209,7 +1200,6 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"graph", &ofdis_context::opt_graph, 0, 2},
       {"patch_window", &ofdis_context::opt_patch_window, 0, 1}, {"patch_quad", &ofdis_context::opt_patch_quad, 0, 1},
       {"patch_generic", &ofdis_context::opt_patch_generic, 0, 1}, {"sor_mode", &ofdis_context::opt_sor_mode, 0, 1},
-      {"lat_fuse", &ofdis_context::opt_lat_fuse, 0, 1},
       {"patch_x16", &ofdis_context::opt_patch_x16, 0, 2},  {"patch_absw", &ofdis_context::opt_patch_absw, 0, 1},
       {"patch_buf", &ofdis_context::opt_patch_buf, 0, 1},  {"patch_fdiv", &ofdis_context::opt_patch_fdiv, 0, 1},
       {"patch_maxres", &ofdis_context::opt_patch_maxres, 0, 1},

@@ -27,15 +27,12 @@
 #include "ofdis_internal.h"
 #include "ofdis_math.h"
 
-#include <algorithm>
-
 #pragma clang fp contract(off)
 
 namespace ofdis {
 namespace {
 
 #include "ofdis_tv_dev.inc"
-#include "ofdis_agg_dev.inc"
 
 constexpr int kLvT = 1024, kLvCpt = 4;
 constexpr int kLvPix = 2 * kLvT * kLvCpt;  // 8192 pixels per level
@@ -137,12 +134,8 @@ __device__ __forceinline__ void lv_load_deriv(const TvArgs &a, int f, unsigned i
   }
 }
 
-// FUSE: the level's aggregation and prep run in this launch too (the latency mode without a capture or usefbcon):
-// AggregateFlowDense's gather per pixel into the level flow, then image_warp + get_derivatives on the whole level in
-// LDS (t, It, Ix, Iy: 16 B per pixel, before the refinement's arrays take the LDS over), the eight planes written in
-// the colour-split layout -- k_aggregate's and k_tv_prepd's expressions, so the same bits and two launches less.
-template <int NOP, int NOC, int CPT, bool FUSE>
-__global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, AggArgs ag, int n_inner) {
+template <int NOP, int NOC, int CPT>
+__global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, int n_inner) {
   using V = typename LvV<NOP>::T;
   constexpr int MODE = NOP == 2 ? 0 : 2;
   // CPT 4 (2,049..8,192 pixels): the four diffusivities of each update (hl, hr, vt, vb) are re-derived from s in LDS
@@ -157,76 +150,6 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, AggArgs ag, int 
   float *S = reinterpret_cast<float *>(WXY + 2 * E);   // [2 E] s
   const long fo = (long)f * a.sp;
 
-  if constexpr (FUSE) {
-    // ---- AggregateFlowDense, own grid (patchgrid.cpp:213-275; k_aggregate's gather and normalisation)
-    float *FLw = a.flow + (long)f * NOP * wh;
-    // 2 CPT pixels per thread at most (wh <= 2 T CPT): a compile-time trip count, so the loads of all of a thread's
-    // pixels can be in flight together instead of one L2 round trip per pixel
-#pragma unroll
-    for (int k = 0; k < 2 * CPT; ++k) {
-      const int p = threadIdx.x + k * T;
-      if (p >= wh) break;
-      const int y = p / w, x = p - y * w;
-      float we = 0.0f, f0 = 0.0f, f1 = 0.0f;
-      aggregate_own(ag, x, y, f, we, f0, f1);
-      if (we > 0) {
-        f0 = f0 / we;
-        f1 = f1 / we;
-      }
-      FLw[p] = f0;
-      if (NOP == 2) FLw[wh + p] = f1;
-    }
-    __syncthreads();
-    // ---- image_warp + get_derivatives (opticalflow_aux.c:31-132) with k_tv_prepd's expressions on the whole level:
-    // a tap outside the level reads the clamped pixel's value (the filters' replicate border)
-    float *T0 = reinterpret_cast<float *>(lv_raw), *DT = T0 + wh, *IX = DT + wh, *IY = IX + wh;
-#pragma unroll 1
-    for (int ch = 0; ch < NOC; ++ch) {
-#pragma unroll
-      for (int k = 0; k < 2 * CPT; ++k) {
-        const int p = threadIdx.x + k * T;
-        if (p >= wh) break;
-        const int y = p / w, x = p - y * w;
-        float t, it, wx, wy;
-        tv_prep_values_ch(a, x, y, f, ch, t, it, wx, wy);
-        T0[p] = t;
-        DT[p] = it;
-      }
-      __syncthreads();
-      for (int p = threadIdx.x; p < wh; p += T) {
-        const int y = p / w, x = p - y * w, r = y * w;
-        const int x0 = r + max(x - 2, 0), x1 = r + max(x - 1, 0), x3 = r + min(x + 1, w - 1), x4 = r + min(x + 2, w - 1);
-        const int y0 = max(y - 2, 0) * w + x, y1 = max(y - 1, 0) * w + x, y3 = min(y + 1, h - 1) * w + x;
-        const int y4 = min(y + 2, h - 1) * w + x;
-        IX[p] = kK5[0] * T0[x0] + ((kK5[1] * T0[x1] + kK5[2] * T0[p]) + (kK5[3] * T0[x3] + kK5[4] * T0[x4]));
-        IY[p] = kK5[0] * T0[y0] + ((kK5[1] * T0[y1] + kK5[2] * T0[p]) + (kK5[3] * T0[y3] + kK5[4] * T0[y4]));
-      }
-      __syncthreads();
-      for (int p = threadIdx.x; p < wh; p += T) {
-        const int y = p / w, x = p - y * w, r = y * w;
-        const int x0 = r + max(x - 2, 0), x1 = r + max(x - 1, 0), x3 = r + min(x + 1, w - 1), x4 = r + min(x + 2, w - 1);
-        const int y0 = max(y - 2, 0) * w + x, y1 = max(y - 1, 0) * w + x, y3 = min(y + 1, h - 1) * w + x;
-        const int y4 = min(y + 2, h - 1) * w + x;
-        auto c5h = [&](const float *P) {
-          return kK5[0] * P[x0] + ((kK5[1] * P[x1] + kK5[2] * P[p]) + (kK5[3] * P[x3] + kK5[4] * P[x4]));
-        };
-        auto c5v = [&](const float *P) {
-          return kK5[0] * P[y0] + ((kK5[1] * P[y1] + kK5[2] * P[p]) + (kK5[3] * P[y3] + kK5[4] * P[y4]));
-        };
-        const long q = ((long)f * NOC + ch) * a.sp + lat_idx(x, y, w, E);
-        a.Iz[q] = DT[p];
-        a.Ix[q] = IX[p];
-        a.Iy[q] = IY[p];
-        a.Ixx[q] = c5h(IX);
-        a.Ixy[q] = c5v(IX);
-        a.Iyy[q] = c5v(IY);
-        a.Ixz[q] = c5h(DT);
-        a.Iyz[q] = c5v(DT);
-      }
-      __syncthreads();
-    }
-  }
-
   int xy[2][CPT];  // x | y << 16 of the owned pixels, -1: none
   RbPix d[2][CPT];
 #pragma unroll
@@ -240,14 +163,11 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, AggArgs ag, int 
       const int y = p / w, x = p - y * w;
       xy[c][k] = x | (y << 16);
       const int idx = c * E + e;
-      // the level flow: the colour-split copy k_tv_prepd wrote, or (FUSE) the aggregated flow itself
-      const float *FL = a.flow + (long)f * NOP * wh;
-      const float wx = FUSE ? FL[p] : a.wxs[fo + idx], wy = NOP == 2 ? (FUSE ? FL[wh + p] : a.wys[fo + idx]) : 0.0f;
       if constexpr (NOP == 2) {
-        WXY[idx] = make_float2(wx, wy);
+        WXY[idx] = make_float2(a.wxs[fo + idx], a.wys[fo + idx]);
         UV[idx] = make_float2(0.0f, 0.0f);
       } else {
-        WXY[idx] = wx;
+        WXY[idx] = a.wxs[fo + idx];
         UV[idx] = 0.0f;
       }
     }
@@ -384,25 +304,14 @@ __global__ __launch_bounds__(kLvT) void k_tv_level_rb(TvArgs a, AggArgs ag, int 
     }
 }
 
-template <int NOP, int NOC, bool FUSE>
-void launch_level_rb_n(const TvArgs &a, const AggArgs &ag, int n_inner, hipStream_t s) {
+template <int NOP, int NOC>
+void launch_level_rb_n(const TvArgs &a, int n_inner, hipStream_t s) {
   const int E = lat_entries(a.w, a.h);
-  size_t lds = lv_lds(NOP, a.w, a.h);
-  if (FUSE) lds = std::max(lds, (size_t)16 * a.w * a.h);  // the prep's t, It, Ix, Iy
+  const size_t lds = lv_lds(NOP, a.w, a.h);
   auto threads = [](int per) { return (per + 63) / 64 * 64; };
-  if (E <= kLvT) k_tv_level_rb<NOP, NOC, 1, FUSE><<<a.n, threads(E), lds, s>>>(a, ag, n_inner);
-  else if (E <= 2 * kLvT) k_tv_level_rb<NOP, NOC, 2, FUSE><<<a.n, threads((E + 1) / 2), lds, s>>>(a, ag, n_inner);
-  else k_tv_level_rb<NOP, NOC, 4, FUSE><<<a.n, threads((E + 3) / 4), lds, s>>>(a, ag, n_inner);
-}
-template <bool FUSE>
-void launch_level_rb(const TvArgs &a, const AggArgs &ag, int n_inner, hipStream_t s) {
-  if (a.nop == 2) {
-    if (a.noc == 1) launch_level_rb_n<2, 1, FUSE>(a, ag, n_inner, s);
-    else launch_level_rb_n<2, 3, FUSE>(a, ag, n_inner, s);
-  } else {
-    if (a.noc == 1) launch_level_rb_n<1, 1, FUSE>(a, ag, n_inner, s);
-    else launch_level_rb_n<1, 3, FUSE>(a, ag, n_inner, s);
-  }
+  if (E <= kLvT) k_tv_level_rb<NOP, NOC, 1><<<a.n, threads(E), lds, s>>>(a, n_inner);
+  else if (E <= 2 * kLvT) k_tv_level_rb<NOP, NOC, 2><<<a.n, threads((E + 1) / 2), lds, s>>>(a, n_inner);
+  else k_tv_level_rb<NOP, NOC, 4><<<a.n, threads((E + 3) / 4), lds, s>>>(a, n_inner);
 }
 
 }  // namespace
@@ -420,11 +329,14 @@ bool tv_level_rb_ok(const TvArgs &a) {
          tv_prepd_ok(a) && lv_lds(a.nop, a.w, a.h) <= 160 * 1024 && (a.noc == 1 || a.noc == 3);
 }
 
-void launch_tv_level_rb(const TvArgs &a, int n_inner, hipStream_t s) { launch_level_rb<false>(a, AggArgs{}, n_inner, s); }
-
-// The same with the level's aggregation (own grid, no usefbcon) and prep in the launch (ag: k_aggregate's arguments)
-void launch_tv_level_rb_fused(const TvArgs &a, const AggArgs &ag, int n_inner, hipStream_t s) {
-  launch_level_rb<true>(a, ag, n_inner, s);
+void launch_tv_level_rb(const TvArgs &a, int n_inner, hipStream_t s) {
+  if (a.nop == 2) {
+    if (a.noc == 1) launch_level_rb_n<2, 1>(a, n_inner, s);
+    else launch_level_rb_n<2, 3>(a, n_inner, s);
+  } else {
+    if (a.noc == 1) launch_level_rb_n<1, 1>(a, n_inner, s);
+    else launch_level_rb_n<1, 3>(a, n_inner, s);
+  }
 }
 
 }  // namespace ofdis

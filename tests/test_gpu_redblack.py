@@ -100,15 +100,15 @@ def test_redblack_bitexact_vs_oracle_rb(oracle, od, rbctx, w, h, noc, mode, op, 
     _assert_bitexact(got, ref, "full-resolution flow")
 
 
-@pytest.mark.parametrize("w,h,noc,mode,op,over", [c for c in RB_CASES if not c[5].get("usefbcon")])
-def test_redblack_fused_level_bitexact(oracle, od, rbctx, w, h, noc, mode, op, over):
-    """Without a stage capture (and without usefbcon) the latency mode runs each level's aggregation and prep inside its
-    refinement launch (k_tv_level_rb<..., FUSE>): the full-resolution flow is still the oracle's red-black bits."""
+@pytest.mark.parametrize("w,h,noc,mode,op,over", RB_CASES)
+def test_redblack_uncaptured_bitexact(oracle, od, rbctx, w, h, noc, mode, op, over):
+    """The same geometries without a stage capture (the path the CLI and batches take): the full-resolution flow is
+    the oracle's red-black bits for another synthetic scene."""
     a, b = od.synth_pair(w, h, noc, 2, mode)
     p, q = _params(od, oracle, w, noc, mode, op, over)
     with oracle.sor_order(1):
         ref = oracle.run_u8(a, b, q)
-    _assert_bitexact(rbctx.run_host(a, b, p), ref, "full-resolution flow (fused levels)")
+    _assert_bitexact(rbctx.run_host(a, b, p), ref, "full-resolution flow (no capture)")
 
 
 # (W, H, noc, mode, op, frame, gate): the 0.05 px gate of SURVEY §8(c) at the op-point-2 configs (A, B / D);

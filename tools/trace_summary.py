@@ -21,16 +21,17 @@ def main():
     rows = list(csv.DictReader(open(path)))[skip:]
     agg = OrderedDict()
     for r in rows:
-        key = (short(r["Kernel_Name"]), r.get("Grid_Size_X", r.get("Grid_Size", "")), r.get("Workgroup_Size_X", ""),
-               r.get("LDS_Block_Size", r.get("Lds_Size", "")))
+        grid = "x".join(g for g in (r.get("Grid_Size_X", r.get("Grid_Size", "")), r.get("Grid_Size_Y", ""),
+                                       r.get("Grid_Size_Z", "")) if g not in ("", "1"))
+        key = (short(r["Kernel_Name"]), grid, r.get("Workgroup_Size_X", ""), r.get("LDS_Block_Size", r.get("Lds_Size", "")))
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         a = agg.setdefault(key, [0, 0.0])
         a[0] += 1
         a[1] += d
     tot = sum(v[1] for v in agg.values())
-    print(f"{'kernel':60s} {'grid':>9s} {'wg':>5s} {'lds':>7s} {'n':>6s} {'avg us':>9s} {'total us':>10s} {'%':>5s}")
+    print(f"{'kernel':60s} {'grid':>16s} {'wg':>5s} {'lds':>7s} {'n':>6s} {'avg us':>9s} {'total us':>10s} {'%':>5s}")
     for (k, g, wg, lds), (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        print(f"{k[:60]:60s} {g:>9s} {wg:>5s} {lds:>7s} {n:6d} {t / n:9.2f} {t:10.1f} {100 * t / tot:5.1f}")
+        print(f"{k[:60]:60s} {g:>16s} {wg:>5s} {lds:>7s} {n:6d} {t / n:9.2f} {t:10.1f} {100 * t / tot:5.1f}")
 
 
 if __name__ == "__main__":
