@@ -179,6 +179,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        or the register march (taller levels, intensity and colour images) run, the system kernel
  *                        filters Ixx, Ixy, Iyy, Ixz, Iyz from Ix, Iy, Iz and the prep launch does not write those
  *                        five planes (per channel);
+ *   "prepd_df" (0/1, default 1): on those levels the prep launch warps a 2-pixel halo with every channel in one pass
+ *                        and writes Ix, Iy, It only (k_tv_prepd_df; 0: k_tv_prepd's 4-pixel halo, channel by channel);
  *   "smsys_march" (0/1, default 1): levels taller than 256 rows run smoothness + system as a register march
  *                        (one wave per 60 columns x 64 rows, no LDS; takes precedence over smsys2d);
  *   "prepd" (0..2, default 2): image warp, temporal images and the derivative filters of a level in one launch

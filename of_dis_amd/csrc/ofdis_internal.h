@@ -128,6 +128,7 @@ struct TvArgs {
   int smsys_small;             // k_tv_smsys: ~1 pixel per thread when a launch cannot fill the chip
   int smsys_march;             // tall levels: the register march k_tv_smsys_m (takes precedence over smsys2d)
   int smsys_deriv;             // row-block k_tv_smsys, intensity images: Ixx .. Iyz computed from staged Ix, Iy, Iz
+  int prepd_df;                // smsys_deriv levels: the prep launch warps on a 2-pixel halo, all channels at once (k_tv_prepd_df)
                                // (k_tv_prepd then writes only Ix, Iy, Iz of the derivative planes); set by the
                                // runtime only where tv_deriv_fused() holds
   int sor_redblack;            // opt-in red-black SOR order (a different iteration: EPE-gated, not bit-exact)

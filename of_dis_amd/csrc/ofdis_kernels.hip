@@ -2739,9 +2739,8 @@ __device__ __forceinline__ float conv5v(const float *s, int x, int y, int w, int
 // plane written in skewed order (threads walk the tile's anti-diagonals: contiguous skewed rows).  A halo position
 // outside the level holds the value of the clamped position, which is exactly the filters' replicate border; every
 // value is the same expression as in k_tv_prep / k_tv_deriv1 / k_tv_deriv2: same bits, t / It / Ix / Iy never go
-// through memory.  Colour images (NOC 3, color_image_convolve_hv filters every channel alike: image.cpp:737-760) run
-// the three phases once per channel on the same LDS tiles (the warp positions are recomputed per channel: cheap),
-// writing that channel's eight planes.
+// through memory.  Intensity images; colour images (color_image_convolve_hv filters every channel alike:
+// image.cpp:737-760) take k_tv_prepd_c3 below, every phase over the three channels.
 constexpr int kPdW = 64, kPdH = 16;
 template <int NOC>
 __global__ __launch_bounds__(256) void k_tv_prepd(TvArgs a) {
@@ -2817,6 +2816,162 @@ __global__ __launch_bounds__(256) void k_tv_prepd(TvArgs a) {
       a.Iyy[q] = iyy;
       a.Ixz[q] = ixz;
       a.Iyz[q] = iyz;
+    }
+  }
+}
+
+// Colour images, all eight planes (levels whose system kernel reads them): k_tv_prepd<3> with the three channels in
+// each phase instead of the phases once per channel -- the flow, warp position and bilinear weights once per halo
+// position (tv_prep_values_all), It kept on the 2-pixel halo only (Ixz / Iyz), and two barriers instead of eight.
+// 78 KB of LDS: two workgroups per CU.  Same expressions, same bits.  Config C: 3.36 -> 3.15 ms of prep per
+// 512-pair step (r06_s11), the 240 x 135 level 554 -> 471 us per 256 pairs (r06_s12).
+__global__ __launch_bounds__(256) void k_tv_prepd_c3(TvArgs a) {
+  const uint3 xb = xcd_block();
+  constexpr int NOC = 3, H4 = kPdH + 8, W4 = kPdW + 8, H2 = kPdH + 4, W2 = kPdW + 4;
+  __shared__ float T[NOC][H4][W4], DT[NOC][H2][W2], IX[NOC][H2][W2], IY[NOC][H2][W2], WX[kPdH][kPdW], WY[kPdH][kPdW];
+  const int x0 = xb.x * kPdW, y0 = xb.y * kPdH, f = xb.z;
+  const int w = a.w, h = a.h;
+  constexpr int NPOS = H4 * W4, NIT = (NPOS + 255) / 256, PB = 2;
+#pragma unroll
+  for (int j0 = 0; j0 < NIT; j0 += PB) {
+    float t[PB][NOC], it[PB][NOC], wx[PB], wy[PB];
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int i = min((int)threadIdx.x + (j0 + j) * 256, NPOS - 1);
+      const int ly = i / W4, lx = i - ly * W4;
+      const int cx = clampi(x0 - 4 + lx, 0, w - 1), cy = clampi(y0 - 4 + ly, 0, h - 1);
+      tv_prep_values_all<NOC>(a, cx, cy, f, t[j], it[j], wx[j], wy[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int i = (int)threadIdx.x + (j0 + j) * 256;
+      if (j0 + j >= NIT || i >= NPOS) break;
+      const int ly = i / W4, lx = i - ly * W4;
+#pragma unroll
+      for (int ch = 0; ch < NOC; ++ch) T[ch][ly][lx] = t[j][ch];
+      const int hx = lx - 2, hy = ly - 2;
+      if (hx >= 0 && hx < W2 && hy >= 0 && hy < H2) {
+#pragma unroll
+        for (int ch = 0; ch < NOC; ++ch) DT[ch][hy][hx] = it[j][ch];
+      }
+      const int cxl = lx - 4, cyl = ly - 4;
+      if (cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < kPdH) {
+        WX[cyl][cxl] = wx[j];
+        WY[cyl][cxl] = wy[j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NOC * H2 * W2; i += 256) {
+    const int ch = i / (H2 * W2), r = i - ch * (H2 * W2);
+    const int ly = r / W2, lx = r - ly * W2;
+    const int cx = clampi(x0 - 2 + lx, 0, w - 1), cy = clampi(y0 - 2 + ly, 0, h - 1);
+    const int tx = cx - x0 + 4, ty = cy - y0 + 4;
+    IX[ch][ly][lx] = kK5[0] * T[ch][ty][tx - 2] + ((kK5[1] * T[ch][ty][tx - 1] + kK5[2] * T[ch][ty][tx]) +
+                                                  (kK5[3] * T[ch][ty][tx + 1] + kK5[4] * T[ch][ty][tx + 2]));
+    IY[ch][ly][lx] = kK5[0] * T[ch][ty - 2][tx] + ((kK5[1] * T[ch][ty - 1][tx] + kK5[2] * T[ch][ty][tx]) +
+                                                  (kK5[3] * T[ch][ty + 1][tx] + kK5[4] * T[ch][ty + 2][tx]));
+  }
+  __syncthreads();
+  constexpr int TD = kPdW + kPdH - 1;
+  for (int i = threadIdx.x; i < TD * kPdH; i += 256) {
+    const int yy = i & (kPdH - 1), dd = i / kPdH, xl = dd - yy;
+    const int x = x0 + xl, y = y0 + yy;
+    if (xl < 0 || xl >= kPdW || x >= w || y >= h) continue;
+    const int ix = xl + 2, iy = yy + 2;  // (DT, IX, IY: 2-pixel halo)
+    const long sk = a.lat ? lat_idx(x, y, w, lat_entries(w, h)) : skw(x, y, h, w, a.wrap), k = (long)f * a.sp + sk;
+    a.wxs[k] = WX[yy][xl];
+    if (a.nop == 2) a.wys[k] = WY[yy][xl];
+    if (!a.lat) {  // (the latency mode's level launch keeps du, dv in LDS)
+      a.du[k] = 0.0f;
+      if (a.nop == 2) a.dv[k] = 0.0f;
+    }
+#pragma unroll
+    for (int ch = 0; ch < NOC; ++ch) {
+      const float(&D)[H2][W2] = DT[ch];
+      const float(&X)[H2][W2] = IX[ch];
+      const float(&Y)[H2][W2] = IY[ch];
+      const long q = ((long)f * NOC + ch) * a.sp + sk;
+      a.Iz[q] = D[iy][ix];
+      a.Ix[q] = X[iy][ix];
+      a.Iy[q] = Y[iy][ix];
+      a.Ixz[q] = kK5[0] * D[iy][ix - 2] + ((kK5[1] * D[iy][ix - 1] + kK5[2] * D[iy][ix]) +
+                                          (kK5[3] * D[iy][ix + 1] + kK5[4] * D[iy][ix + 2]));
+      a.Iyz[q] = kK5[0] * D[iy - 2][ix] + ((kK5[1] * D[iy - 1][ix] + kK5[2] * D[iy][ix]) +
+                                          (kK5[3] * D[iy + 1][ix] + kK5[4] * D[iy + 2][ix]));
+      a.Ixx[q] = kK5[0] * X[iy][ix - 2] + ((kK5[1] * X[iy][ix - 1] + kK5[2] * X[iy][ix]) +
+                                          (kK5[3] * X[iy][ix + 1] + kK5[4] * X[iy][ix + 2]));
+      a.Ixy[q] = kK5[0] * X[iy - 2][ix] + ((kK5[1] * X[iy - 1][ix] + kK5[2] * X[iy][ix]) +
+                                          (kK5[3] * X[iy + 1][ix] + kK5[4] * X[iy + 2][ix]));
+      a.Iyy[q] = kK5[0] * Y[iy - 2][ix] + ((kK5[1] * Y[iy - 1][ix] + kK5[2] * Y[iy][ix]) +
+                                          (kK5[3] * Y[iy + 1][ix] + kK5[4] * Y[iy + 2][ix]));
+    }
+  }
+}
+
+// The same launch where the system kernel filters the second derivatives itself (smsys_deriv: k_tv_smsys<.., DF> /
+// k_tv_smsys_m<.., DF>), so only t's first derivatives and It are written: t is needed on a 2-pixel halo (not 4),
+// It only at the core (it goes straight to Iz), and every channel is warped in the same pass (the flow, the warp
+// position and the bilinear weights once per position, not once per channel; tv_prep_values_all).  One barrier, no
+// second-derivative tiles: 1360 warped positions per tile instead of 1728 per channel, and 37 KB of LDS (colour) /
+// 13 KB (intensity).  Ix = conv5h(t), Iy = conv5v(t) with the replicate border of the clamped halo: the values of
+// k_tv_prepd's phase B, same bits.
+template <int NOC>
+__global__ __launch_bounds__(256) void k_tv_prepd_df(TvArgs a) {
+  const uint3 xb = xcd_block();
+  constexpr int H2 = kPdH + 4, W2 = kPdW + 4;
+  __shared__ float T[NOC][H2][W2], DT[NOC][kPdH][kPdW], WX[kPdH][kPdW], WY[kPdH][kPdW];
+  const int x0 = xb.x * kPdW, y0 = xb.y * kPdH, f = xb.z;
+  const int w = a.w, h = a.h;
+  // positions in batches of PB per thread with unconditional (index-clamped) loads: PB independent warp chains in
+  // flight instead of one
+  constexpr int NPOS = H2 * W2, NIT = (NPOS + 255) / 256, PB = 3;
+#pragma unroll
+  for (int j0 = 0; j0 < NIT; j0 += PB) {
+    float t[PB][NOC], it[PB][NOC], wx[PB], wy[PB];
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int i = min((int)threadIdx.x + (j0 + j) * 256, NPOS - 1);
+      const int ly = i / W2, lx = i - ly * W2;
+      const int cx = clampi(x0 - 2 + lx, 0, w - 1), cy = clampi(y0 - 2 + ly, 0, h - 1);
+      tv_prep_values_all<NOC>(a, cx, cy, f, t[j], it[j], wx[j], wy[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int i = (int)threadIdx.x + (j0 + j) * 256;
+      if (j0 + j >= NIT || i >= NPOS) break;
+      const int ly = i / W2, lx = i - ly * W2;
+#pragma unroll
+      for (int ch = 0; ch < NOC; ++ch) T[ch][ly][lx] = t[j][ch];
+      const int cxl = lx - 2, cyl = ly - 2;
+      if (cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < kPdH) {
+#pragma unroll
+        for (int ch = 0; ch < NOC; ++ch) DT[ch][cyl][cxl] = it[j][ch];
+        WX[cyl][cxl] = wx[j];
+        WY[cyl][cxl] = wy[j];
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int TD = kPdW + kPdH - 1;
+  for (int i = threadIdx.x; i < TD * kPdH; i += 256) {
+    const int yy = i & (kPdH - 1), dd = i / kPdH, xl = dd - yy;
+    const int x = x0 + xl, y = y0 + yy;
+    if (xl < 0 || xl >= kPdW || x >= w || y >= h) continue;
+    const int tx = xl + 2, ty = yy + 2;
+    const long sk = skw(x, y, h, w, a.wrap), k = (long)f * a.sp + sk;
+    a.wxs[k] = WX[yy][xl];
+    if (a.nop == 2) a.wys[k] = WY[yy][xl];
+    a.du[k] = 0.0f;
+    if (a.nop == 2) a.dv[k] = 0.0f;
+#pragma unroll
+    for (int ch = 0; ch < NOC; ++ch) {
+      const long q = ((long)f * NOC + ch) * a.sp + sk;
+      a.Iz[q] = DT[ch][yy][xl];
+      a.Ix[q] = kK5[0] * T[ch][ty][tx - 2] + ((kK5[1] * T[ch][ty][tx - 1] + kK5[2] * T[ch][ty][tx]) +
+                                             (kK5[3] * T[ch][ty][tx + 1] + kK5[4] * T[ch][ty][tx + 2]));
+      a.Iy[q] = kK5[0] * T[ch][ty - 2][tx] + ((kK5[1] * T[ch][ty - 1][tx] + kK5[2] * T[ch][ty][tx]) +
+                                             (kK5[3] * T[ch][ty + 1][tx] + kK5[4] * T[ch][ty + 2][tx]));
     }
   }
 }
@@ -4848,8 +5003,13 @@ void warm_kernels_module(hipStream_t s) { k_warm_kernels<<<1, 64, 0, s>>>(nullpt
 bool tv_prepd_ok(const TvArgs &a) { return a.prepd && (a.noc == 1 || a.prepd == 2); }
 void launch_tv_prepd(const TvArgs &a, hipStream_t s) {
   const dim3 grid(ceil_div(a.w, kPdW), ceil_div(a.h, kPdH), a.n);
+  if (a.smsys_deriv && !a.lat && a.prepd_df) {  // tv_deriv_fused(): Ix, Iy, Iz only
+    if (a.noc == 1) k_tv_prepd_df<1><<<grid, 256, 0, s>>>(a);
+    else k_tv_prepd_df<3><<<grid, 256, 0, s>>>(a);
+    return;
+  }
   if (a.noc == 1) k_tv_prepd<1><<<grid, 256, 0, s>>>(a);
-  else k_tv_prepd<3><<<grid, 256, 0, s>>>(a);
+  else k_tv_prepd_c3<<<grid, 256, 0, s>>>(a);
 }
 void launch_tv_deriv1(const TvArgs &a, hipStream_t s) {
   k_tv_deriv1<<<dim3(ceil_div(a.sp, 256), a.n * a.noc), 256, 0, s>>>(a);
@@ -4866,6 +5026,11 @@ void launch_tv_smooth(const TvArgs &a, hipStream_t s) {
 // The fused form stages RB + 4 rows for RB computed ones: below RB = 4 (h > 256) the halo re-reads cost
 // more than the smoothness round trip saves (config E, h = 544 / 272: 518 vs 299 us per launch).
 // Tall levels take the 2-D tiled form (k_tv_smsys2d) unless a.smsys2d = 0 (A/B: two launches there).
+// The register march for a level: tall levels (no row block fits).  (Colour levels of 135 rows on the march too: prep
+// -0.50 ms, system +0.62 ms per config-C step, r06_s13: not taken.)
+static bool smsys_use_march(const TvArgs &a) {
+  return a.smsys_march && !(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024);
+}
 bool tv_smsys_ok(const TvArgs &a) {
   return a.smsys && ((smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) || a.smsys2d || a.smsys_march);
 }
@@ -4875,14 +5040,15 @@ bool tv_smsys_ok(const TvArgs &a) {
 // block would then stage 5-6 rows of seven planes for 1-2 computed ones, 3-5x redundant staging.
 bool tv_deriv_fused(const TvArgs &a) {
   if (!(a.smsys_deriv && tv_prepd_ok(a) && a.smsys)) return false;
-  if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) return a.smsys_march != 0;  // the march filters them too
+  if (smsys_use_march(a)) return true;  // the march filters them too
+  if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024)) return false;
   if (a.noc != 1) return false;  // colour images: the march only (a row block would stage 9 derivative planes)
   int rb = smsys_rb_n(a.h, smsys_rows(a.w, a.h, a.wrap), a.n, a.smsys_small);
   while (rb > 1 && smsys_lds_df(a.h, rb, true) > kSmsysDfCap) --rb;
   return rb >= 3;
 }
 void launch_tv_smsys(const TvArgs &a, hipStream_t s) {
-  if (!(smsys_rb(a.h) >= 4 && smsys_lds(a.h) <= 64 * 1024) && a.smsys_march) {
+  if (smsys_use_march(a)) {
     const long waves = (long)a.n * march_segments(smsys_rows(a.w, a.h, a.wrap)) * march_strips(a.h);
     const unsigned grid = ceil_div(waves, 4);
     if (a.smsys_deriv) {  // tv_deriv_fused(): k_tv_prepd wrote Ix, Iy, Iz only

@@ -95,6 +95,7 @@ struct ofdis_context {
   int opt_smsys_march = 1;     // tall levels: smoothness + system as a register march (k_tv_smsys_m)
   int opt_smsys_prefetch = 1;  // fused smoothness + system (gray): derivative images issued before the staging
   int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
+  int opt_prepd_df = 1;        // smsys_deriv levels: k_tv_prepd_df (Ix, Iy, Iz from a 2-pixel halo, channels in one pass)
   int opt_smsys_deriv = 1;     // fused smoothness + system (gray; colour: the march): second derivatives filtered from Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
   int call_lanes = 1;          // streams the current call's chunks run on (auto options)
@@ -519,6 +520,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
       tv.smsys_prefetch = c->opt_smsys_prefetch;
       tv.smsys_small = c->opt_smsys_small;
       tv.smsys_deriv = c->opt_smsys_deriv;
+      tv.prepd_df = c->opt_prepd_df;
       tv.sor_redblack = c->opt_sor_mode == 1;
       tv.sor_point = p->omp_build && nop == 2;  // refine_variational.cpp:202-203
       tv.prepd = c->opt_prepd;
@@ -1194,6 +1196,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_prefetch", &ofdis_context::opt_smsys_prefetch, 0, 1},
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
+      {"prepd_df", &ofdis_context::opt_prepd_df, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},

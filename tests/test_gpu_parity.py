@@ -121,6 +121,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("smsys_prefetch", 0, 1),  # fused smoothness + system: derivative images loaded in phase 2
     ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)
     ("smsys_deriv", 0, 1),     # fused launch reads all eight derivative planes (prepd writes them)
+    ("prepd_df", 0, 1),        # smsys_deriv levels: k_tv_prepd (4-pixel halo, per channel) writes Ix, Iy, Iz
     ("smsys_march", 0, 1),     # tall levels: the 2-D tiled fused launch (smsys2d auto: on below 512 pairs)
     (("smsys_march", "smsys2d"), (0, 0), (1, 2)),  # tall levels: two launches (smoothness, then system)
     ("prepd", 0, 2),           # prep and the derivative filters as three launches (t, It, Ix, Iy through memory)
