@@ -543,6 +543,21 @@ def main():
         torch.cuda.synchronize(dev)
         t32 = time.perf_counter() - t0s
         rb_out = out[:min(nd, n32)].cpu().numpy()
+        # strong-scaling configs (D): the same mode on the whole job's batch on this one GPU, so the 1 -> 8 projection
+        # can be read against either N = 1 figure (the exact path's `value`, or this mode's own full-batch rate)
+        full_rb = None
+        if scaling == "strong" and world == 1 and B > n32:
+            ctx.set_option("streams", args.streams)
+            ctx.set_option("chunk", args.chunk)
+            step()
+            torch.cuda.synchronize(dev)
+            t0s = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize(dev)
+            tf = time.perf_counter() - t0s
+            rf = W * H * B * args.steps / tf / 1e6
+            full_rb = {"pairs_per_call": B, "mpix_s": round(rf, 2), "ms_per_step": round(tf / args.steps * 1e3, 3)}
         ctx.set_option("sor_mode", 0)
         ctx.set_option("streams", args.streams)
         ctx.set_option("chunk", args.chunk)
@@ -551,6 +566,12 @@ def main():
                         "shard_32": {"pairs_per_call": n32, "mpix_s_per_gpu": round(r32, 2),
                                      "ms_per_call": round(t32 / args.steps * 1e3, 3)},
                         "exact_single_pair_device_ms_median": latency["device_ms_median"] if latency else None}
+        if full_rb is not None:
+            latency_mode["full_batch_1gpu"] = full_rb
+            latency_mode["projected_1to8_efficiency"] = {
+                "vs_exact_value": round(r32 / mpix, 3), "vs_same_mode_full_batch": round(r32 / full_rb["mpix_s"], 3),
+                "what": f"the {n32}-pair shard's rate in this mode over the 1-GPU rate of all {B} pairs: the exact "
+                        "path's value, or this mode's own"}
 
     # ---- host-buffer entry point (PCIe-inclusive; never the headline value)
     host_io = None
