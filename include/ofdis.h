@@ -158,13 +158,12 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *   "sor_generic" (0/1): force the generic global-memory SOR wavefront;
  *   "sor_pipe" (0/1):    force the one-wave-per-row-group register pipeline (the default for tall levels)
  *                        instead of the sweep-per-wave SOR;
- *   "sor_cring" (0..4, default 2): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
+ *   "sor_cring" (0..3, default 2): in the sweep-per-wave SOR, sweep 0 loads each pixel's coefficients once and
  *                        hands them to the later sweeps through LDS (solverit <= 3); 2: the LDS ring sized to
- *                        the level's rows (more frames per CU at 3 sweeps), its optical-flow entries 28 instead
- *                        of 32 bytes in launches with more frames than the chip holds where that fits more
- *                        frames per CU, and in such launches the lanes outside the frame load one shared slot
- *                        (fewer fetched lines, one more select per load); 3: always 28-byte entries and that
- *                        select; 4: always 32-byte entries and the select; 1: sized to the workgroup limit;
+ *                        the level's rows (more frames per CU at 3 sweeps), and in launches with more frames than
+ *                        CUs the lanes outside the frame load a slot of their wave's in-frame run (fewer fetched
+ *                        lines, one v_med3 per load); 3: that load form in every launch; 1: sized to the
+ *                        workgroup limit;
  *   "sor_rows2" (0/1, default 1): levels too tall for one row per lane in a 1024-thread workgroup run the
  *                        sweep-per-wave SOR with two rows per lane -- 321..640 rows at 3 sweeps, 513..1024 at
  *                        2 (else the register pipeline);

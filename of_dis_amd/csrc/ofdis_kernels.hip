@@ -4055,7 +4055,7 @@ __device__ __forceinline__ int sor_row2(int d, int lim, int rmax) {
 // the ring), so R = 2 runs levels of up to 640 rows with S <= 3 in 16 waves (E's 544-row level) where R = 1
 // would need 27.  Every per-row ring / coefficient-ring offset is a compile-time multiple of 64 entries.
 // SEL: load form of the lanes outside the frame (see load()).
-template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool CZ = false, bool SEL = false>
+template <int S, int MODE, int SI, int NB, int CRN, int R = 1, bool SEL = false>
 struct SorLane {
   static constexpr bool FIRST = SI == 0, LAST = SI == S - 1;
   static_assert(CRN == 0 || S <= 3, "coefficient ring depth 6 needs S <= 3");
@@ -4091,12 +4091,10 @@ struct SorLane {
   f2v *ring_s;        // [NR][3] this sweep, lane base = entry y + 1 (entry 0 = row -1 stays zero)
   const f2v *ring_p;  // [NR][3] previous sweep
   float *sv_s;        // [NR][3] this sweep's sv (row y's sv at entry y + 1) (CRN = 0)
-  // coefficient ring (CRN > 0), lane base = entry y + 1, slot = diagonal mod 6: [6][CW][CRN] float4.  CZ (MODE 0,
-  // throughput launches): 7 of the pixel's 8 coefficient floats (c0 holds i12 twice) -- cr [6][CRN] (i11, i12, i22,
-  // hr), cr2 [6][CRN] (b1, b2), crv [6][CRN] sv: 28 instead of 32 bytes per entry, one more LDS read per step
+  // coefficient ring (CRN > 0), lane base = entry y + 1, slot = diagonal mod 6: [6][CW][CRN] float4.  (Round 4's
+  // 28-byte entries for throughput launches -- more frames per CU -- were removed in round 6: with the clamped load
+  // form the 32-byte ring runs B's launches 4 % faster and fetches 7 % (A: 30 %) fewer bytes, profiles/r06/s21.)
   float4 *cr;
-  f2v *cr2;
-  float *crv;
   int w, h, y, s, lim, rmax, hplane;
   unsigned yc[R];  // !SEL load slot: row y + 64 r clamped into the frame (lanes past h read row h - 1: in the plane)
   bool border[R], notop[R];
@@ -4175,19 +4173,8 @@ struct SorLane {
         if (FIRST) {
           c0 = B.c0[r];
           c1 = MODE == 0 ? B.c1[r] : B.c0[r];
-          if constexpr (MODE == 0 && CZ) {
-            cr[cs * CRN + 64 * r] = make_float4(c0.x, c0.y, c0.w, c1.z);
-            cr2[cs * CRN + 64 * r] = f2v{c1.x, c1.y};
-            crv[cs * CRN + 64 * r] = c1.w;
-          } else {
-            cr[cs * CW * CRN + 64 * r] = c0;
-            if (MODE == 0) cr[(cs * CW + 1) * CRN + 64 * r] = c1;
-          }
-        } else if constexpr (MODE == 0 && CZ) {
-          const float4 q = cr[cs * CRN + 64 * r];
-          const f2v bq = cr2[cs * CRN + 64 * r];
-          c0 = make_float4(q.x, q.y, q.y, q.z);
-          c1 = make_float4(bq.x, bq.y, q.w, crv[cs * CRN + 64 * r]);
+          cr[cs * CW * CRN + 64 * r] = c0;
+          if (MODE == 0) cr[(cs * CW + 1) * CRN + 64 * r] = c1;
         } else {
           c0 = cr[cs * CW * CRN + 64 * r];
           c1 = MODE == 0 ? cr[(cs * CW + 1) * CRN + 64 * r] : c0;
@@ -4204,11 +4191,11 @@ struct SorLane {
         tsv = dpp_from_prev_lane(pvv[r]);
         if (top_lds) {
           tp = ring_s[r * RO + m1 - 3];
-          tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + 64 * r] : cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w) : sv_s[r * RO + m1 - 3];
+          tsv = CRN > 0 ? cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w : sv_s[r * RO + m1 - 3];
         }
       } else {
         tp = ring_s[r * RO + m1 - 3];
-        tsv = CRN > 0 ? (MODE == 0 && CZ ? crv[ct * CRN - 1 + 64 * r] : cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w) : sv_s[r * RO + m1 - 3];
+        tsv = CRN > 0 ? cr[(ct * CW + CW - 1) * CRN - 1 + 64 * r].w : sv_s[r * RO + m1 - 3];
       }
       f2v nw;
       float vv;
@@ -4305,7 +4292,6 @@ struct SorLane {
 };
 
 constexpr size_t kSorLds = 160 * 1024;  // LDS per workgroup (gfx950: 160 KB per CU)
-constexpr int kCuWaves = 32;             // wave slots per CU (8 per SIMD)
 // Compute units of the current device (hipDeviceProp_t::multiProcessorCount; 256 on MI355X), cached per device.
 static long device_cus() {
   static long cus[64] = {};
@@ -4317,10 +4303,6 @@ static long device_cus() {
   }
   return cus[dev];
 }
-// Frames of the sweep-per-wave SOR one CU holds at once: the LDS limit and the wave-slot limit (waves per frame).
-static long sor_frames_per_cu(size_t lds, int waves) {
-  return std::max(1L, std::min((long)(kSorLds / std::max<size_t>(lds, 1)), (long)(kCuWaves / std::max(waves, 1))));
-}
 // Entries per slot of the coefficient ring: the most rows a workgroup of MAXT threads holds, + 2 halos
 // (a compile-time constant, so every ring offset is an immediate); 0 = no coefficient ring (S > 3).
 __host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
@@ -4328,19 +4310,17 @@ __host__ __device__ constexpr int sor_crn(int S, int MAXT, int R = 1) {
 }
 
 // LDS of the lean SOR: S (u, v) rings of NR = 64 R G + 2 entries x 3 slots of float2, then S sv rings
-// (CRN = 0) or the coefficient ring (16-byte aligned): 6 slots x CRN entries of 28 (OF, cw = 2) / 16 (DE) bytes.
-__host__ __device__ __forceinline__ size_t sor_cring_bytes(int crn, int cw, bool cz = false) {
-  return (size_t)6 * crn * (cw == 2 ? (cz ? 28 : 32) : 16);
-}
-__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1, bool cz = false) {
+// (CRN = 0) or the coefficient ring (16-byte aligned): 6 slots x CRN entries of 32 (OF, cw = 2) / 16 (DE) bytes.
+__host__ __device__ __forceinline__ size_t sor_cring_bytes(int crn, int cw) { return (size_t)6 * crn * (cw == 2 ? 32 : 16); }
+__host__ __device__ __forceinline__ size_t sor_lanes_lds(int S, int h, int crn, int cw, int R = 1) {
   const size_t nr = (size_t)((h + 64 * R - 1) / (64 * R)) * 64 * R + 2;
   const size_t uv = sizeof(float) * 2 * 3 * (size_t)S * nr;
   if (crn == 0) return uv + sizeof(float) * 3 * (size_t)S * nr;
-  return (uv + 15) / 16 * 16 + sor_cring_bytes(crn, cw, cz);
+  return (uv + 15) / 16 * 16 + sor_cring_bytes(crn, cw);
 }
 
 // One frame's SOR call, lean form: 64 * G * S threads, R rows per lane.
-template <int S, int MODE, int NB, int CRN, int R, bool CZ = false, bool SEL = false>
+template <int S, int MODE, int NB, int CRN, int R, bool SEL = false>
 __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v *ring) {
   constexpr int CW = MODE == 0 ? 2 : 1;
   const int G = (a.h + 64 * R - 1) / (64 * R);
@@ -4349,16 +4329,14 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
   const int g = wid / S, s = wid - g * S;
   float *svr = reinterpret_cast<float *>(ring + S * 3 * NR);
   char *crb = reinterpret_cast<char *>(ring) + (sizeof(f2v) * S * 3 * NR + 15) / 16 * 16;
-  float4 *crr = reinterpret_cast<float4 *>(crb);                // [6][CRN] float4
-  f2v *cr2r = reinterpret_cast<f2v *>(crb + 16 * 6 * CRN);      // MODE 0: [6][CRN] float2
-  float *crvr = reinterpret_cast<float *>(crb + 24 * 6 * CRN);  // MODE 0: [6][CRN] float
+  float4 *crr = reinterpret_cast<float4 *>(crb);  // [6][CW][CRN] float4
   for (int i = threadIdx.x; i < S * 3 * NR; i += blockDim.x) {
     ring[i] = f2v{0.f, 0.f};
     if (CRN == 0) svr[i] = 0.0f;
   }
   if (CRN > 0) {
     float *z = reinterpret_cast<float *>(crb);
-    for (int i = threadIdx.x; i < (int)(sor_cring_bytes(CRN, CW, CZ) / 4); i += blockDim.x) z[i] = 0.0f;
+    for (int i = threadIdx.x; i < (int)(sor_cring_bytes(CRN, CW) / 4); i += blockDim.x) z[i] = 0.0f;
   }
   __syncthreads();
 #ifdef OFDIS_SOR_PROBE
@@ -4381,8 +4359,6 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.ring_p = ring + ((s > 0 ? s - 1 : 0) * NR + y + 1) * 3;
     st.sv_s = svr + (s * NR + y + 1) * 3;
     st.cr = crr + y + 1;
-    st.cr2 = cr2r + y + 1;
-    st.crv = crvr + y + 1;
     st.w = a.w; st.h = a.h; st.y = y; st.s = s;  // s == SI
     st.lim = a.wrap ? a.w : 1 << 30;
     st.rmax = a.wrap ? a.w - 1 : a.w + a.h - 2;
@@ -4403,28 +4379,28 @@ __device__ __forceinline__ void sor_lanes_frame(const TvArgs &a, int frame, f2v 
     st.run(T, y0, ymax);
   };
   if (s == 0) {
-    SorLane<S, MODE, 0, NB, CRN, R, CZ, SEL> st;
+    SorLane<S, MODE, 0, NB, CRN, R, SEL> st;
     setup(st);
   } else if (s == 1) {
-    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, CZ, SEL> st;
+    SorLane<S, MODE, (S > 1 ? 1 : 0), NB, CRN, R, SEL> st;
     setup(st);
   } else if (s == 2) {
-    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, CZ, SEL> st;
+    SorLane<S, MODE, (S > 2 ? 2 : 0), NB, CRN, R, SEL> st;
     setup(st);
   } else {
-    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, CZ, SEL> st;
+    SorLane<S, MODE, (S > 3 ? 3 : 0), NB, CRN, R, SEL> st;
     setup(st);
   }
 }
 
 // CG > 0: the coefficient ring holds exactly the CG row groups of the level (+ 2 halos) instead of the most a
 // workgroup of MAXT threads can hold -- less LDS per frame, more frames per CU.
-template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool CZ = false, bool SEL = false>
+template <int S, int MODE, int NB, int MAXT, bool CRING, int R = 1, int CG = 0, bool SEL = false>
 __global__ __launch_bounds__(MAXT) void k_tv_sor_lanes(TvArgs a) {
   extern __shared__ f2v ring_uv[];  // [S][NR][3], then the sv rings or the coefficient ring
   constexpr int crn = !CRING ? 0 : CG > 0 ? 64 * R * CG + 2 : sor_crn(S, MAXT, R);
   static_assert(CG == 0 || CG * 64 * S <= MAXT, "row groups of the workgroup");
-  sor_lanes_frame<S, MODE, NB, crn, R, CZ, SEL>(a, blockIdx.x, ring_uv);
+  sor_lanes_frame<S, MODE, NB, crn, R, SEL>(a, blockIdx.x, ring_uv);
 }
 
 template <int TH>
@@ -5150,31 +5126,20 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
   const int th = 64 * G * S;
   if constexpr (S == 3 && R == 1) {
     if (cring && a.sor_cring >= 2) {  // the ring sized to the level's G row groups
-      // OF launches with more frames than the chip holds at once: the 28-byte ring entries where they let more
-      // frames share a CU (throughput); else the 32-byte entries (one LDS read less on the step's critical path).
-      // Frames per CU: the lesser of the LDS and the wave-slot limits (G S waves per frame), CUs of the device.
-      const size_t ld32 = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R), ld28 = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R, true);
-      const long cus = device_cus(), f32 = sor_frames_per_cu(ld32, G * S), f28 = sor_frames_per_cu(ld28, G * S);
-      const bool cz = a.nop == 2 && (a.sor_cring == 3 || (a.sor_cring != 4 && f28 > f32 && (long)a.n > f32 * cus));
-      const size_t ldsg = cz ? ld28 : ld32;
+      const size_t ldsg = sor_lanes_lds(S, a.h, 64 * G + 2, cw, R);
       // the clamped in-frame load form in throughput launches -- more frames than CUs -- and the lane-constant slots in
-      // latency launches, where the per-step v_med3 would sit on the wavefront's critical path (sor_cring 3 / 4:
-      // everywhere, parity).  Measured (profiles/r06/s5): B's tv_sor 111-113 us per 2048-pair launch either way, its
-      // counted bytes 1.36x -> 1.27x the compulsory ones; the single pair 0.84 -> 0.91 ms with it everywhere.
-      const bool sel = a.sor_cring >= 3 || (long)a.n > cus;
+      // latency launches, where the per-step v_med3 would sit on the wavefront's critical path (sor_cring 3: everywhere,
+      // parity).  Measured (profiles/r06/s5, s21): B's tv_sor 4.16 -> 4.00 ms per step and its counted bytes 1.33x ->
+      // 1.23x the compulsory ones, A's 1.82x -> 1.27x; the single pair 0.84 -> 0.91 ms with it everywhere.
+      const bool sel = a.sor_cring >= 3 || (long)a.n > device_cus();
       auto go = [&](auto gc) {
         constexpr int CG = decltype(gc)::value;
         if (a.nop == 2) {
-          if (cz) {
-            if (sel) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true, true><<<a.n, th, ldsg, s>>>(a);
-            else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true, false><<<a.n, th, ldsg, s>>>(a);
-          } else {
-            if (sel) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, false, true><<<a.n, th, ldsg, s>>>(a);
-            else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, false, false><<<a.n, th, ldsg, s>>>(a);
-          }
+          if (sel) k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, true><<<a.n, th, ldsg, s>>>(a);
+          else k_tv_sor_lanes<S, 0, 3, MAXT, true, R, CG, false><<<a.n, th, ldsg, s>>>(a);
         } else {
-          if (sel) k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG, false, true><<<a.n, th, ldsg, s>>>(a);
-          else k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG, false, false><<<a.n, th, ldsg, s>>>(a);
+          if (sel) k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG, true><<<a.n, th, ldsg, s>>>(a);
+          else k_tv_sor_lanes<S, 2, 3, MAXT, true, R, CG, false><<<a.n, th, ldsg, s>>>(a);
         }
       };
       if constexpr (MAXT == 512) {
@@ -5191,8 +5156,8 @@ static void sor_lanes(const TvArgs &a, hipStream_t s) {
   const bool sel = a.sor_cring >= 3 || (long)a.n > device_cus();
   auto go2 = [&](auto cr, auto sl) {
     constexpr bool CR = decltype(cr)::value, SL = decltype(sl)::value;
-    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, CR, R, 0, false, SL><<<a.n, th, lds, s>>>(a);
-    else k_tv_sor_lanes<S, 2, 3, MAXT, CR, R, 0, false, SL><<<a.n, th, lds, s>>>(a);
+    if (a.nop == 2) k_tv_sor_lanes<S, 0, 3, MAXT, CR, R, 0, SL><<<a.n, th, lds, s>>>(a);
+    else k_tv_sor_lanes<S, 2, 3, MAXT, CR, R, 0, SL><<<a.n, th, lds, s>>>(a);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;

@@ -100,10 +100,8 @@ struct ofdis_context {
   int call_frames = 1;         // pairs of the current call (auto options)
   int call_lanes = 1;          // streams the current call's chunks run on (auto options)
   int opt_sor_cring = 2;       // sweep-per-wave SOR: coefficient ring in LDS (0: every sweep loads its coefficients;
-                               // 2: ring sized to the level's row groups (28-byte OF entries in throughput
-                               // launches where they fit more frames per CU; the in-frame load select in launches
-                               // that oversubscribe the chip), 3: always 28-byte + select, 4: always 32-byte +
-                               // select, 1: workgroup limit)
+                               // 2: ring sized to the level's row groups, the clamped in-frame load form in launches
+                               // that oversubscribe the chip; 3: that load form in every launch; 1: workgroup limit)
   int opt_prepd = 2;           // prep + derivatives in one launch: 1 intensity images, 2 colour images too (0: three launches)
   int opt_sor_rows2 = 1;       // sweep-per-wave SOR with two rows per lane for 321..640-row levels (0: pipeline)
   int opt_wave_per_patch = 0;  // 1: one wave per patch instead of eight lanes (A/B)
@@ -1191,7 +1189,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
   static const Opt opts[] = {
       {"sor_generic", &ofdis_context::opt_sor_generic, 0, 1},
       {"sor_pipe", &ofdis_context::opt_sor_pipe, 0, 1},     {"smsys", &ofdis_context::opt_smsys, 0, 1},
-      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 4},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
+      {"sor_cring", &ofdis_context::opt_sor_cring, 0, 3},   {"smsys2d", &ofdis_context::opt_smsys2d, 0, 2},
       {"smsys_march", &ofdis_context::opt_smsys_march, 0, 1},
       {"smsys_prefetch", &ofdis_context::opt_smsys_prefetch, 0, 1},
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},

@@ -114,8 +114,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("wave_per_patch", 1, 0),  # one wave per DIS patch instead of eight lanes
     ("sor_cring", 0, 2),       # sweep-per-wave SOR without the LDS coefficient ring
     ("sor_cring", 1, 2),       # the coefficient ring sized to the workgroup limit instead of the level
-    ("sor_cring", 3, 2),       # 28-byte optical-flow ring entries (the throughput launches' form) on every launch
-    ("sor_cring", 4, 2),       # 32-byte entries with the in-frame load select (the oversubscribed launches' loads)
+    ("sor_cring", 3, 2),       # the clamped in-frame load form (the oversubscribed launches' loads) on every launch
     ("smsys", 0, 1),           # smoothness and system as two launches (s through memory)
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
     ("smsys_prefetch", 0, 1),  # fused smoothness + system: derivative images loaded in phase 2
