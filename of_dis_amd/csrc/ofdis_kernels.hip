@@ -2916,35 +2916,36 @@ __global__ __launch_bounds__(256) void k_tv_prepd_c3(TvArgs a) {
 // second-derivative tiles: 1360 warped positions per tile instead of 1728 per channel, and 37 KB of LDS (colour) /
 // 13 KB (intensity).  Ix = conv5h(t), Iy = conv5v(t) with the replicate border of the clamped halo: the values of
 // k_tv_prepd's phase B, same bits.
-template <int NOC>
-__global__ __launch_bounds__(256) void k_tv_prepd_df(TvArgs a) {
+template <int NOC, int TH = kPdH>
+__global__ __launch_bounds__(16 * TH) void k_tv_prepd_df(TvArgs a) {
+  constexpr int NT = 16 * TH;  // threads: 16 per tile row
   const uint3 xb = xcd_block();
-  constexpr int H2 = kPdH + 4, W2 = kPdW + 4;
-  __shared__ float T[NOC][H2][W2], DT[NOC][kPdH][kPdW], WX[kPdH][kPdW], WY[kPdH][kPdW];
-  const int x0 = xb.x * kPdW, y0 = xb.y * kPdH, f = xb.z;
+  constexpr int H2 = TH + 4, W2 = kPdW + 4;
+  __shared__ float T[NOC][H2][W2], DT[NOC][TH][kPdW], WX[TH][kPdW], WY[TH][kPdW];
+  const int x0 = xb.x * kPdW, y0 = xb.y * TH, f = xb.z;
   const int w = a.w, h = a.h;
   // positions in batches of PB per thread with unconditional (index-clamped) loads: PB independent warp chains in
   // flight instead of one
-  constexpr int NPOS = H2 * W2, NIT = (NPOS + 255) / 256, PB = 3;
+  constexpr int NPOS = H2 * W2, NIT = (NPOS + NT - 1) / NT, PB = 3;
 #pragma unroll
   for (int j0 = 0; j0 < NIT; j0 += PB) {
     float t[PB][NOC], it[PB][NOC], wx[PB], wy[PB];
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
-      const int i = min((int)threadIdx.x + (j0 + j) * 256, NPOS - 1);
+      const int i = min((int)threadIdx.x + (j0 + j) * NT, NPOS - 1);
       const int ly = i / W2, lx = i - ly * W2;
       const int cx = clampi(x0 - 2 + lx, 0, w - 1), cy = clampi(y0 - 2 + ly, 0, h - 1);
       tv_prep_values_all<NOC>(a, cx, cy, f, t[j], it[j], wx[j], wy[j]);
     }
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
-      const int i = (int)threadIdx.x + (j0 + j) * 256;
+      const int i = (int)threadIdx.x + (j0 + j) * NT;
       if (j0 + j >= NIT || i >= NPOS) break;
       const int ly = i / W2, lx = i - ly * W2;
 #pragma unroll
       for (int ch = 0; ch < NOC; ++ch) T[ch][ly][lx] = t[j][ch];
       const int cxl = lx - 2, cyl = ly - 2;
-      if (cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < kPdH) {
+      if (cxl >= 0 && cxl < kPdW && cyl >= 0 && cyl < TH) {
 #pragma unroll
         for (int ch = 0; ch < NOC; ++ch) DT[ch][cyl][cxl] = it[j][ch];
         WX[cyl][cxl] = wx[j];
@@ -2953,9 +2954,9 @@ __global__ __launch_bounds__(256) void k_tv_prepd_df(TvArgs a) {
     }
   }
   __syncthreads();
-  constexpr int TD = kPdW + kPdH - 1;
-  for (int i = threadIdx.x; i < TD * kPdH; i += 256) {
-    const int yy = i & (kPdH - 1), dd = i / kPdH, xl = dd - yy;
+  constexpr int TD = kPdW + TH - 1;
+  for (int i = threadIdx.x; i < TD * TH; i += NT) {
+    const int yy = i & (TH - 1), dd = i / TH, xl = dd - yy;
     const int x = x0 + xl, y = y0 + yy;
     if (xl < 0 || xl >= kPdW || x >= w || y >= h) continue;
     const int tx = xl + 2, ty = yy + 2;
@@ -4980,7 +4981,14 @@ bool tv_prepd_ok(const TvArgs &a) { return a.prepd && (a.noc == 1 || a.prepd == 
 void launch_tv_prepd(const TvArgs &a, hipStream_t s) {
   const dim3 grid(ceil_div(a.w, kPdW), ceil_div(a.h, kPdH), a.n);
   if (a.smsys_deriv && !a.lat && a.prepd_df) {  // tv_deriv_fused(): Ix, Iy, Iz only
-    if (a.noc == 1) k_tv_prepd_df<1><<<grid, 256, 0, s>>>(a);
+    // tall levels (the march's, h >= 256) on 64 x 32 tiles, 512 threads: halo 1.33x -> 1.2x the core, the same
+    // occupancy; config E's prep 3.06 -> 2.61 ms per step, C's 3.16 -> 3.04 (profiles/r06/s29); short levels keep
+    // 16 rows (B's 68-row levels would compute 96)
+    if (a.h >= 256) {
+      const dim3 g32(ceil_div(a.w, kPdW), ceil_div(a.h, 32), a.n);
+      if (a.noc == 1) k_tv_prepd_df<1, 32><<<g32, 512, 0, s>>>(a);
+      else k_tv_prepd_df<3, 32><<<g32, 512, 0, s>>>(a);
+    } else if (a.noc == 1) k_tv_prepd_df<1><<<grid, 256, 0, s>>>(a);
     else k_tv_prepd_df<3><<<grid, 256, 0, s>>>(a);
     return;
   }
