@@ -2831,7 +2831,7 @@ __global__ __launch_bounds__(256) void k_tv_prepd_c3(TvArgs a) {
   __shared__ float T[NOC][H4][W4], DT[NOC][H2][W2], IX[NOC][H2][W2], IY[NOC][H2][W2], WX[kPdH][kPdW], WY[kPdH][kPdW];
   const int x0 = xb.x * kPdW, y0 = xb.y * kPdH, f = xb.z;
   const int w = a.w, h = a.h;
-  constexpr int NPOS = H4 * W4, NIT = (NPOS + 255) / 256, PB = 2;
+  constexpr int NPOS = H4 * W4, NIT = (NPOS + 255) / 256, PB = 4;
 #pragma unroll
   for (int j0 = 0; j0 < NIT; j0 += PB) {
     float t[PB][NOC], it[PB][NOC], wx[PB], wy[PB];
@@ -2926,7 +2926,7 @@ __global__ __launch_bounds__(16 * TH) void k_tv_prepd_df(TvArgs a) {
   const int w = a.w, h = a.h;
   // positions in batches of PB per thread with unconditional (index-clamped) loads: PB independent warp chains in
   // flight instead of one
-  constexpr int NPOS = H2 * W2, NIT = (NPOS + NT - 1) / NT, PB = 3;
+  constexpr int NPOS = H2 * W2, NIT = (NPOS + NT - 1) / NT, PB = TH >= 32 && NOC == 3 ? 5 : 3;
 #pragma unroll
   for (int j0 = 0; j0 < NIT; j0 += PB) {
     float t[PB][NOC], it[PB][NOC], wx[PB], wy[PB];
