@@ -2913,9 +2913,9 @@ __global__ __launch_bounds__(256) void k_tv_prepd_c3(TvArgs a) {
 // k_tv_smsys_m<.., DF>), so only t's first derivatives and It are written: t is needed on a 2-pixel halo (not 4),
 // It only at the core (it goes straight to Iz), and every channel is warped in the same pass (the flow, the warp
 // position and the bilinear weights once per position, not once per channel; tv_prep_values_all).  One barrier, no
-// second-derivative tiles: 1360 warped positions per tile instead of 1728 per channel, and 37 KB of LDS (colour) /
-// 13 KB (intensity).  Ix = conv5h(t), Iy = conv5v(t) with the replicate border of the clamped halo: the values of
-// k_tv_prepd's phase B, same bits.
+// second-derivative tiles: 1360 warped positions per 64 x 16 tile instead of 1728 per channel, and 37 KB of LDS
+// (colour) / 18 KB (intensity); TH = 32 (levels of 256+ rows, 512 threads): 70 / 34 KB.  Ix = conv5h(t), Iy =
+// conv5v(t) with the replicate border of the clamped halo: the values of k_tv_prepd's phase B, same bits.
 template <int NOC, int TH = kPdH>
 __global__ __launch_bounds__(16 * TH) void k_tv_prepd_df(TvArgs a) {
   constexpr int NT = 16 * TH;  // threads: 16 per tile row
