@@ -91,6 +91,7 @@ struct AggArgs {
   int n, nop, noc, p, novals, steps;
   int absw;     // 1: pweight holds the patch kernel's aggregation weights as slot planes ([n][A * A][h][w]), 0: loss weights
   int aslots;   // A
+  int stage;    // k_aggregate: the tile's patch displacements staged in LDS (option agg_stage)
   LevelGeom g;
 };
 

@@ -95,6 +95,7 @@ struct ofdis_context {
   int opt_smsys_march = 1;     // tall levels: smoothness + system as a register march (k_tv_smsys_m)
   int opt_smsys_prefetch = 1;  // fused smoothness + system (gray): derivative images issued before the staging
   int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
+  int opt_agg_stage = 1;       // k_aggregate: patch displacements of the tile staged in LDS (0: gathered from p_iter)
   int opt_prepd_df = 1;        // smsys_deriv levels: k_tv_prepd_df (Ix, Iy, Iz from a 2-pixel halo, channels in one pass)
   int opt_smsys_deriv = 1;     // fused smoothness + system (gray; colour: the march): second derivatives filtered from Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
@@ -457,6 +458,7 @@ int run_levels(ofdis_context *c, char *ws, const Plan &P, const ofdis_params *p,
     ag.novals = novals;
     ag.absw = absw;
     ag.aslots = pa.aslots;
+    ag.stage = c->opt_agg_stage;
     ag.steps = steps;
     ag.g = g;
     ag.cg_p_iter = P.fb ? pb.p_iter : nullptr;
@@ -1195,6 +1197,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"prepd_df", &ofdis_context::opt_prepd_df, 0, 1},
+      {"agg_stage", &ofdis_context::opt_agg_stage, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},
       {"wave_per_patch", &ofdis_context::opt_wave_per_patch, 0, 1},
       {"nt_store", &ofdis_context::opt_nt_store, 0, 1},     {"up_form", &ofdis_context::opt_up_form, 0, 3},
