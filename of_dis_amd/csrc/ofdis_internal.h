@@ -51,6 +51,7 @@ struct PyrPadGradArgs {
   const float *lvl;        // unpadded [2n][h][w][noc]
   float *img, *dx, *dy;    // padded [2n][H][W][noc]
   int n2, w, h, noc, pad;
+  int per_value;           // colour: one thread per value (k_pyr_pad_grad_v; option pad_grad_v)
 };
 
 struct PatchArgs {

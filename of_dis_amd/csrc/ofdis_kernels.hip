@@ -232,6 +232,41 @@ __global__ __launch_bounds__(256) void k_pyr_pad_grad(PyrPadGradArgs a) {
   }
 }
 
+// Colour images: one thread per output VALUE over the flattened [2n][H][W * NOC] range (the loop above runs the
+// channels inside a thread: three stride-3 store instructions per array and pixel), the same expressions.  Config
+// C: 4.70 -> 3.49 ms per step (profiles/r06/s35).
+template <int NOC>
+__global__ __launch_bounds__(256) void k_pyr_pad_grad_v(PyrPadGradArgs a) {
+  const int W = a.w + 2 * a.pad, H = a.h + 2 * a.pad, RW = W * NOC;
+  const long total = (long)a.n2 * H * RW;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long r = t / RW;
+    const int xc = (int)(t - r * RW), Y = (int)(r % H), f = (int)(r / H);
+    const int X = xc / NOC, c = xc - X * NOC;
+    const int sx = X - a.pad, sy = Y - a.pad;
+    const int w = a.w;
+    const float *L = a.lvl + (long)f * a.h * a.w * NOC;
+    if (sx >= 0 && sx < a.w && sy >= 0 && sy < a.h) {
+      const int xm = reflect101(sx - 1, a.w), xp = reflect101(sx + 1, a.w);
+      const int ym = reflect101(sy - 1, a.h), yp = reflect101(sy + 1, a.h);
+#define PX(xx, yy) L[((yy) * w + (xx)) * NOC + c]
+      const float tm = PX(xp, ym) - PX(xm, ym);
+      const float t0 = PX(xp, sy) - PX(xm, sy);
+      const float tp = PX(xp, yp) - PX(xm, yp);
+      const float sm = (PX(xm, ym) + PX(xp, ym)) * 0.125f + PX(sx, ym) * 0.25f;
+      const float sp = (PX(xm, yp) + PX(xp, yp)) * 0.125f + PX(sx, yp) * 0.25f;
+      a.img[t] = PX(sx, sy);
+      a.dx[t] = (tm + tp) * 0.125f + t0 * 0.25f;
+      a.dy[t] = sp - sm;
+#undef PX
+    } else {
+      a.img[t] = L[(clampi(sy, 0, a.h - 1) * w + clampi(sx, 0, a.w - 1)) * NOC + c];
+      a.dx[t] = 0.0f;
+      a.dy[t] = 0.0f;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ DIS patches
 
 constexpr int kPatchWaves = 4;
@@ -4856,6 +4891,11 @@ void launch_pyr_down(const PyrDownArgs &a, hipStream_t s) {
   k_pyr_down<<<std::min(ceil_div((long)a.n2 * a.h * a.w * a.noc, 256), 1u << 22), 256, 0, s>>>(a);  // grid-stride beyond
 }
 void launch_pyr_pad_grad(const PyrPadGradArgs &a, hipStream_t s) {
+  if (a.noc == 3 && a.per_value) {
+    k_pyr_pad_grad_v<3><<<std::min(ceil_div((long)a.n2 * (a.h + 2 * a.pad) * (a.w + 2 * a.pad) * 3, 256), 1u << 22),
+                          256, 0, s>>>(a);
+    return;
+  }
   k_pyr_pad_grad<<<std::min(ceil_div((long)a.n2 * (a.h + 2 * a.pad) * (a.w + 2 * a.pad), 256), 1u << 22), 256, 0,
                    s>>>(a);  // grid-stride beyond 2^22 workgroups
 }
