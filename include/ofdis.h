@@ -178,6 +178,8 @@ int ofdis_context_set_stage_capture(ofdis_context *ctx, float *const *dis_flow, 
  *                        or the register march (taller levels, intensity and colour images) run, the system kernel
  *                        filters Ixx, Ixy, Iyy, Ixz, Iyz from Ix, Iy, Iz and the prep launch does not write those
  *                        five planes (per channel);
+ *   "pyr_rgb" (0/1, default 1): colour images, pyramid base levels 2..4: dword loads and per-channel masked byte
+ *                        sums (v_sad_u8) instead of the byte loop;
  *   "pad_grad_v" (0/1, default 1): colour images: the pyramid's pad + Sobel launch runs one thread per value
  *                        (0: one per pixel, the channels inside the thread);
  *   "agg_stage" (0/1, default 1): the aggregation stages the displacements of the patches covering each 64 x 16

@@ -30,6 +30,7 @@ struct PyrBaseArgs {
   int log2s;                     // level of the output (sc_l)
   int w, h;                      // output level size
   float *out;                    // unpadded level [2n][h][w][noc]
+  int rgb_sad;                   // colour, 2^l = 4..16: k_pyr_base_rgb (option pyr_rgb)
 };
 
 // SELECTCHANNEL 2 (run_dense.cpp:139-148): level 0 = Sobel gradient magnitude of the divisibility-padded

@@ -97,6 +97,7 @@ struct ofdis_context {
   int opt_smsys_small = 1;     // fused smoothness + system: small row blocks for launches that cannot fill the chip
   int opt_agg_stage = 1;       // k_aggregate: patch displacements of the tile staged in LDS (0: gathered from p_iter)
   int opt_pad_grad_v = 1;      // colour pyramid pad + gradients: one thread per value (0: per pixel, channels inside)
+  int opt_pyr_rgb = 1;         // colour pyramid base by dword loads and masked v_sad_u8 (0: the byte loop)
   int opt_prepd_df = 1;        // smsys_deriv levels: k_tv_prepd_df (Ix, Iy, Iz from a 2-pixel halo, channels in one pass)
   int opt_smsys_deriv = 1;     // fused smoothness + system (gray; colour: the march): second derivatives filtered from Ix, Iy, Iz
   int call_frames = 1;         // pairs of the current call (auto options)
@@ -673,6 +674,7 @@ int run_pyramid(ofdis_context *c, char *ws, const Plan &P, const uint8_t *a, con
     pb.w = P.lv[0].w;
     pb.h = P.lv[0].h;
     pb.out = (float *)(ws + P.off_lvl[0]);
+    pb.rgb_sad = c->opt_pyr_rgb;
     timed(c, 0, s, [&] { launch_pyr_base(pb, s); });
   }
   for (size_t i = 1; i < P.lv.size(); ++i) {
@@ -1199,6 +1201,7 @@ int ofdis_context_set_option(ofdis_context *c, const char *key, int value) {
       {"smsys_small", &ofdis_context::opt_smsys_small, 0, 1},
       {"smsys_deriv", &ofdis_context::opt_smsys_deriv, 0, 1},
       {"prepd_df", &ofdis_context::opt_prepd_df, 0, 1},
+      {"pyr_rgb", &ofdis_context::opt_pyr_rgb, 0, 1},
       {"pad_grad_v", &ofdis_context::opt_pad_grad_v, 0, 1},
       {"agg_stage", &ofdis_context::opt_agg_stage, 0, 1},
       {"sor_rows2", &ofdis_context::opt_sor_rows2, 0, 1},   {"prepd", &ofdis_context::opt_prepd, 0, 2},

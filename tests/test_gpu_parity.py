@@ -119,6 +119,7 @@ VARIANTS = [  # (option, value, default): non-default kernels
     ("sor_rows2", 0, 1),       # 321..640-row levels on the register pipeline instead of two rows per lane
     ("smsys_prefetch", 0, 1),  # fused smoothness + system: derivative images loaded in phase 2
     ("smsys_small", 0, 1),     # latency regime: the throughput row blocks (4 pixels per thread)
+    ("pyr_rgb", 0, 1),         # colour pyramid base by the byte loop (k_pyr_base) instead of dword loads + SAD
     ("pad_grad_v", 0, 1),      # colour pyramid pad + gradients one thread per pixel (the channels in the thread)
     ("agg_stage", 0, 1),       # aggregation gathering every patch displacement from p_iter (no LDS staging)
     ("smsys_deriv", 0, 1),     # fused launch reads all eight derivative planes (prepd writes them)
